@@ -1,0 +1,87 @@
+// Compute backends.  The engine (engine.hpp) is written once against this
+// interface; two implementations exist:
+//   * HipBackend  - MI355X: hand-written CDNA4 kernels, one HIP stream,
+//                   everything asynchronous (backend_hip.hip, kernels/*.hip).
+//   * CpuBackend  - bit-exact C++ emulation of the same kernels on host
+//                   threads; it replaces the reference's OpenMP loops
+//                   (src/game_openmp.c:34,63,97) and lets the whole engine
+//                   (epochs, halos, lazy termination) be tested without a GPU.
+#pragma once
+
+#include <memory>
+#include <string>
+
+#include "gol/tile.hpp"
+
+namespace gol {
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual std::string name() const = 0;
+  virtual bool is_device() const = 0;
+  virtual int device() const { return -1; }
+  virtual void* stream() const { return nullptr; }  // hipStream_t for HIP
+
+  // Memory.  alloc() returns zeroed memory in the backend's address space.
+  virtual void* alloc(size_t bytes) = 0;
+  virtual void release(void* p) = 0;
+  virtual void* alloc_host(size_t bytes) = 0;  // pinned host staging for HIP
+  virtual void release_host(void* p) = 0;
+  virtual void memset_async(void* p, int v, size_t bytes) = 0;
+  virtual void copy_h2d(void* dst, const void* src, size_t bytes) = 0;        // synchronous
+  virtual void copy_d2h(void* dst, const void* src, size_t bytes) = 0;        // synchronous
+  virtual void copy_d2h_async(void* dst, const void* src, size_t bytes) = 0;  // into pinned
+  virtual void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch,
+                             int64_t width_bytes, int64_t rows) = 0;
+  virtual void synchronize() = 0;
+  // Events: returns an opaque handle recorded on the stream.
+  virtual void* event_record() = 0;
+  virtual void event_wait(void* ev) = 0;  // host blocks until the event completes
+  virtual void event_destroy(void* ev) = 0;
+
+  // Kernels.
+  virtual void run_block(const BlockArgs& a) = 0;
+  // Periodic self-fill of halo regions of a single tile (any tile size):
+  // columns (left/right halo words of owned rows) and/or rows (full padded
+  // rows of the top/bottom halo, which also fills the corners).
+  virtual void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) = 0;
+  // OR of all owned cells -> *flag (device) = 1 if any cell is alive.
+  virtual void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) = 0;
+  // Count of live owned cells (synchronous, for diagnostics/tests).
+  virtual int64_t alive_count(const void* buf, const TileGeom& g) = 0;
+  // Host <-> tile conversion: `cells` is an H x W array of bytes (ld = row
+  // stride); load treats byte == '1' or byte == 1 as alive; store writes
+  // '0'/'1' when ascii else 0/1.
+  virtual void load_owned(void* buf, const TileGeom& g, const uint8_t* cells, int64_t ld) = 0;
+  virtual void store_owned(const void* buf, const TileGeom& g, uint8_t* cells, int64_t ld,
+                           bool ascii) = 0;
+  // Counter-based random init of owned cells from global coordinates, so the
+  // grid is identical for every decomposition and layout.
+  virtual void init_random(void* buf, const TileGeom& g, uint64_t seed, double density,
+                           int64_t grow0, int64_t gcol0) = 0;
+};
+
+std::unique_ptr<Backend> make_cpu_backend(int threads);
+// Defined in backend_hip.hip; throws if no device or the kernels are missing.
+std::unique_ptr<Backend> make_hip_backend(int device);
+bool hip_available();
+
+// Counter-based RNG used by init_random (host and device agree bit-for-bit).
+GOL_HD inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+GOL_HD inline bool rng_cell(uint64_t seed, int64_t row, int64_t col, uint32_t thresh24) {
+  uint64_t k = seed ^ (uint64_t(row) * 0xD1B54A32D192ED03ull) ^ (uint64_t(col) * 0xABC98388FB8FAC03ull);
+  return uint32_t(splitmix64(k) >> 40) < thresh24;
+}
+inline uint32_t density_thresh(double d) {
+  if (d <= 0) return 0;
+  if (d >= 1) return 1u << 24;
+  return uint32_t(d * double(1u << 24) + 0.5);
+}
+
+}  // namespace gol

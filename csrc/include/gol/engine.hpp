@@ -1,0 +1,118 @@
+// The generation engine: one rank's tile, its double buffer, the epoch /
+// temporal-block schedule, halo exchange and lazy exact termination.
+//
+// Reference loops: serial src/game.c:169-196, MPI src/game_mpi.c:385-422,
+// CUDA src/game_cuda.cu:213-276.  All of them test termination every
+// generation (a full scan + MPI_Allreduce, or a kernel + 4-byte D2H copy).
+// Both stop conditions are absorbing: an empty grid stays
+// empty and G_t == G_{t-1} implies G_{t+k} == G_t.  So the kernels record
+// one "changed" flag per generation, the engine polls them every few hundred
+// generations, and the reference's reported generation count is rebuilt
+// exactly from the first unchanged generation g_f:
+//   * grid at g_f empty   -> extinction, reports g_f - 1 (src/game.c:177)
+//   * otherwise, with similarity checks every F gens -> the first check
+//     t >= g_f reports t - 1 (the break skips generation++, src/game.c:186)
+//   * otherwise -> GEN_LIMIT.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gol/backend.hpp"
+#include "gol/decomp.hpp"
+#include "gol/tile.hpp"
+#include "gol/transport.hpp"
+
+namespace gol {
+
+struct EngineConfig {
+  int64_t W = 0, H = 0;            // global grid (cells)
+  Layout layout = Layout::Bits;
+  std::string decomp = "auto";     // "auto" or "PxQ"
+  int64_t gen_limit = 1000;        // GEN_LIMIT (src/game.c:6)
+  bool check_similarity = true;    // CHECK_SIMILARITY (src/game.c:8)
+  int sim_freq = 3;                // SIMILARITY_FREQUENCY (src/game.c:9)
+  int64_t start_gen = 0;           // generation number of the loaded state (resume)
+  int sim_phase = 0;               // similarity counter value at start_gen (resume)
+  int tmax = 0;                    // max generations per kernel launch (0 = backend default)
+  int epoch = 0;                   // generations per halo exchange (0 = auto)
+  int poll_gens = 0;               // generations between termination polls (0 = auto)
+};
+
+struct RunResult {
+  int64_t generations = 0;       // the reference's "Generations:" value
+  int64_t executed = 0;          // generations actually evaluated in this run
+  int64_t first_unchanged = -1;  // g_f, or -1 if no fixed point was seen
+  bool extinct = false;
+  std::string stop_reason = "limit";  // limit | extinction | similarity | fixed_point
+  double loop_ms = 0;            // wall time of the generation loop (incl. final sync)
+  int64_t exchanges = 0;         // halo exchanges performed
+  int64_t polls = 0;             // termination polls performed
+  int64_t kernel_launches = 0;
+};
+
+class Engine {
+ public:
+  Engine(const EngineConfig& cfg, Backend* backend, Transport* transport);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  const EngineConfig& config() const { return cfg_; }
+  const Decomposition& decomp() const { return dec_; }
+  const TileGeom& geom() const { return g_; }
+  int rank() const { return rank_; }
+  Extent rows() const { return dec_.rows(rank_); }
+  Extent cols() const { return dec_.cols(rank_); }
+  int epoch_depth() const { return D_; }
+  int tmax() const { return tmax_; }
+  int64_t generation() const { return gen_; }
+  void set_generation(int64_t g) { gen_ = g; }
+  Backend* backend() const { return be_; }
+  void* current_buffer() const { return buf_[cur_]; }
+
+  // State I/O.  `cells` is this rank's owned tile (rows() x cols()).
+  void load_cells(const uint8_t* cells, int64_t ld);
+  // `grid` is the full global grid; this rank copies out its subarray.
+  void load_global(const uint8_t* grid, int64_t ld);
+  void store_cells(uint8_t* cells, int64_t ld, bool ascii);
+  void init_random(uint64_t seed, double density);
+  int64_t alive_count();  // local owned cells
+
+  // Runs from the current generation up to config().gen_limit with the
+  // reference's termination semantics.
+  RunResult run();
+  // Runs exactly n more generations (termination flags still recorded, but
+  // no early stop): the bench path.
+  RunResult advance(int64_t n);
+
+  // Exchange halos of the current buffer (exposed for tests).
+  void halo_exchange();
+  // Performs one temporal block from the current buffer (tests).
+  void step_block(int T, int64_t row_lo, int64_t row_hi);
+
+ private:
+  RunResult run_impl(int64_t limit, bool stop_early);
+  bool poll(int64_t from, int64_t to, int64_t* first_unchanged);
+  int pick_T(int64_t remaining) const;
+
+  EngineConfig cfg_;
+  Backend* be_;
+  Transport* tr_;
+  Decomposition dec_;
+  int rank_ = 0;
+  TileGeom g_;
+  int D_ = 0, tmax_ = 0, poll_gens_ = 0;
+  void* buf_[2] = {nullptr, nullptr};
+  int cur_ = 0;
+  uint32_t* flags_ = nullptr;      // device: changed[t - flags_base_]
+  uint32_t* flags_host_ = nullptr; // pinned mirror
+  int64_t flags_base_ = 0, flags_len_ = 0;
+  uint32_t* alive_dev_ = nullptr;
+  void* colbuf_[4] = {nullptr, nullptr, nullptr, nullptr};  // send W, send E, recv W, recv E
+  int64_t gen_ = 0;
+  int64_t exchanges_ = 0, polls_ = 0, launches_ = 0;
+};
+
+}  // namespace gol

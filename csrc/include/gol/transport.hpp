@@ -1,0 +1,113 @@
+// Inter-rank transport for halo exchange and termination-flag reduction.
+//
+// Reference: 16 persistent MPI requests per buffer (8 Recv_init + 8
+// Send_init, rows / strided columns / corner cells), Startall+Waitall every
+// generation (src/game_mpi.c:340-401), plus two MPI_Allreduce(SUM) of 4-byte
+// flags (empty_all every generation, similarity_all every 3rd:
+// src/game_mpi.c:104-143).  Here a halo exchange happens once per epoch of
+// Dv generations, as one group of 2 sends + 2 receives per phase, and the
+// termination flags of many generations travel in one MAX all-reduce.
+//
+// Implementations:
+//   RcclTransport     - RCCL ncclSend/ncclRecv/ncclAllReduce over xGMI, one
+//                       process per GPU, communicator bootstrapped through
+//                       torch.distributed (transport_rccl.cpp).
+//   ThreadTransport   - in-process ranks (one host thread per rank); used for
+//                       multi-subdomain runs on one device and CPU tests.
+//   CallbackTransport - delegates to Python (torch.distributed: gloo on CPU,
+//                       nccl=RCCL on GPU); defined in bindings.cpp.
+#pragma once
+
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace gol {
+
+class Backend;
+
+struct P2POp {
+  bool send = false;
+  int peer = 0;
+  void* buf = nullptr;  // backend address space (device memory for HIP)
+  size_t bytes = 0;
+};
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual const char* name() const = 0;
+  // Executes a group of point-to-point operations.  Messages between a pair
+  // of ranks are matched in issue order.  Enqueued on `stream` (HIP) or
+  // completed before return (host transports).
+  virtual void exchange(const std::vector<P2POp>& ops, void* stream) = 0;
+  // In-place element-wise MAX over ranks of n uint32 values.
+  virtual void allreduce_max_u32(uint32_t* buf, size_t n, void* stream) = 0;
+  virtual void barrier() = 0;
+};
+
+// Single rank: nothing to exchange with.
+class SelfTransport final : public Transport {
+ public:
+  int rank() const override { return 0; }
+  int size() const override { return 1; }
+  const char* name() const override { return "self"; }
+  void exchange(const std::vector<P2POp>& ops, void* stream) override;
+  void allreduce_max_u32(uint32_t*, size_t, void*) override {}
+  void barrier() override {}
+};
+
+// Shared state of a group of in-process ranks.
+class ThreadHub {
+ public:
+  explicit ThreadHub(int nranks);
+  int size() const { return n_; }
+
+  struct Msg {
+    const void* buf;
+    size_t bytes;
+    bool consumed = false;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<std::pair<int, int>, std::deque<std::shared_ptr<Msg>>> queues;  // (src,dst)
+  // barrier / reduction state
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<uint32_t> red;
+
+ private:
+  int n_;
+};
+
+class ThreadTransport final : public Transport {
+ public:
+  ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, Backend* backend);
+  int rank() const override { return rank_; }
+  int size() const override { return hub_->size(); }
+  const char* name() const override { return "thread"; }
+  void exchange(const std::vector<P2POp>& ops, void* stream) override;
+  void allreduce_max_u32(uint32_t* buf, size_t n, void* stream) override;
+  void barrier() override;
+
+ private:
+  std::shared_ptr<ThreadHub> hub_;
+  int rank_;
+  Backend* backend_;
+};
+
+// RCCL transport (one process per GPU).  `unique_id` is the 128-byte
+// ncclUniqueId created on rank 0 and broadcast by the caller.
+std::unique_ptr<Transport> make_rccl_transport(const std::vector<uint8_t>& unique_id, int rank,
+                                               int nranks, int device);
+std::vector<uint8_t> rccl_unique_id();
+bool rccl_available();
+
+}  // namespace gol

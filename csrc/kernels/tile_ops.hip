@@ -1,0 +1,225 @@
+// Tile utility kernels: periodic halo fill, alive reduction, host-format
+// conversion and counter-based random init.
+//
+// Reference equivalents: halo_rows / halo_cols (src/game_cuda.cu:52-74, one
+// 32-thread block per 32 cells, called every generation with a device sync)
+// and the empty() reduction (src/game_cuda.cu:102-126: 32-int shared-memory
+// tree + int atomicAdd, covering only ~3% of the grid for W > 64, quirks
+// Q9/Q19).  Here the halo fill runs once per epoch of Dv generations, the
+// reduction is a wave64 reduction with 64-bit counts over every owned cell,
+// and all loops are grid-stride with 256-thread (4 x wave64) blocks.
+#include <hip/hip_runtime.h>
+
+#include "gol/backend.hpp"
+#include "life_kernels.hpp"
+
+namespace gol {
+namespace hipk {
+namespace {
+
+constexpr int kBlock = 256;
+
+inline unsigned grid_for(int64_t n, int64_t cap = 256 * 8 * 4) {
+  return unsigned(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, kBlock), cap)));
+}
+
+__device__ __forceinline__ int64_t pmod(int64_t x, int64_t m) {
+  int64_t r = x % m;
+  return r < 0 ? r + m : r;
+}
+
+__global__ void fill_cols_bits(uint32_t* buf, int64_t pitch_w, int64_t row0, int64_t H, int hw,
+                               int64_t ow) {
+  const int64_t nh = 2 * int64_t(hw);
+  const int64_t n = H * nh;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / nh, j = t - i * nh;
+    const int64_t c = j < hw ? j : ow + j;  // left halo words, then right ones
+    uint32_t* row = buf + (row0 + i) * pitch_w;
+    row[c] = row[hw + pmod(c - hw, ow)];
+  }
+}
+
+__global__ void fill_cols_u8(uint8_t* buf, int64_t pitch, int64_t row0, int64_t H, int64_t c0,
+                             int64_t W) {
+  const int64_t nh = 2 * c0;
+  const int64_t n = H * nh;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / nh, j = t - i * nh;
+    const int64_t x = j < c0 ? j : W + j;  // [0,c0) then [c0+W, 2c0+W)
+    uint8_t* row = buf + (row0 + i) * pitch;
+    row[x] = row[c0 + pmod(x - c0, W)];
+  }
+}
+
+__global__ void fill_rows_k(uint4* buf, int64_t pitch16, int64_t Dv, int64_t H) {
+  const int64_t n = 2 * Dv * pitch16;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t hr = t / pitch16, x = t - hr * pitch16;
+    const int64_t r = hr < Dv ? hr : H + hr;  // top halo rows, then bottom ones
+    const int64_t src = Dv + pmod(r - Dv, H);
+    buf[r * pitch16 + x] = buf[src * pitch16 + x];
+  }
+}
+
+__global__ void alive_k(const uint8_t* buf, int64_t pitch, int64_t row0, int64_t H,
+                        int64_t byte0, int64_t nbytes, uint32_t* any_flag,
+                        unsigned long long* count) {
+  // Owned span of each row: [byte0, byte0 + nbytes); 4-byte chunks, the last
+  // one masked.  Bits layout: popcount of words; U8: bytes are 0/1, so the
+  // popcount of a 4-byte chunk is its live-cell count.
+  const int64_t chunks = ceil_div(nbytes, 4);
+  const int64_t n = H * chunks;
+  unsigned long long local = 0;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / chunks, j = t - i * chunks;
+    const uint8_t* p = buf + (row0 + i) * pitch + byte0 + 4 * j;
+    uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+    const int64_t rem = nbytes - 4 * j;
+    if (rem < 4) v &= (1u << (8 * rem)) - 1u;
+    local += __popc(v);
+  }
+  // wave64 reduction, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+  if ((threadIdx.x & 63) == 0 && local) {
+    if (count) atomicAdd(count, local);
+    if (any_flag) atomicOr(any_flag, 1u);
+  }
+}
+
+__global__ void load_rows_bits(uint32_t* buf, int64_t pitch_w, int64_t first_row, int hw, int64_t ow,
+                               const uint8_t* stage, int64_t ld, int64_t n) {
+  const int64_t total = n * ow;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / ow, c = t - i * ow;
+    const uint8_t* s = stage + i * ld + 32 * c;
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) w |= uint32_t(s[j] == 1 || s[j] == '1') << j;
+    buf[(first_row + i) * pitch_w + hw + c] = w;
+  }
+}
+
+__global__ void load_rows_u8(uint8_t* buf, int64_t pitch, int64_t first_row, int64_t c0, int64_t W,
+                             const uint8_t* stage, int64_t ld, int64_t n) {
+  const int64_t total = n * W;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / W, x = t - i * W;
+    const uint8_t b = stage[i * ld + x];
+    buf[(first_row + i) * pitch + c0 + x] = uint8_t(b == 1 || b == '1');
+  }
+}
+
+__global__ void store_rows_k(const uint8_t* buf, int64_t pitch, int64_t first_row, int64_t c0,
+                             int64_t W, bool bits, uint8_t* stage, int64_t ld, int64_t n,
+                             uint8_t base) {
+  const int64_t total = n * W;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / W, x = t - i * W;
+    const uint8_t* row = buf + (first_row + i) * pitch;
+    uint8_t v;
+    if (bits) {
+      const int64_t cell = c0 + x;
+      v = uint8_t((reinterpret_cast<const uint32_t*>(row)[cell / 32] >> (cell % 32)) & 1u);
+    } else {
+      v = row[c0 + x] != 0;
+    }
+    stage[i * ld + x] = uint8_t(base + v);
+  }
+}
+
+__global__ void init_random_bits(uint32_t* buf, int64_t pitch_w, int64_t row0, int hw, int64_t H,
+                                 int64_t ow, uint64_t seed, uint32_t th, int64_t grow0,
+                                 int64_t gcol0) {
+  const int64_t total = H * ow;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / ow, c = t - i * ow;
+    uint32_t w = 0;
+    for (int j = 0; j < 32; ++j) w |= uint32_t(rng_cell(seed, grow0 + i, gcol0 + 32 * c + j, th)) << j;
+    buf[(row0 + i) * pitch_w + hw + c] = w;
+  }
+}
+
+__global__ void init_random_u8(uint8_t* buf, int64_t pitch, int64_t row0, int64_t c0, int64_t H,
+                               int64_t W, uint64_t seed, uint32_t th, int64_t grow0, int64_t gcol0) {
+  const int64_t total = H * W;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total;
+       t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / W, x = t - i * W;
+    buf[(row0 + i) * pitch + c0 + x] = uint8_t(rng_cell(seed, grow0 + i, gcol0 + x, th));
+  }
+}
+
+}  // namespace
+
+void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s) {
+  if (g.hw == 0) return;
+  if (g.layout == Layout::Bits) {
+    const int64_t n = g.H * 2 * g.hw;
+    hipLaunchKernelGGL(fill_cols_bits, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                       reinterpret_cast<uint32_t*>(buf), g.pitch / 4, int64_t(g.row0()), g.H, g.hw,
+                       g.W / 32);
+  } else {
+    const int64_t n = g.H * 2 * g.cell0();
+    hipLaunchKernelGGL(fill_cols_u8, dim3(grid_for(n)), dim3(kBlock), 0, s, buf, g.pitch,
+                       int64_t(g.row0()), g.H, g.cell0(), g.W);
+  }
+}
+
+void launch_fill_rows(uint8_t* buf, const TileGeom& g, hipStream_t s) {
+  if (g.Dv == 0) return;
+  const int64_t n = 2 * int64_t(g.Dv) * (g.pitch / 16);
+  hipLaunchKernelGGL(fill_rows_k, dim3(grid_for(n)), dim3(kBlock), 0, s, reinterpret_cast<uint4*>(buf),
+                     g.pitch / 16, int64_t(g.Dv), g.H);
+}
+
+void launch_alive(const uint8_t* buf, const TileGeom& g, uint32_t* any_flag,
+                  unsigned long long* count, hipStream_t s) {
+  const int64_t byte0 = g.offset(0, g.cell0());
+  const int64_t nbytes = g.span_bytes(g.W);
+  const int64_t n = g.H * ceil_div(nbytes, 4);
+  hipLaunchKernelGGL(alive_k, dim3(grid_for(n)), dim3(kBlock), 0, s, buf, g.pitch, int64_t(g.row0()),
+                     g.H, byte0, nbytes, any_flag, count);
+}
+
+void launch_load_rows(uint8_t* buf, const TileGeom& g, const uint8_t* stage, int64_t ld, int64_t r0,
+                      int64_t n, hipStream_t s) {
+  if (g.layout == Layout::Bits) {
+    hipLaunchKernelGGL(load_rows_bits, dim3(grid_for(n * (g.W / 32))), dim3(kBlock), 0, s,
+                       reinterpret_cast<uint32_t*>(buf), g.pitch / 4, g.row0() + r0, g.hw, g.W / 32,
+                       stage, ld, n);
+  } else {
+    hipLaunchKernelGGL(load_rows_u8, dim3(grid_for(n * g.W)), dim3(kBlock), 0, s, buf, g.pitch,
+                       g.row0() + r0, g.cell0(), g.W, stage, ld, n);
+  }
+}
+
+void launch_store_rows(const uint8_t* buf, const TileGeom& g, uint8_t* stage, int64_t ld, int64_t r0,
+                       int64_t n, bool ascii, hipStream_t s) {
+  hipLaunchKernelGGL(store_rows_k, dim3(grid_for(n * g.W)), dim3(kBlock), 0, s, buf, g.pitch,
+                     g.row0() + r0, g.cell0(), g.W, g.layout == Layout::Bits, stage, ld, n,
+                     uint8_t(ascii ? '0' : 0));
+}
+
+void launch_init_random(uint8_t* buf, const TileGeom& g, uint64_t seed, uint32_t th, int64_t grow0,
+                        int64_t gcol0, hipStream_t s) {
+  if (g.layout == Layout::Bits) {
+    hipLaunchKernelGGL(init_random_bits, dim3(grid_for(g.H * (g.W / 32))), dim3(kBlock), 0, s,
+                       reinterpret_cast<uint32_t*>(buf), g.pitch / 4, int64_t(g.row0()), g.hw, g.H,
+                       g.W / 32, seed, th, grow0, gcol0);
+  } else {
+    hipLaunchKernelGGL(init_random_u8, dim3(grid_for(g.H * g.W)), dim3(kBlock), 0, s, buf, g.pitch,
+                       int64_t(g.row0()), g.cell0(), g.H, g.W, seed, th, grow0, gcol0);
+  }
+}
+
+}  // namespace hipk
+}  // namespace gol

@@ -1,0 +1,283 @@
+// CPU backend: bit-exact host emulation of the HIP kernels.
+//
+// Serves three purposes: (1) the engine's logic (epochs, deep halos, lazy
+// termination, decomposition) is testable without a GPU; (2) it is the
+// multi-threaded CPU engine that replaces the reference's OpenMP variant
+// (src/game_openmp.c:29-112); (3) it is an independent oracle for the HIP
+// kernels (same bit-sliced rule as common.hpp, but plain word loops).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "gol/backend.hpp"
+#include "gol/parallel.hpp"
+
+namespace gol {
+namespace {
+
+inline uint32_t pack32(const uint8_t* p) {
+  uint32_t w = 0;
+  for (int j = 0; j < 32; ++j) w |= uint32_t(p[j] != 0) << j;
+  return w;
+}
+inline void unpack32(uint32_t w, uint8_t* p) {
+  for (int j = 0; j < 32; ++j) p[j] = uint8_t((w >> j) & 1u);
+}
+
+// Mask of owned cells inside padded word c.
+inline uint32_t owned_mask(const TileGeom& g, int64_t c) {
+  int64_t lo = g.cell0(), hi = g.cell0() + g.W;
+  int64_t b = 32 * c;
+  if (b + 32 <= lo || b >= hi) return 0;
+  uint32_t m = 0xFFFFFFFFu;
+  if (b < lo) m &= 0xFFFFFFFFu << (lo - b);
+  if (b + 32 > hi) m &= 0xFFFFFFFFu >> (b + 32 - hi);
+  return m;
+}
+
+class CpuBackend final : public Backend {
+ public:
+  explicit CpuBackend(int threads) : pool_(threads > 0 ? threads : default_host_threads()) {}
+  std::string name() const override { return "cpu"; }
+  bool is_device() const override { return false; }
+
+  void* alloc(size_t bytes) override {
+    void* p = std::calloc(bytes ? bytes : 1, 1);
+    GOL_REQUIRE(p, "host allocation of " + std::to_string(bytes) + " bytes failed");
+    return p;
+  }
+  void release(void* p) override { std::free(p); }
+  void* alloc_host(size_t bytes) override { return alloc(bytes); }
+  void release_host(void* p) override { std::free(p); }
+  void memset_async(void* p, int v, size_t bytes) override { std::memset(p, v, bytes); }
+  void copy_h2d(void* d, const void* s, size_t n) override { std::memcpy(d, s, n); }
+  void copy_d2h(void* d, const void* s, size_t n) override { std::memcpy(d, s, n); }
+  void copy_d2h_async(void* d, const void* s, size_t n) override { std::memcpy(d, s, n); }
+  void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
+                     int64_t rows) override {
+    auto* d = static_cast<uint8_t*>(dst);
+    auto* s = static_cast<const uint8_t*>(src);
+    for (int64_t r = 0; r < rows; ++r) std::memmove(d + r * dpitch, s + r * spitch, size_t(width));
+  }
+  void synchronize() override {}
+  void* event_record() override { return nullptr; }
+  void event_wait(void*) override {}
+  void event_destroy(void*) override {}
+
+  void run_block(const BlockArgs& a) override;
+  void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override;
+  void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {
+    *flag = alive_count(buf, g) > 0 ? 1u : 0u;
+  }
+  int64_t alive_count(const void* buf, const TileGeom& g) override;
+  void load_owned(void* buf, const TileGeom& g, const uint8_t* cells, int64_t ld) override;
+  void store_owned(const void* buf, const TileGeom& g, uint8_t* cells, int64_t ld,
+                   bool ascii) override;
+  void init_random(void* buf, const TileGeom& g, uint64_t seed, double density, int64_t grow0,
+                   int64_t gcol0) override;
+
+ private:
+  // Word c of padded row r as a 32-cell bit word (0 outside [0, Wp)).
+  uint32_t read_word(const uint8_t* base, const TileGeom& g, int64_t r, int64_t c) const {
+    if (c < 0 || c >= g.Wp()) return 0;
+    const uint8_t* row = base + r * g.pitch;
+    if (g.layout == Layout::Bits) {
+      uint32_t w;
+      std::memcpy(&w, row + 4 * c, 4);
+      return w;
+    }
+    return pack32(row + 32 * c);
+  }
+  ThreadPool pool_;
+};
+
+void CpuBackend::run_block(const BlockArgs& a) {
+  const TileGeom& g = a.g;
+  const int T = a.T;
+  const int64_t Wp = g.Wp();
+  const int64_t r0 = a.row_lo - T, r1 = a.row_hi + T;  // input rows
+  GOL_REQUIRE(r0 >= 0 && r1 <= g.R() && a.row_lo < a.row_hi && T >= 1, "run_block: bad row range");
+  const int64_t nr = r1 - r0;
+  std::vector<uint32_t> lvl[2] = {std::vector<uint32_t>(size_t(nr * Wp)),
+                                  std::vector<uint32_t>(size_t(nr * Wp))};
+  auto* in = static_cast<const uint8_t*>(a.in);
+  pool_.parallel_for(nr, [&](int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i)
+      for (int64_t c = 0; c < Wp; ++c) lvl[0][size_t(i * Wp + c)] = read_word(in, g, r0 + i, c);
+  });
+  std::vector<uint32_t> owned(static_cast<size_t>(Wp));
+  for (int64_t c = 0; c < Wp; ++c) owned[size_t(c)] = owned_mask(g, c);
+
+  for (int lev = 1; lev <= T; ++lev) {
+    const auto& src = lvl[(lev - 1) & 1];
+    auto& dst = lvl[lev & 1];
+    // Level `lev` is valid on rows [r0 + lev, r1 - lev).
+    const int64_t lo = lev, hi = nr - lev;
+    std::vector<uint8_t> any(size_t(hi - lo), 0);
+    pool_.parallel_for(hi - lo, [&](int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) {
+        const int64_t i = lo + k;
+        const uint32_t* up = &src[size_t((i - 1) * Wp)];
+        const uint32_t* mid = &src[size_t(i * Wp)];
+        const uint32_t* dn = &src[size_t((i + 1) * Wp)];
+        uint32_t* out = &dst[size_t(i * Wp)];
+        uint32_t acc = 0;
+        for (int64_t c = 0; c < Wp; ++c) {
+          auto nb = [&](const uint32_t* row) {
+            return hsum_host(c > 0 ? row[c - 1] : 0u, row[c], c + 1 < Wp ? row[c + 1] : 0u);
+          };
+          uint32_t nw = rule_host(nb(up), nb(mid), nb(dn), mid[c]);
+          out[c] = nw;
+          acc |= (nw ^ mid[c]) & owned[size_t(c)];
+        }
+        any[size_t(k)] = acc != 0;
+      }
+    }, 8);
+    if (a.changed) {
+      bool ch = std::any_of(any.begin(), any.end(), [](uint8_t v) { return v != 0; });
+      if (ch) a.changed[a.gen_base + lev - a.flags_base] = 1u;
+    }
+  }
+  const auto& fin = lvl[T & 1];
+  auto* out = static_cast<uint8_t*>(a.out);
+  pool_.parallel_for(a.row_hi - a.row_lo, [&](int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      const int64_t r = a.row_lo + k;
+      const uint32_t* src = &fin[size_t((r - r0) * Wp)];
+      uint8_t* row = out + r * g.pitch;
+      if (g.layout == Layout::Bits)
+        std::memcpy(row, src, size_t(4 * Wp));
+      else
+        for (int64_t c = 0; c < Wp; ++c) unpack32(src[c], row + 32 * c);
+    }
+  });
+}
+
+void CpuBackend::fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) {
+  auto* p = static_cast<uint8_t*>(buf);
+  const int64_t H = g.H, W = g.W, c0 = g.cell0();
+  if (cols) {
+    pool_.parallel_for(H, [&](int64_t b, int64_t e) {
+      for (int64_t r = g.row0() + b; r < g.row0() + e; ++r) {
+        uint8_t* row = p + r * g.pitch;
+        if (g.layout == Layout::Bits) {
+          auto* w = reinterpret_cast<uint32_t*>(row);
+          const int64_t ow = W / 32, h = g.hw;
+          for (int64_t c = 0; c < g.Wp(); ++c) {
+            if (c >= h && c < h + ow) continue;
+            w[c] = w[h + (((c - h) % ow) + ow) % ow];
+          }
+        } else {
+          for (int64_t x = 0; x < 32 * g.Wp(); ++x) {
+            if (x >= c0 && x < c0 + W) continue;
+            if (x >= g.Wc()) break;
+            row[x] = row[c0 + (((x - c0) % W) + W) % W];
+          }
+        }
+      }
+    });
+  }
+  if (rows) {
+    for (int64_t r = 0; r < g.R(); ++r) {
+      if (r >= g.row0() && r < g.row0() + H) continue;
+      int64_t src = g.row0() + (((r - g.row0()) % H) + H) % H;
+      std::memcpy(p + r * g.pitch, p + src * g.pitch, size_t(g.pitch));
+    }
+  }
+}
+
+int64_t CpuBackend::alive_count(const void* buf, const TileGeom& g) {
+  auto* p = static_cast<const uint8_t*>(buf);
+  std::vector<int64_t> part(size_t(g.H), 0);
+  pool_.parallel_for(g.H, [&](int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      const uint8_t* row = p + (g.row0() + i) * g.pitch;
+      int64_t n = 0;
+      if (g.layout == Layout::Bits) {
+        const auto* w = reinterpret_cast<const uint32_t*>(row) + g.hw;
+        for (int64_t c = 0; c < g.W / 32; ++c) n += __builtin_popcount(w[c]);
+      } else {
+        for (int64_t x = 0; x < g.W; ++x) n += row[g.cell0() + x] != 0;
+      }
+      part[size_t(i)] = n;
+    }
+  });
+  int64_t s = 0;
+  for (auto v : part) s += v;
+  return s;
+}
+
+void CpuBackend::load_owned(void* buf, const TileGeom& g, const uint8_t* cells, int64_t ld) {
+  auto* p = static_cast<uint8_t*>(buf);
+  pool_.parallel_for(g.H, [&](int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      uint8_t* row = p + (g.row0() + i) * g.pitch;
+      const uint8_t* src = cells + i * ld;
+      if (g.layout == Layout::Bits) {
+        auto* w = reinterpret_cast<uint32_t*>(row) + g.hw;
+        for (int64_t c = 0; c < g.W / 32; ++c) {
+          uint32_t v = 0;
+          for (int j = 0; j < 32; ++j) {
+            uint8_t ch = src[32 * c + j];
+            v |= uint32_t(ch == '1' || ch == 1) << j;
+          }
+          w[c] = v;
+        }
+      } else {
+        for (int64_t x = 0; x < g.W; ++x) {
+          uint8_t ch = src[x];
+          row[g.cell0() + x] = uint8_t(ch == '1' || ch == 1);
+        }
+      }
+    }
+  });
+}
+
+void CpuBackend::store_owned(const void* buf, const TileGeom& g, uint8_t* cells, int64_t ld,
+                             bool ascii) {
+  auto* p = static_cast<const uint8_t*>(buf);
+  const uint8_t base = ascii ? '0' : 0;
+  pool_.parallel_for(g.H, [&](int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      const uint8_t* row = p + (g.row0() + i) * g.pitch;
+      uint8_t* dst = cells + i * ld;
+      if (g.layout == Layout::Bits) {
+        const auto* w = reinterpret_cast<const uint32_t*>(row) + g.hw;
+        for (int64_t x = 0; x < g.W; ++x) dst[x] = uint8_t(base + ((w[x / 32] >> (x % 32)) & 1u));
+      } else {
+        for (int64_t x = 0; x < g.W; ++x) dst[x] = uint8_t(base + (row[g.cell0() + x] != 0));
+      }
+    }
+  });
+}
+
+void CpuBackend::init_random(void* buf, const TileGeom& g, uint64_t seed, double density,
+                             int64_t grow0, int64_t gcol0) {
+  auto* p = static_cast<uint8_t*>(buf);
+  const uint32_t th = density_thresh(density);
+  pool_.parallel_for(g.H, [&](int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      uint8_t* row = p + (g.row0() + i) * g.pitch;
+      if (g.layout == Layout::Bits) {
+        auto* w = reinterpret_cast<uint32_t*>(row) + g.hw;
+        for (int64_t c = 0; c < g.W / 32; ++c) {
+          uint32_t v = 0;
+          for (int j = 0; j < 32; ++j) v |= uint32_t(rng_cell(seed, grow0 + i, gcol0 + 32 * c + j, th)) << j;
+          w[c] = v;
+        }
+      } else {
+        for (int64_t x = 0; x < g.W; ++x) row[g.cell0() + x] = uint8_t(rng_cell(seed, grow0 + i, gcol0 + x, th));
+      }
+    }
+  });
+}
+
+}  // namespace
+
+std::unique_ptr<Backend> make_cpu_backend(int threads) {
+  return std::make_unique<CpuBackend>(threads);
+}
+
+}  // namespace gol

@@ -1,0 +1,216 @@
+// HIP backend: device memory, one non-blocking stream, CDNA4 kernels.
+//
+// Reference runtime pattern (src/game_cuda.cu:185-276): cudaMalloc of
+// (W+2)(H+2) bytes computed in int, cudaMemcpy of the whole grid, and a
+// cudaDeviceSynchronize after every kernel.  Here every call is enqueued on
+// the backend's stream and only the engine's periodic flag poll and the
+// final copy-out block the host.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../kernels/life_kernels.hpp"
+#include "gol/backend.hpp"
+
+#define HIP_CHECK(expr)                                                                     \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      ::gol::fail(std::string("HIP error in ") + __FILE__ + ":" + std::to_string(__LINE__) + \
+                  " (" #expr "): " + hipGetErrorString(e_));                                \
+  } while (0)
+
+namespace gol {
+namespace {
+
+int env_int(const char* name, int dflt) {
+  if (const char* s = std::getenv(name)) {
+    int v = std::atoi(s);
+    if (v > 0) return v;
+  }
+  return dflt;
+}
+
+class HipBackend final : public Backend {
+ public:
+  explicit HipBackend(int device) : dev_(device) {
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    GOL_REQUIRE(n > 0, "no HIP device available");
+    GOL_REQUIRE(device >= 0 && device < n, "HIP device index out of range");
+    HIP_CHECK(hipSetDevice(dev_));
+    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
+    arch_ = prop.gcnArchName;
+    cus_ = prop.multiProcessorCount;
+    tune_.target_waves = env_int("GOL_TARGET_WAVES", std::max(1024, cus_ * 16));
+    tune_.min_seg_rows = env_int("GOL_MIN_SEG_ROWS", 64);
+  }
+  ~HipBackend() override {
+    hipSetDevice(dev_);
+    if (stream_) hipStreamSynchronize(stream_);
+    if (stage_) hipFree(stage_);
+    if (stream_) hipStreamDestroy(stream_);
+  }
+
+  std::string name() const override { return "hip:" + std::to_string(dev_) + ":" + arch_; }
+  bool is_device() const override { return true; }
+  int device() const override { return dev_; }
+  void* stream() const override { return stream_; }
+
+  void* alloc(size_t bytes) override {
+    HIP_CHECK(hipSetDevice(dev_));
+    void* p = nullptr;
+    HIP_CHECK(hipMalloc(&p, bytes ? bytes : 1));
+    HIP_CHECK(hipMemsetAsync(p, 0, bytes ? bytes : 1, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    return p;
+  }
+  void release(void* p) override {
+    if (!p) return;
+    hipSetDevice(dev_);
+    hipStreamSynchronize(stream_);
+    hipFree(p);
+  }
+  void* alloc_host(size_t bytes) override {
+    void* p = nullptr;
+    HIP_CHECK(hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault));
+    return p;
+  }
+  void release_host(void* p) override {
+    if (p) hipHostFree(p);
+  }
+  void memset_async(void* p, int v, size_t bytes) override {
+    HIP_CHECK(hipMemsetAsync(p, v, bytes, stream_));
+  }
+  void copy_h2d(void* d, const void* s, size_t n) override {
+    HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  void copy_d2h(void* d, const void* s, size_t n) override {
+    HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  void copy_d2h_async(void* d, const void* s, size_t n) override {
+    HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
+  }
+  void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
+                     int64_t rows) override {
+    if (rows <= 0 || width <= 0) return;
+    HIP_CHECK(hipMemcpy2DAsync(dst, size_t(dpitch), src, size_t(spitch), size_t(width), size_t(rows),
+                               hipMemcpyDefault, stream_));
+  }
+  void synchronize() override { HIP_CHECK(hipStreamSynchronize(stream_)); }
+  void* event_record() override {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(e, stream_));
+    return e;
+  }
+  void event_wait(void* ev) override { HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(ev))); }
+  void event_destroy(void* ev) override { hipEventDestroy(static_cast<hipEvent_t>(ev)); }
+
+  void run_block(const BlockArgs& a) override {
+    hipk::launch_life_block(a, tune_, stream_);
+    HIP_CHECK(hipGetLastError());
+  }
+  void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override {
+    if (cols) hipk::launch_fill_cols(static_cast<uint8_t*>(buf), g, stream_);
+    if (rows) hipk::launch_fill_rows(static_cast<uint8_t*>(buf), g, stream_);
+    HIP_CHECK(hipGetLastError());
+  }
+  void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {
+    HIP_CHECK(hipMemsetAsync(flag, 0, 4, stream_));
+    hipk::launch_alive(static_cast<const uint8_t*>(buf), g, flag, nullptr, stream_);
+    HIP_CHECK(hipGetLastError());
+  }
+  int64_t alive_count(const void* buf, const TileGeom& g) override {
+    unsigned long long* d = nullptr;
+    HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d), 8, stream_));
+    HIP_CHECK(hipMemsetAsync(d, 0, 8, stream_));
+    hipk::launch_alive(static_cast<const uint8_t*>(buf), g, nullptr, d, stream_);
+    HIP_CHECK(hipGetLastError());
+    unsigned long long h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipFreeAsync(d, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    return int64_t(h);
+  }
+
+  // Host <-> tile transfers go through a bounded device staging buffer so a
+  // 32768^2 (1 GiB) or larger grid never needs a second full-size copy.
+  void load_owned(void* buf, const TileGeom& g, const uint8_t* cells, int64_t ld) override {
+    const int64_t chunk = rows_per_chunk(g);
+    uint8_t* stage = static_cast<uint8_t*>(stage_buf(chunk * g.W));
+    for (int64_t r = 0; r < g.H; r += chunk) {
+      const int64_t n = std::min(chunk, g.H - r);
+      HIP_CHECK(hipMemcpy2DAsync(stage, size_t(g.W), cells + r * ld, size_t(ld), size_t(g.W), size_t(n),
+                                 hipMemcpyHostToDevice, stream_));
+      hipk::launch_load_rows(static_cast<uint8_t*>(buf), g, stage, g.W, r, n, stream_);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+  }
+  void store_owned(const void* buf, const TileGeom& g, uint8_t* cells, int64_t ld, bool ascii) override {
+    const int64_t chunk = rows_per_chunk(g);
+    uint8_t* stage = static_cast<uint8_t*>(stage_buf(chunk * g.W));
+    for (int64_t r = 0; r < g.H; r += chunk) {
+      const int64_t n = std::min(chunk, g.H - r);
+      hipk::launch_store_rows(static_cast<const uint8_t*>(buf), g, stage, g.W, r, n, ascii, stream_);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipMemcpy2DAsync(cells + r * ld, size_t(ld), stage, size_t(g.W), size_t(g.W), size_t(n),
+                                 hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+  }
+  void init_random(void* buf, const TileGeom& g, uint64_t seed, double density, int64_t grow0,
+                   int64_t gcol0) override {
+    hipk::launch_init_random(static_cast<uint8_t*>(buf), g, seed, density_thresh(density), grow0, gcol0,
+                             stream_);
+    HIP_CHECK(hipGetLastError());
+  }
+
+ private:
+  int64_t rows_per_chunk(const TileGeom& g) const {
+    const int64_t budget = int64_t(256) << 20;
+    return std::max<int64_t>(1, std::min<int64_t>(g.H, budget / std::max<int64_t>(1, g.W)));
+  }
+  void* stage_buf(int64_t bytes) {
+    if (bytes > stage_bytes_) {
+      if (stage_) {
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        HIP_CHECK(hipFree(stage_));
+      }
+      HIP_CHECK(hipMalloc(&stage_, size_t(bytes)));
+      stage_bytes_ = bytes;
+    }
+    return stage_;
+  }
+
+  int dev_;
+  hipStream_t stream_ = nullptr;
+  std::string arch_;
+  int cus_ = 256;
+  hipk::LifeTuning tune_;
+  void* stage_ = nullptr;
+  int64_t stage_bytes_ = 0;
+};
+
+}  // namespace
+
+bool hip_available() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return false;
+  return n > 0;
+}
+
+std::unique_ptr<Backend> make_hip_backend(int device) {
+  GOL_REQUIRE(hip_available(), "no HIP device available (HIP backend requested)");
+  return std::make_unique<HipBackend>(device);
+}
+
+}  // namespace gol

@@ -1,0 +1,257 @@
+#include "gol/engine.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+namespace gol {
+
+namespace {
+constexpr int kTSizes[] = {32, 16, 8, 4, 2, 1};  // temporal block sizes built for every backend
+
+int64_t min_tile_rows(const Decomposition& d) { return d.H / d.Py; }
+int64_t min_tile_cols(const Decomposition& d) { return (d.W / d.col_unit / d.Px) * d.col_unit; }
+}  // namespace
+
+Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
+    : cfg_(cfg), be_(backend), tr_(transport) {
+  GOL_REQUIRE(be_ && tr_, "engine needs a backend and a transport");
+  GOL_REQUIRE(cfg_.W > 0 && cfg_.H > 0, "grid dimensions must be positive");
+  GOL_REQUIRE(cfg_.sim_freq > 0, "similarity frequency must be positive");
+  GOL_REQUIRE(cfg_.gen_limit >= 0, "generation limit must be >= 0");
+  rank_ = tr_->rank();
+  int64_t unit = (cfg_.layout == Layout::Bits || cfg_.W % 32 == 0) ? 32 : 1;
+  if (cfg_.layout == Layout::Bits)
+    GOL_REQUIRE(cfg_.W % 32 == 0, "bit-packed layout needs width % 32 == 0 (use the u8 layout)");
+  dec_ = Decomposition::make(cfg_.W, cfg_.H, tr_->size(), cfg_.decomp, unit);
+
+  tmax_ = cfg_.tmax > 0 ? cfg_.tmax : 16;
+  tmax_ = std::min(tmax_, 32);
+  int D = cfg_.epoch > 0 ? cfg_.epoch : 4 * tmax_;
+  if (dec_.Py > 1) D = int(std::min<int64_t>(D, min_tile_rows(dec_)));
+  if (dec_.Px > 1) {
+    int64_t cap = 32 * (min_tile_cols(dec_) / 32);
+    GOL_REQUIRE(cap >= 1, "tiles narrower than 32 cells cannot exchange column halos");
+    D = int(std::min<int64_t>(D, cap));
+  }
+  D_ = std::max(1, D);
+  tmax_ = std::min(tmax_, D_);
+  int hw = int(ceil_div(D_, 32));
+  Extent r = rows(), c = cols();
+  g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
+  poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : 256;
+
+  for (auto& b : buf_) b = be_->alloc(size_t(g_.bytes()));
+  alive_dev_ = static_cast<uint32_t*>(be_->alloc(64));
+  if (dec_.Px > 1) {
+    size_t n = size_t(g_.span_bytes(32 * int64_t(g_.hw)) * g_.H);
+    for (auto& b : colbuf_) b = be_->alloc(n);
+  }
+  gen_ = cfg_.start_gen;
+}
+
+Engine::~Engine() {
+  for (auto& b : buf_)
+    if (b) be_->release(b);
+  for (auto& b : colbuf_)
+    if (b) be_->release(b);
+  if (flags_) be_->release(flags_);
+  if (flags_host_) be_->release_host(flags_host_);
+  if (alive_dev_) be_->release(alive_dev_);
+}
+
+void Engine::load_cells(const uint8_t* cells, int64_t ld) {
+  be_->load_owned(buf_[cur_], g_, cells, ld);
+  be_->synchronize();
+}
+
+void Engine::load_global(const uint8_t* grid, int64_t ld) {
+  Extent r = rows(), c = cols();
+  load_cells(grid + r.begin * ld + c.begin, ld);
+}
+
+void Engine::store_cells(uint8_t* cells, int64_t ld, bool ascii) {
+  be_->synchronize();
+  be_->store_owned(buf_[cur_], g_, cells, ld, ascii);
+}
+
+void Engine::init_random(uint64_t seed, double density) {
+  be_->init_random(buf_[cur_], g_, seed, density, rows().begin, cols().begin);
+  be_->synchronize();
+}
+
+int64_t Engine::alive_count() {
+  be_->synchronize();
+  return be_->alive_count(buf_[cur_], g_);
+}
+
+int Engine::pick_T(int64_t remaining) const {
+  for (int t : kTSizes)
+    if (t <= tmax_ && t <= remaining) return t;
+  return 1;
+}
+
+// Two-phase halo exchange (columns, then full-width rows so the corner
+// cells travel with the rows): 4 messages instead of the reference's 8
+// per-generation messages with a strided MPI_Type_vector column
+// (src/game_mpi.c:335-383).
+void Engine::halo_exchange() {
+  void* buf = buf_[cur_];
+  auto* base = static_cast<uint8_t*>(buf);
+  auto nb = dec_.neighbors(rank_);
+  const int64_t H = g_.H, pitch = g_.pitch;
+  // Phase A: west/east halo columns of the owned rows.
+  if (dec_.Px == 1) {
+    be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/false);
+  } else {
+    const int64_t halo = 32 * int64_t(g_.hw);
+    const int64_t span = g_.span_bytes(halo);
+    const int64_t r0 = g_.row0();
+    be_->copy_2d_async(colbuf_[0], span, base + g_.offset(r0, g_.cell0()), pitch, span, H);
+    be_->copy_2d_async(colbuf_[1], span, base + g_.offset(r0, g_.cell0() + g_.W - halo), pitch, span, H);
+    std::vector<P2POp> ops = {
+        {true, nb[kWest], colbuf_[0], size_t(span * H)},
+        {false, nb[kEast], colbuf_[3], size_t(span * H)},
+        {true, nb[kEast], colbuf_[1], size_t(span * H)},
+        {false, nb[kWest], colbuf_[2], size_t(span * H)},
+    };
+    tr_->exchange(ops, be_->stream());
+    be_->copy_2d_async(base + g_.offset(r0, 0), pitch, colbuf_[2], span, span, H);
+    be_->copy_2d_async(base + g_.offset(r0, g_.cell0() + g_.W), pitch, colbuf_[3], span, span, H);
+  }
+  // Phase B: north/south halo rows over the full padded width.
+  if (dec_.Py == 1) {
+    be_->fill_periodic(buf, g_, /*cols=*/false, /*rows=*/true);
+  } else {
+    const int64_t Dv = g_.Dv;
+    const size_t bytes = size_t(Dv * pitch);
+    std::vector<P2POp> ops = {
+        {true, nb[kNorth], base + Dv * pitch, bytes},        // my top rows -> north's bottom halo
+        {false, nb[kSouth], base + (Dv + H) * pitch, bytes},  // south's top rows -> my bottom halo
+        {true, nb[kSouth], base + H * pitch, bytes},          // my bottom rows -> south's top halo
+        {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
+    };
+    tr_->exchange(ops, be_->stream());
+  }
+  ++exchanges_;
+}
+
+void Engine::step_block(int T, int64_t row_lo, int64_t row_hi) {
+  BlockArgs a;
+  a.in = buf_[cur_];
+  a.out = buf_[cur_ ^ 1];
+  a.g = g_;
+  a.row_lo = row_lo;
+  a.row_hi = row_hi;
+  a.T = T;
+  a.gen_base = gen_;
+  a.changed = (flags_ && gen_ + T < flags_base_ + flags_len_ && gen_ >= flags_base_) ? flags_ : nullptr;
+  a.flags_base = flags_base_;
+  be_->run_block(a);
+  ++launches_;
+  cur_ ^= 1;
+  gen_ += T;
+}
+
+bool Engine::poll(int64_t from, int64_t to, int64_t* first_unchanged) {
+  // Flags for generations (from, to]; MAX over ranks == logical OR.
+  const int64_t n = to - from;
+  if (n <= 0) return false;
+  uint32_t* dev = flags_ + (from + 1 - flags_base_);
+  if (tr_->size() > 1) tr_->allreduce_max_u32(dev, size_t(n), be_->stream());
+  be_->copy_d2h_async(flags_host_, dev, size_t(n) * sizeof(uint32_t));
+  void* ev = be_->event_record();
+  be_->event_wait(ev);
+  be_->event_destroy(ev);
+  ++polls_;
+  for (int64_t i = 0; i < n; ++i)
+    if (flags_host_[i] == 0) {
+      *first_unchanged = from + 1 + i;
+      return true;
+    }
+  return false;
+}
+
+RunResult Engine::run() { return run_impl(cfg_.gen_limit, /*stop_early=*/true); }
+
+RunResult Engine::advance(int64_t n) { return run_impl(gen_ + n, /*stop_early=*/false); }
+
+RunResult Engine::run_impl(int64_t limit, bool stop_early) {
+  RunResult res;
+  const int64_t start = gen_;
+  if (limit < start) limit = start;
+  // (Re)allocate per-generation flags for (start, limit].
+  const int64_t need = limit - start + 2;
+  if (!flags_ || flags_len_ < need) {
+    if (flags_) be_->release(flags_);
+    if (flags_host_) be_->release_host(flags_host_);
+    flags_len_ = std::max<int64_t>(need, 64);
+    flags_ = static_cast<uint32_t*>(be_->alloc(size_t(flags_len_) * 4));
+    flags_host_ = static_cast<uint32_t*>(be_->alloc_host(size_t(flags_len_) * 4));
+  }
+  flags_base_ = start;
+  be_->memset_async(flags_, 0, size_t(flags_len_) * 4);
+  const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_;
+  tr_->barrier();
+  be_->synchronize();
+  auto t0 = std::chrono::steady_clock::now();
+
+  int64_t checked = start, found = -1;
+  const int64_t poll_epochs = std::max<int64_t>(1, poll_gens_ / D_);
+  int64_t epoch = 0;
+  while (gen_ < limit) {
+    int64_t d = std::min<int64_t>(D_, limit - gen_);
+    halo_exchange();
+    int64_t a = 0;
+    while (d > 0) {
+      int T = pick_T(d);
+      step_block(T, a + T, g_.R() - a - T);
+      a += T;
+      d -= T;
+    }
+    ++epoch;
+    if (stop_early && (epoch % poll_epochs == 0 || gen_ == limit)) {
+      if (poll(checked, gen_, &found)) break;
+      checked = gen_;
+    }
+  }
+  be_->synchronize();
+  tr_->barrier();
+  auto t1 = std::chrono::steady_clock::now();
+  res.loop_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  res.executed = gen_ - start;
+  res.exchanges = exchanges_ - e0;
+  res.polls = polls_ - p0;
+  res.kernel_launches = launches_ - l0;
+  res.generations = limit;
+  if (found >= 0) {
+    res.first_unchanged = found;
+    be_->alive_any(buf_[cur_], g_, alive_dev_);
+    if (tr_->size() > 1) tr_->allreduce_max_u32(alive_dev_, 1, be_->stream());
+    uint32_t alive = 0;
+    be_->copy_d2h(&alive, alive_dev_, 4);
+    if (!alive) {
+      res.extinct = true;
+      res.generations = found - 1;
+      res.stop_reason = "extinction";
+    } else if (cfg_.check_similarity) {
+      // Similarity checks happen at generations t > start with
+      // (t - start + sim_phase) % F == 0 (counter reset only on a failed check,
+      // src/game.c:181-189).
+      const int64_t F = cfg_.sim_freq;
+      int64_t k = found - start + cfg_.sim_phase;
+      int64_t tsim = found + ((F - (k % F)) % F);
+      if (tsim <= limit) {
+        res.generations = tsim - 1;
+        res.stop_reason = "similarity";
+      } else {
+        res.stop_reason = "fixed_point";
+      }
+    } else {
+      res.stop_reason = "fixed_point";
+    }
+  }
+  return res;
+}
+
+}  // namespace gol

@@ -1,0 +1,160 @@
+#include "gol/io.hpp"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstring>
+
+#include "gol/backend.hpp"
+#include "gol/parallel.hpp"
+
+namespace gol {
+namespace {
+
+struct Fd {
+  int fd = -1;
+  ~Fd() {
+    if (fd >= 0) ::close(fd);
+  }
+};
+
+[[noreturn]] void sys_fail(const std::string& what, const std::string& path) {
+  fail(what + " '" + path + "': " + std::strerror(errno));
+}
+
+void pread_all(int fd, void* buf, size_t n, int64_t off, const std::string& path) {
+  auto* p = static_cast<uint8_t*>(buf);
+  while (n > 0) {
+    ssize_t r = ::pread(fd, p, n, off);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      sys_fail("read", path);
+    }
+    if (r == 0) fail("input file '" + path + "' is too short for the requested grid");
+    p += r;
+    n -= size_t(r);
+    off += r;
+  }
+}
+
+void pwrite_all(int fd, const void* buf, size_t n, int64_t off, const std::string& path) {
+  auto* p = static_cast<const uint8_t*>(buf);
+  while (n > 0) {
+    ssize_t r = ::pwrite(fd, p, n, off);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      sys_fail("write", path);
+    }
+    p += r;
+    n -= size_t(r);
+    off += r;
+  }
+}
+
+inline uint8_t cell_of(uint8_t ch) { return ch == '1' ? 1 : 0; }
+
+}  // namespace
+
+void read_text_tile(const std::string& path, int64_t W, int64_t H, Extent rows, Extent cols,
+                    std::vector<uint8_t>& out) {
+  GOL_REQUIRE(W > 0 && H > 0, "grid dimensions must be positive");
+  GOL_REQUIRE(rows.begin >= 0 && rows.end <= H && cols.begin >= 0 && cols.end <= W, "tile out of range");
+  Fd f;
+  f.fd = ::open(path.c_str(), O_RDONLY);
+  if (f.fd < 0) sys_fail("cannot open input", path);
+  struct stat st;
+  if (::fstat(f.fd, &st) != 0) sys_fail("cannot stat input", path);
+  const int64_t size = st.st_size;
+  const int64_t nr = rows.size(), nc = cols.size();
+  out.assign(size_t(nr * nc), 0);
+  const int64_t exact = H * (W + 1);
+
+  if (size == exact || size == exact - 1) {
+    // Exact layout: parallel pread of each row's subarray (MPI-IO view math).
+    std::atomic<bool> bad{false};
+    global_pool().parallel_for(nr, [&](int64_t b, int64_t e) {
+      std::vector<uint8_t> line(size_t(nc + 1));
+      for (int64_t i = b; i < e && !bad.load(); ++i) {
+        const int64_t r = rows.begin + i;
+        const int64_t off = r * (W + 1) + cols.begin;
+        bool want_nl = cols.end == W && off + nc < size;
+        pread_all(f.fd, line.data(), size_t(nc + (want_nl ? 1 : 0)), off, path);
+        if (want_nl && line[size_t(nc)] != '\n') {
+          bad = true;
+          break;
+        }
+        uint8_t* dst = &out[size_t(i * nc)];
+        for (int64_t x = 0; x < nc; ++x) dst[x] = cell_of(line[size_t(x)]);
+      }
+    }, 64);
+    if (!bad.load()) return;
+  }
+  // Sequential fallback with the reference's fgetc semantics (skip '\n'; we
+  // also skip '\r' so CRLF files work): cells are the first W*H other bytes.
+  std::vector<uint8_t> data(static_cast<size_t>(size));
+  if (size > 0) pread_all(f.fd, data.data(), size_t(size), 0, path);
+  int64_t k = 0;
+  const int64_t need = W * H;
+  for (int64_t i = 0; i < size && k < need; ++i) {
+    uint8_t ch = data[size_t(i)];
+    if (ch == '\n' || ch == '\r') continue;
+    int64_t r = k / W, x = k % W;
+    if (r >= rows.begin && r < rows.end && x >= cols.begin && x < cols.end)
+      out[size_t((r - rows.begin) * nc + (x - cols.begin))] = cell_of(ch);
+    ++k;
+  }
+  if (k < need)
+    fail("input file '" + path + "' holds " + std::to_string(k) + " cells, need " +
+         std::to_string(need) + " (" + std::to_string(W) + "x" + std::to_string(H) + ")");
+}
+
+void create_text_file(const std::string& path, int64_t W, int64_t H) {
+  Fd f;
+  f.fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+  if (f.fd < 0) sys_fail("cannot create output", path);
+  if (::ftruncate(f.fd, H * (W + 1)) != 0) sys_fail("cannot size output", path);
+}
+
+void write_text_tile(const std::string& path, int64_t W, int64_t H, Extent rows, Extent cols,
+                     const uint8_t* cells, int64_t ld) {
+  Fd f;
+  f.fd = ::open(path.c_str(), O_WRONLY);
+  if (f.fd < 0) sys_fail("cannot open output", path);
+  const int64_t nr = rows.size(), nc = cols.size();
+  const bool nl = cols.end == W;
+  (void)H;
+  global_pool().parallel_for(nr, [&](int64_t b, int64_t e) {
+    // Batch consecutive rows when the tile spans the full width (contiguous).
+    std::vector<uint8_t> buf;
+    for (int64_t i = b; i < e; ++i) {
+      buf.resize(size_t(nc + (nl ? 1 : 0)));
+      const uint8_t* src = cells + i * ld;
+      for (int64_t x = 0; x < nc; ++x) buf[size_t(x)] = uint8_t('0' + (src[x] == 1 || src[x] == '1'));
+      if (nl) buf[size_t(nc)] = '\n';
+      pwrite_all(f.fd, buf.data(), buf.size(), (rows.begin + i) * (W + 1) + cols.begin, path);
+    }
+  }, 64);
+}
+
+void generate_text_file(const std::string& path, int64_t W, int64_t H, uint64_t seed,
+                        double density) {
+  create_text_file(path, W, H);
+  Fd f;
+  f.fd = ::open(path.c_str(), O_WRONLY);
+  if (f.fd < 0) sys_fail("cannot open output", path);
+  const uint32_t th = density_thresh(density);
+  global_pool().parallel_for(H, [&](int64_t b, int64_t e) {
+    std::vector<uint8_t> buf(size_t(W + 1));
+    for (int64_t r = b; r < e; ++r) {
+      for (int64_t x = 0; x < W; ++x) buf[size_t(x)] = uint8_t('0' + rng_cell(seed, r, x, th));
+      buf[size_t(W)] = '\n';
+      pwrite_all(f.fd, buf.data(), buf.size(), r * (W + 1), path);
+    }
+  }, 16);
+}
+
+}  // namespace gol

@@ -1,0 +1,99 @@
+#include "gol/transport.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "gol/backend.hpp"
+#include "gol/common.hpp"
+
+namespace gol {
+
+void SelfTransport::exchange(const std::vector<P2POp>& ops, void*) {
+  GOL_REQUIRE(ops.empty(), "SelfTransport cannot exchange with other ranks");
+}
+
+ThreadHub::ThreadHub(int nranks) : red(), n_(nranks) { GOL_REQUIRE(nranks > 0, "hub size"); }
+
+ThreadTransport::ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, Backend* backend)
+    : hub_(std::move(hub)), rank_(rank), backend_(backend) {}
+
+// Rendezvous exchange: sends publish the sender's buffer, the receiver copies
+// straight out of it (device-to-device for HIP backends on one device) and
+// marks it consumed; the sender returns once all its messages are consumed.
+void ThreadTransport::exchange(const std::vector<P2POp>& ops, void*) {
+  backend_->synchronize();  // sender data must be complete before publishing
+  std::vector<std::shared_ptr<ThreadHub::Msg>> sent;
+  {
+    std::lock_guard<std::mutex> lk(hub_->mu);
+    for (const auto& op : ops) {
+      if (!op.send) continue;
+      auto m = std::make_shared<ThreadHub::Msg>();
+      m->buf = op.buf;
+      m->bytes = op.bytes;
+      hub_->queues[{rank_, op.peer}].push_back(m);
+      sent.push_back(m);
+    }
+  }
+  hub_->cv.notify_all();
+  for (const auto& op : ops) {
+    if (op.send) continue;
+    std::shared_ptr<ThreadHub::Msg> m;
+    {
+      std::unique_lock<std::mutex> lk(hub_->mu);
+      auto& q = hub_->queues[{op.peer, rank_}];
+      hub_->cv.wait(lk, [&] { return !q.empty(); });
+      m = q.front();
+      q.pop_front();
+    }
+    GOL_REQUIRE(m->bytes == op.bytes, "thread transport: message size mismatch (" +
+                                          std::to_string(m->bytes) + " vs " +
+                                          std::to_string(op.bytes) + ")");
+    backend_->copy_2d_async(op.buf, int64_t(op.bytes), m->buf, int64_t(op.bytes), int64_t(op.bytes), 1);
+    backend_->synchronize();
+    {
+      std::lock_guard<std::mutex> lk(hub_->mu);
+      m->consumed = true;
+    }
+    hub_->cv.notify_all();
+  }
+  std::unique_lock<std::mutex> lk(hub_->mu);
+  hub_->cv.wait(lk, [&] {
+    return std::all_of(sent.begin(), sent.end(), [](const auto& m) { return m->consumed; });
+  });
+}
+
+void ThreadTransport::allreduce_max_u32(uint32_t* buf, size_t n, void*) {
+  std::vector<uint32_t> local(n);
+  backend_->copy_d2h(local.data(), buf, n * sizeof(uint32_t));
+  std::unique_lock<std::mutex> lk(hub_->mu);
+  uint64_t gen = hub_->generation;
+  if (hub_->arrived == 0) hub_->red.assign(n, 0u);
+  GOL_REQUIRE(hub_->red.size() == n, "thread allreduce: size mismatch");
+  for (size_t i = 0; i < n; ++i) hub_->red[i] = std::max(hub_->red[i], local[i]);
+  if (++hub_->arrived == hub_->size()) {
+    hub_->arrived = 0;
+    ++hub_->generation;
+    hub_->cv.notify_all();
+  } else {
+    hub_->cv.wait(lk, [&] { return hub_->generation != gen; });
+  }
+  local = hub_->red;
+  lk.unlock();
+  // Everybody must have read `red` before the next reduction resets it.
+  barrier();
+  backend_->copy_h2d(buf, local.data(), n * sizeof(uint32_t));
+}
+
+void ThreadTransport::barrier() {
+  std::unique_lock<std::mutex> lk(hub_->mu);
+  uint64_t gen = hub_->generation;
+  if (++hub_->arrived == hub_->size()) {
+    hub_->arrived = 0;
+    ++hub_->generation;
+    hub_->cv.notify_all();
+  } else {
+    hub_->cv.wait(lk, [&] { return hub_->generation != gen; });
+  }
+}
+
+}  // namespace gol

@@ -1,0 +1,97 @@
+// RCCL transport: halo exchange with grouped ncclSend/ncclRecv and the
+// termination-flag MAX all-reduce, enqueued on the engine's HIP stream.
+//
+// Replaces the reference's MPI layer (src/game_mpi.c:340-401 persistent
+// Send_init/Recv_init + Startall/Waitall every generation, and
+// MPI_Allreduce in empty_all/similarity_all, src/game_mpi.c:104-143).  On an
+// MI355X node every GPU pair has a direct xGMI link, so a 1 x P row-strip
+// exchange is 2 sends + 2 receives per epoch, one hop each; halo messages
+// are a few hundred KB, i.e. latency-bound, which is why the engine
+// exchanges Dv rows once per Dv generations instead of 1 row per generation.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+
+#include "gol/common.hpp"
+#include "gol/transport.hpp"
+
+#define NCCL_CHECK(expr)                                                                      \
+  do {                                                                                        \
+    ncclResult_t r_ = (expr);                                                                 \
+    if (r_ != ncclSuccess)                                                                    \
+      ::gol::fail(std::string("RCCL error in ") + __FILE__ + ":" + std::to_string(__LINE__) + \
+                  " (" #expr "): " + ncclGetErrorString(r_));                                 \
+  } while (0)
+
+namespace gol {
+namespace {
+
+class RcclTransport final : public Transport {
+ public:
+  RcclTransport(const std::vector<uint8_t>& uid, int rank, int nranks, int device)
+      : rank_(rank), size_(nranks), dev_(device) {
+    GOL_REQUIRE(uid.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size");
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    if (hipSetDevice(dev_) != hipSuccess) fail("hipSetDevice failed for RCCL transport");
+    NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+    if (hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking) != hipSuccess)
+      fail("hipStreamCreate failed");
+    if (hipMalloc(&barrier_buf_, 64) != hipSuccess) fail("hipMalloc failed");
+  }
+  ~RcclTransport() override {
+    hipSetDevice(dev_);
+    if (barrier_buf_) hipFree(barrier_buf_);
+    if (barrier_stream_) hipStreamDestroy(barrier_stream_);
+    if (comm_) ncclCommDestroy(comm_);
+  }
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  const char* name() const override { return "rccl"; }
+
+  void exchange(const std::vector<P2POp>& ops, void* stream) override {
+    auto s = static_cast<hipStream_t>(stream);
+    NCCL_CHECK(ncclGroupStart());
+    for (const auto& op : ops) {
+      if (op.send)
+        NCCL_CHECK(ncclSend(op.buf, op.bytes, ncclUint8, op.peer, comm_, s));
+      else
+        NCCL_CHECK(ncclRecv(op.buf, op.bytes, ncclUint8, op.peer, comm_, s));
+    }
+    NCCL_CHECK(ncclGroupEnd());
+  }
+  void allreduce_max_u32(uint32_t* buf, size_t n, void* stream) override {
+    NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, comm_, static_cast<hipStream_t>(stream)));
+  }
+  void barrier() override {
+    NCCL_CHECK(ncclAllReduce(barrier_buf_, barrier_buf_, 1, ncclUint32, ncclMax, comm_, barrier_stream_));
+    if (hipStreamSynchronize(barrier_stream_) != hipSuccess) fail("RCCL barrier failed");
+  }
+
+ private:
+  int rank_, size_, dev_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t barrier_stream_ = nullptr;
+  void* barrier_buf_ = nullptr;
+};
+
+}  // namespace
+
+std::vector<uint8_t> rccl_unique_id() {
+  ncclUniqueId id;
+  NCCL_CHECK(ncclGetUniqueId(&id));
+  std::vector<uint8_t> v(sizeof(id));
+  std::memcpy(v.data(), &id, sizeof(id));
+  return v;
+}
+
+bool rccl_available() { return true; }
+
+std::unique_ptr<Transport> make_rccl_transport(const std::vector<uint8_t>& uid, int rank, int nranks,
+                                               int device) {
+  return std::make_unique<RcclTransport>(uid, rank, nranks, device);
+}
+
+}  // namespace gol

@@ -1,0 +1,313 @@
+// gol: command-line front end, contract-compatible with the reference's
+// `./a.out <width> <height> <input_file>` (README.md:50-57, src/game.c:224-245).
+//
+//   gol 1024 1024 input.txt                 # like the serial build
+//   gol 32768 32768 --random 7 --gpus 8     # 8 GPUs in one process
+//   gol 96 96 in.txt --engine ref           # exact serial src/game.c loop
+//
+// Width/height default to 30 when <= 0 (src/game.c:233-236); without an
+// input file (and no --random) nothing runs and only "Finished" is printed
+// (src/game.c:238-241).  The compile-time knobs of the reference
+// (GEN_LIMIT, CHECK_SIMILARITY, SIMILARITY_FREQUENCY: README.md:65) are
+// runtime flags with the same defaults.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gol/backend.hpp"
+#include "gol/cpu_ref.hpp"
+#include "gol/engine.hpp"
+#include "gol/io.hpp"
+#include "gol/transport.hpp"
+
+using namespace gol;
+
+namespace {
+
+struct Options {
+  int64_t W = 0, H = 0;
+  std::string input;
+  std::string engine = "auto";  // auto | hip | cpu | ref
+  std::string layout = "auto";  // auto | bits | u8
+  std::string decomp = "auto";
+  std::string comm = "thread";  // thread | rccl (in-process ranks)
+  std::string output = "./game_output.out";
+  std::string style = "serial";  // serial | mpi | openmp | cuda
+  std::string metrics;
+  int64_t gens = 1000;
+  int sim_freq = 3;
+  bool similarity = true;
+  bool random = false;
+  uint64_t seed = 1;
+  double density = 0.5;
+  int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0;
+  bool show = false;
+};
+
+[[noreturn]] void usage(int code) {
+  std::fprintf(code ? stderr : stdout,
+               "usage: gol [width] [height] [input_file] [options]\n"
+               "  --engine auto|hip|cpu|ref   compute engine (ref = exact serial game.c loop)\n"
+               "  --layout auto|bits|u8       cell storage (bits needs width %% 32 == 0)\n"
+               "  --gens N                    GEN_LIMIT (default 1000)\n"
+               "  --sim-freq F                SIMILARITY_FREQUENCY (default 3)\n"
+               "  --no-similarity             disable the similarity check\n"
+               "  --random SEED[:DENSITY]     random initial grid instead of an input file\n"
+               "  --output PATH|none          output file (default ./game_output.out)\n"
+               "  --gpus N                    run on N GPUs in this process (one rank each)\n"
+               "  --ranks N                   in-process ranks (subdomains; share devices)\n"
+               "  --comm thread|rccl          in-process halo transport\n"
+               "  --decomp auto|PxQ           process grid (Px columns x Py rows)\n"
+               "  --tmax T --epoch D --poll N temporal block, halo depth, poll interval\n"
+               "  --threads N                 host threads for the cpu engine\n"
+               "  --style serial|mpi|openmp|cuda   stdout format of the matching reference build\n"
+               "  --metrics-json PATH         write run metrics as JSON\n"
+               "  --show                      print the final grid with VT100 escapes\n");
+  std::exit(code);
+}
+
+Options parse(int argc, char** argv) {
+  Options o;
+  std::vector<std::string> pos;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) usage(2);
+      return argv[++i];
+    };
+    if (a == "-h" || a == "--help") usage(0);
+    else if (a == "--engine") o.engine = next();
+    else if (a == "--layout") o.layout = next();
+    else if (a == "--decomp") o.decomp = next();
+    else if (a == "--comm") o.comm = next();
+    else if (a == "--gens") o.gens = std::atoll(next().c_str());
+    else if (a == "--sim-freq") o.sim_freq = std::atoi(next().c_str());
+    else if (a == "--no-similarity") o.similarity = false;
+    else if (a == "--output") o.output = next();
+    else if (a == "--style") o.style = next();
+    else if (a == "--metrics-json") o.metrics = next();
+    else if (a == "--gpus") o.gpus = std::atoi(next().c_str());
+    else if (a == "--ranks") o.ranks = std::atoi(next().c_str());
+    else if (a == "--threads") o.threads = std::atoi(next().c_str());
+    else if (a == "--tmax") o.tmax = std::atoi(next().c_str());
+    else if (a == "--epoch") o.epoch = std::atoi(next().c_str());
+    else if (a == "--poll") o.poll = std::atoi(next().c_str());
+    else if (a == "--show") o.show = true;
+    else if (a == "--random") {
+      std::string v = next();
+      o.random = true;
+      auto c = v.find(':');
+      o.seed = std::strtoull(v.substr(0, c).c_str(), nullptr, 10);
+      if (c != std::string::npos) o.density = std::atof(v.substr(c + 1).c_str());
+    } else if (!a.empty() && a[0] == '-' && a.size() > 1) {
+      std::fprintf(stderr, "unknown option %s\n", a.c_str());
+      usage(2);
+    } else pos.push_back(a);
+  }
+  if (pos.size() > 0) o.W = std::atoll(pos[0].c_str());
+  if (pos.size() > 1) o.H = std::atoll(pos[1].c_str());
+  if (pos.size() > 2) o.input = pos[2];
+  if (o.W <= 0) o.W = 30;
+  if (o.H <= 0) o.H = 30;
+  if (o.gpus > 0) o.ranks = o.gpus;
+  return o;
+}
+
+void show(const std::vector<uint8_t>& g, int64_t W, int64_t H) {
+  // VT100 viewer (src/game.c:42-58): reverse video for live cells.
+  std::printf("\033[H");
+  for (int64_t y = 0; y < H; ++y) {
+    for (int64_t x = 0; x < W; ++x) std::printf(g[size_t(y * W + x)] ? "\033[07m  \033[m" : "  ");
+    std::printf("\033[E");
+  }
+  std::fflush(stdout);
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+int run(const Options& o) {
+  const bool have_input = o.random || !o.input.empty();
+  if (!have_input) {
+    std::printf("Finished\n");
+    return 0;
+  }
+  std::string engine = o.engine;
+  if (engine == "auto") engine = hip_available() ? "hip" : "cpu";
+  Layout layout = Layout::Bits;
+  if (o.layout == "u8" || (o.layout == "auto" && o.W % 32 != 0)) layout = Layout::U8;
+  else if (o.layout != "auto" && o.layout != "bits") throw Error("unknown layout " + o.layout);
+
+  double read_ms = 0, write_ms = 0;
+  RunResult res;
+  std::vector<uint8_t> final_grid;
+  const bool want_grid = o.output != "none" || o.show;
+
+  if (engine == "ref") {
+    // Exact serial semantics (src/game.c), every generation evaluated eagerly.
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint8_t> grid;
+    if (o.random) {
+      grid.resize(size_t(o.W * o.H));
+      uint32_t th = density_thresh(o.density);
+      for (int64_t r = 0; r < o.H; ++r)
+        for (int64_t x = 0; x < o.W; ++x) grid[size_t(r * o.W + x)] = rng_cell(o.seed, r, x, th);
+    } else {
+      read_text_grid(o.input, o.W, o.H, grid);
+    }
+    read_ms = ms_since(t0);
+    RefResult rr = cpu_reference_run(grid, o.W, o.H, o.gens, o.similarity, o.sim_freq, o.threads);
+    res.generations = rr.generations;
+    res.loop_ms = rr.loop_ms;
+    res.executed = rr.generations;
+    final_grid = std::move(grid);
+    if (o.output != "none") {
+      auto t1 = std::chrono::steady_clock::now();
+      write_text_grid(o.output, o.W, o.H, final_grid.data());
+      write_ms = ms_since(t1);
+    }
+  } else {
+    const int P = std::max(1, o.ranks);
+    EngineConfig cfg;
+    cfg.W = o.W;
+    cfg.H = o.H;
+    cfg.layout = layout;
+    cfg.decomp = o.decomp;
+    cfg.gen_limit = o.gens;
+    cfg.check_similarity = o.similarity;
+    cfg.sim_freq = o.sim_freq;
+    cfg.tmax = o.tmax;
+    cfg.epoch = o.epoch;
+    cfg.poll_gens = o.poll;
+    int ndev = 1;
+    if (engine == "hip") {
+      GOL_REQUIRE(hip_available(), "--engine hip: no HIP device available");
+      ndev = o.gpus > 0 ? o.gpus : 1;
+    }
+    std::vector<std::unique_ptr<Backend>> backends(P);
+    std::vector<std::unique_ptr<Transport>> transports(P);
+    std::vector<std::unique_ptr<Engine>> engines(P);
+    auto hub = std::make_shared<ThreadHub>(P);
+    std::vector<uint8_t> uid;
+    if (o.comm == "rccl" && P > 1) uid = rccl_unique_id();
+    for (int r = 0; r < P; ++r)
+      backends[r] = engine == "hip" ? make_hip_backend(r % ndev) : make_cpu_backend(o.threads > 0 ? o.threads : 0);
+    if (P == 1) {
+      transports[0] = std::make_unique<SelfTransport>();
+    } else if (o.comm == "rccl") {
+      std::vector<std::thread> th;
+      for (int r = 0; r < P; ++r)
+        th.emplace_back([&, r] { transports[r] = make_rccl_transport(uid, r, P, r % ndev); });
+      for (auto& t : th) t.join();
+    } else {
+      for (int r = 0; r < P; ++r) transports[r] = std::make_unique<ThreadTransport>(hub, r, backends[r].get());
+    }
+    for (int r = 0; r < P; ++r) engines[r] = std::make_unique<Engine>(cfg, backends[r].get(), transports[r].get());
+
+    auto par = [&](const std::function<void(int)>& fn) {
+      std::vector<std::thread> th;
+      std::vector<std::string> errs(P);
+      for (int r = 0; r < P; ++r)
+        th.emplace_back([&, r] {
+          try {
+            fn(r);
+          } catch (const std::exception& e) {
+            errs[r] = e.what();
+          }
+        });
+      for (auto& t : th) t.join();
+      for (auto& e : errs)
+        if (!e.empty()) throw Error(e);
+    };
+
+    auto t0 = std::chrono::steady_clock::now();
+    par([&](int r) {
+      Engine& e = *engines[r];
+      if (o.random) {
+        e.init_random(o.seed, o.density);
+      } else {
+        std::vector<uint8_t> tile;
+        read_text_tile(o.input, o.W, o.H, e.rows(), e.cols(), tile);
+        e.load_cells(tile.data(), e.cols().size());
+      }
+    });
+    read_ms = ms_since(t0);
+    std::vector<RunResult> results(P);
+    par([&](int r) { results[r] = engines[r]->run(); });
+    res = results[0];
+    for (auto& rr : results) res.loop_ms = std::max(res.loop_ms, rr.loop_ms);
+
+    if (want_grid) {
+      auto t1 = std::chrono::steady_clock::now();
+      if (o.output != "none") create_text_file(o.output, o.W, o.H);
+      if (o.show) final_grid.assign(size_t(o.W * o.H), 0);
+      par([&](int r) {
+        Engine& e = *engines[r];
+        std::vector<uint8_t> tile(size_t(e.rows().size() * e.cols().size()));
+        e.store_cells(tile.data(), e.cols().size(), false);
+        if (o.output != "none")
+          write_text_tile(o.output, o.W, o.H, e.rows(), e.cols(), tile.data(), e.cols().size());
+        if (o.show)
+          for (int64_t i = 0; i < e.rows().size(); ++i)
+            std::memcpy(&final_grid[size_t((e.rows().begin + i) * o.W + e.cols().begin)],
+                        &tile[size_t(i * e.cols().size())], size_t(e.cols().size()));
+      });
+      write_ms = ms_since(t1);
+    }
+    if (!o.metrics.empty()) {
+      std::ofstream f(o.metrics);
+      double cups = res.loop_ms > 0 ? double(o.W) * double(o.H) * double(res.executed) / (res.loop_ms * 1e-3) : 0;
+      f << "{\"engine\": \"" << engine << "\", \"backend\": \"" << backends[0]->name()
+        << "\", \"layout\": \"" << layout_name(layout) << "\", \"ranks\": " << P
+        << ", \"decomp\": \"" << engines[0]->decomp().describe() << "\", \"W\": " << o.W
+        << ", \"H\": " << o.H << ", \"generations\": " << res.generations
+        << ", \"executed\": " << res.executed << ", \"stop_reason\": \"" << res.stop_reason
+        << "\", \"loop_ms\": " << res.loop_ms << ", \"read_ms\": " << read_ms
+        << ", \"write_ms\": " << write_ms << ", \"cell_updates_per_s\": " << cups
+        << ", \"epoch\": " << engines[0]->epoch_depth() << ", \"tmax\": " << engines[0]->tmax()
+        << ", \"exchanges\": " << res.exchanges << ", \"polls\": " << res.polls
+        << ", \"kernel_launches\": " << res.kernel_launches << "}\n";
+    }
+  }
+
+  // stdout contract of the matching reference build.
+  if (o.style == "mpi" || o.style == "openmp") {
+    std::printf("Reading file:\t%.2lf msecs\n", read_ms);
+    std::printf("Generations:\t%d\n", int(res.generations));
+    std::printf("Execution time:\t%.2lf msecs\n", res.loop_ms);
+    std::printf("Writing file:\t%.2lf msecs\n", write_ms);
+    if (o.style == "mpi")
+      for (int r = 0; r < std::max(1, o.ranks); ++r) std::printf("Finished\n");
+  } else if (o.style == "cuda") {
+    std::printf("Generations:\t%d\n", int(res.generations));
+    std::printf("Execution time:\t%.2f msecs\n", res.loop_ms);
+    std::printf("Finished\n");
+  } else {
+    std::printf("Finished.\n\n");
+    std::printf("Generations:\t%d\n", int(res.generations));
+    std::printf("Execution time:\t%.2f msecs\n", res.loop_ms);
+    std::printf("Finished\n");
+  }
+  std::fflush(stdout);
+  if (o.show && !final_grid.empty()) show(final_grid, o.W, o.H);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  try {
+    return run(parse(argc, argv));
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "gol: error: %s\n", e.what());
+    return 1;
+  }
+}

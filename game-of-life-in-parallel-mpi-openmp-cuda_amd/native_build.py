@@ -1,0 +1,127 @@
+"""Native build driver: compiles the C++ runtime and the CDNA4 HIP kernels.
+
+Everything is built in-tree so the artefacts travel with the repository:
+
+* ``gol_amd/_gol.so`` - pybind11 module (engine, backends, transports, I/O)
+* ``bin/gol``         - CLI with the reference's ``./a.out W H file`` contract
+* ``bin/gol_gen``     - text-grid generator (replaces generate.sh)
+
+Reference build: one compiler call per program, ``-std=c99 -Wall -O3``, nvcc
+with no flags at all (Makefile:7-31).  Here: host C++17 with g++, HIP sources
+with ``hipcc --offload-arch=gfx950`` (CDNA4 only, no other targets), parallel
+incremental compilation, link against HIP + RCCL.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO = PKG_DIR.parent
+CSRC = REPO / "csrc"
+BUILD = REPO / "build" / "obj"
+BIN = REPO / "bin"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("GOL_OFFLOAD_ARCH", "gfx950")
+
+HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/transport.cpp",
+             "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp"]
+HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
+            "kernels/tile_ops.hip"]
+BIND_SRCS = ["src/bindings.cpp"]
+CLI_MAIN = "tools/gol_main.cpp"
+GEN_MAIN = "tools/gol_gen.cpp"
+
+MODULE = PKG_DIR / "_gol.so"
+
+
+def _hipcc() -> str:
+    for c in (ROCM / "bin" / "hipcc", shutil.which("hipcc")):
+        if c and Path(c).exists():
+            return str(c)
+    raise RuntimeError("hipcc not found: the native build needs ROCm (hipcc --offload-arch=gfx950)")
+
+
+def _headers_mtime() -> float:
+    m = 0.0
+    for p in list(CSRC.rglob("*.hpp")) + list(CSRC.rglob("*.h")):
+        m = max(m, p.stat().st_mtime)
+    return m
+
+
+def _compile_cmd(src: Path, obj: Path) -> list[str]:
+    inc = [f"-I{CSRC / 'include'}", f"-I{CSRC}"]
+    if src.suffix == ".hip":
+        return [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+                "-Wall", "-Wno-unused-result", "-munsafe-fp-atomics", *inc, f"-I{ROCM / 'include'}",
+                "-c", str(src), "-o", str(obj)]
+    extra = []
+    if src.name == "bindings.cpp":
+        import pybind11  # noqa: PLC0415
+        extra = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+                 "-fvisibility=hidden"]
+    return ["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread", *inc, *extra,
+            "-c", str(src), "-o", str(obj)]
+
+
+def _needs(obj: Path, src: Path, hdr_mtime: float) -> bool:
+    if not obj.exists():
+        return True
+    om = obj.stat().st_mtime
+    return om < src.stat().st_mtime or om < hdr_mtime
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> dict[str, Path]:
+    """Compile (incrementally) and link the module and the CLI tools."""
+    BUILD.mkdir(parents=True, exist_ok=True)
+    BIN.mkdir(parents=True, exist_ok=True)
+    hdr = _headers_mtime()
+    srcs = HOST_SRCS + HIP_SRCS + BIND_SRCS + [CLI_MAIN, GEN_MAIN]
+    objs = {s: BUILD / (s.replace("/", "_") + ".o") for s in srcs}
+    todo = [s for s in srcs if force or _needs(objs[s], CSRC / s, hdr)]
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]
+        for f in futs:
+            f.result()
+    core = [str(objs[s]) for s in HOST_SRCS + HIP_SRCS]
+    rocm_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}", "-pthread"]
+    outs = {
+        "module": MODULE,
+        "gol": BIN / "gol",
+        "gol_gen": BIN / "gol_gen",
+    }
+    relink = bool(todo) or force or any(not p.exists() for p in outs.values())
+    if relink:
+        _run([_hipcc(), "-shared", "-fPIC", *core, str(objs[BIND_SRCS[0]]), "-o", str(MODULE), *rocm_libs],
+             verbose)
+        _run([_hipcc(), *core, str(objs[CLI_MAIN]), "-o", str(outs["gol"]), *rocm_libs], verbose)
+        _run([_hipcc(), *core, str(objs[GEN_MAIN]), "-o", str(outs["gol_gen"]), *rocm_libs], verbose)
+    return outs
+
+
+def is_built() -> bool:
+    if not MODULE.exists():
+        return False
+    hdr = _headers_mtime()
+    newest = max([(CSRC / s).stat().st_mtime for s in HOST_SRCS + HIP_SRCS + BIND_SRCS] + [hdr])
+    return MODULE.stat().st_mtime >= newest
+
+
+if __name__ == "__main__":
+    out = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
+    for k, v in out.items():
+        print(f"{k}: {v}")
