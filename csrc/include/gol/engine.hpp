@@ -83,6 +83,9 @@ class Engine {
   // Runs from the current generation up to config().gen_limit with the
   // reference's termination semantics.
   RunResult run();
+  // Same, but stops at `limit` (<= gen_limit) - used for chunked runs with
+  // checkpoints; the result's generation count is relative to `limit`.
+  RunResult run_until(int64_t limit);
   // Runs exactly n more generations (termination flags still recorded, but
   // no early stop): the bench path.
   RunResult advance(int64_t n);

@@ -40,11 +40,11 @@ constexpr int kWaveCols = 62;  // output words per wave (lanes 1..62)
 
 __device__ __forceinline__ uint32_t from_left(uint32_t x) {
   // wave_shr:1 -> lane i receives lane i-1 (lane 0 receives 0)
-  return __builtin_amdgcn_update_dpp(0u, x, 0x138, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(x, 0x138, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t from_right(uint32_t x) {
   // wave_shl:1 -> lane i receives lane i+1 (lane 63 receives 0)
-  return __builtin_amdgcn_update_dpp(0u, x, 0x130, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(x, 0x130, 0xF, 0xF, true);
 }
 
 template <unsigned TT>
@@ -76,7 +76,8 @@ __device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, 
 // ---- storage layouts -------------------------------------------------------
 struct BitsIO {
   __device__ static __forceinline__ uint32_t load(const uint8_t* row, int col, bool ok) {
-    return ok ? reinterpret_cast<const uint32_t*>(row)[col] : 0u;
+    const uint32_t w = reinterpret_cast<const uint32_t*>(row)[col];  // col is clamped in-bounds
+    return ok ? w : 0u;
   }
   __device__ static __forceinline__ void store(uint8_t* row, int col, uint32_t w) {
     reinterpret_cast<uint32_t*>(row)[col] = w;
@@ -88,7 +89,6 @@ struct U8IO {
   // (x_{2j} | x_{2j+1} << 4) dotted with bytes (1,2,4,8) is the 8-bit pattern
   // of cells 8j..8j+7.
   __device__ static __forceinline__ uint32_t load(const uint8_t* row, int col, bool ok) {
-    if (!ok) return 0u;
     const uint4* p = reinterpret_cast<const uint4*>(row + 32 * col);
     const uint4 q0 = p[0];
     const uint4 q1 = p[1];
@@ -97,7 +97,8 @@ struct U8IO {
     const uint32_t b1 = __builtin_amdgcn_udot4(q0.z | (q0.w << 4), kW, 0u, false);
     const uint32_t b2 = __builtin_amdgcn_udot4(q1.x | (q1.y << 4), kW, 0u, false);
     const uint32_t b3 = __builtin_amdgcn_udot4(q1.z | (q1.w << 4), kW, 0u, false);
-    return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    const uint32_t w = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    return ok ? w : 0u;
   }
   // nibble n -> bytes (n&1, n>>1&1, n>>2&1, n>>3&1): n * 0x204081 puts bit i
   // at bit 8i (plus non-colliding cross terms), masked by 0x01010101.
@@ -158,6 +159,7 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
 
   const int col = kcol * kWaveCols - 1 + lane;
   const bool col_ok = col >= 0 && col < p.Wp;
+  const int lcol = min(max(col, 0), p.Wp - 1);  // clamped load column (value discarded if !col_ok)
   const bool out_lane = col_ok && lane >= 1 && lane <= kWaveCols;
   uint32_t fmask = 0;
   if (out_lane && col >= p.own_w0 && col < p.own_w1)
@@ -179,15 +181,15 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
   int k = 0;
   constexpr int kPro = 2 * T;
   for (; k + 3 <= kPro; k += 3) {
-    row_step<T, 0, true>(st, IO::load(in + (k + 0) * pitch, col, col_ok), k + 0);
-    row_step<T, 1, true>(st, IO::load(in + (k + 1) * pitch, col, col_ok), k + 1);
-    row_step<T, 2, true>(st, IO::load(in + (k + 2) * pitch, col, col_ok), k + 2);
+    row_step<T, 0, true>(st, IO::load(in + (k + 0) * pitch, lcol, col_ok), k + 0);
+    row_step<T, 1, true>(st, IO::load(in + (k + 1) * pitch, lcol, col_ok), k + 1);
+    row_step<T, 2, true>(st, IO::load(in + (k + 2) * pitch, lcol, col_ok), k + 2);
   }
   if constexpr (kPro % 3 >= 1) {
-    row_step<T, 0, true>(st, IO::load(in + (k + 0) * pitch, col, col_ok), k + 0);
+    row_step<T, 0, true>(st, IO::load(in + (k + 0) * pitch, lcol, col_ok), k + 0);
   }
   if constexpr (kPro % 3 >= 2) {
-    row_step<T, 1, true>(st, IO::load(in + (k + 1) * pitch, col, col_ok), k + 1);
+    row_step<T, 1, true>(st, IO::load(in + (k + 1) * pitch, lcol, col_ok), k + 1);
   }
   k = kPro;
 
@@ -195,18 +197,18 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
   constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
   const int kend = kPro + int(o1 - o0);
   for (; k + 3 <= kend; k += 3) {
-    uint32_t w0 = row_step<T, S0, false>(st, IO::load(in + (k + 0) * pitch, col, col_ok), 0);
+    uint32_t w0 = row_step<T, S0, false>(st, IO::load(in + (k + 0) * pitch, lcol, col_ok), 0);
     if (out_lane) IO::store(out + int64_t(k + 0 - T) * pitch, col, w0);
-    uint32_t w1 = row_step<T, S1, false>(st, IO::load(in + (k + 1) * pitch, col, col_ok), 0);
+    uint32_t w1 = row_step<T, S1, false>(st, IO::load(in + (k + 1) * pitch, lcol, col_ok), 0);
     if (out_lane) IO::store(out + int64_t(k + 1 - T) * pitch, col, w1);
-    uint32_t w2 = row_step<T, S2, false>(st, IO::load(in + (k + 2) * pitch, col, col_ok), 0);
+    uint32_t w2 = row_step<T, S2, false>(st, IO::load(in + (k + 2) * pitch, lcol, col_ok), 0);
     if (out_lane) IO::store(out + int64_t(k + 2 - T) * pitch, col, w2);
   }
   if (k < kend) {
-    uint32_t w0 = row_step<T, S0, false>(st, IO::load(in + (k + 0) * pitch, col, col_ok), 0);
+    uint32_t w0 = row_step<T, S0, false>(st, IO::load(in + (k + 0) * pitch, lcol, col_ok), 0);
     if (out_lane) IO::store(out + int64_t(k + 0 - T) * pitch, col, w0);
     if (k + 1 < kend) {
-      uint32_t w1 = row_step<T, S1, false>(st, IO::load(in + (k + 1) * pitch, col, col_ok), 0);
+      uint32_t w1 = row_step<T, S1, false>(st, IO::load(in + (k + 1) * pitch, lcol, col_ok), 0);
       if (out_lane) IO::store(out + int64_t(k + 1 - T) * pitch, col, w1);
     }
   }

@@ -243,6 +243,7 @@ PYBIND11_MODULE(_gol, m) {
       .def("alive_count", &Engine::alive_count, py::call_guard<py::gil_scoped_release>())
       .def("run", &Engine::run, py::call_guard<py::gil_scoped_release>())
       .def("advance", &Engine::advance, py::call_guard<py::gil_scoped_release>())
+      .def("run_until", &Engine::run_until, py::call_guard<py::gil_scoped_release>())
       .def("halo_exchange", &Engine::halo_exchange, py::call_guard<py::gil_scoped_release>())
       .def("step_block", &Engine::step_block, py::call_guard<py::gil_scoped_release>())
       .def("read_text", [](Engine& e, const std::string& path) {

@@ -174,6 +174,10 @@ bool Engine::poll(int64_t from, int64_t to, int64_t* first_unchanged) {
 
 RunResult Engine::run() { return run_impl(cfg_.gen_limit, /*stop_early=*/true); }
 
+RunResult Engine::run_until(int64_t limit) {
+  return run_impl(std::min(limit, cfg_.gen_limit), /*stop_early=*/true);
+}
+
 RunResult Engine::advance(int64_t n) { return run_impl(gen_ + n, /*stop_early=*/false); }
 
 RunResult Engine::run_impl(int64_t limit, bool stop_early) {

@@ -1,0 +1,233 @@
+"""High-level simulation API over the native engine.
+
+The "model" of this framework is the B3/S23 cellular automaton on a periodic
+W x H torus - the single model family of the reference (README.md:4-10): six
+programs (serial, MPI x3, MPI+OpenMP, CUDA) that all evolve the same
+automaton.  Here those six programs are one engine with pluggable pieces:
+
+======================  ==========================================  ==================================
+reference program       this framework                              how to select it
+======================  ==========================================  ==================================
+src/game.c              ``engine="ref"`` (exact eager serial loop)   ``Simulation(..., engine="ref")``
+src/game_openmp.c       ``engine="cpu"`` (threaded bit-sliced)       ``engine="cpu", threads=N``
+src/game_cuda.cu        ``engine="hip"`` (CDNA4 temporal blocking)   ``engine="hip"``
+src/game_mpi*.c         any engine x ``transport=thread|rccl|torch`` ``Simulation.distributed(...)``
+======================  ==========================================  ==================================
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+from typing import Any, Optional
+
+import numpy as np
+
+from .._native import native
+
+
+@dataclasses.dataclass
+class LifeConfig:
+    """Runtime configuration; defaults equal the reference's compile-time
+    constants (GEN_LIMIT 1000, CHECK_SIMILARITY on, SIMILARITY_FREQUENCY 3:
+    src/game.c:6-9)."""
+
+    width: int
+    height: int
+    gen_limit: int = 1000
+    check_similarity: bool = True
+    sim_freq: int = 3
+    layout: str = "auto"        # auto | bits | u8
+    decomp: str = "auto"        # auto | PxQ
+    tmax: int = 0               # generations per kernel launch (0 = default 16)
+    epoch: int = 0              # generations per halo exchange (0 = 4*tmax)
+    poll_gens: int = 0          # generations between termination polls (0 = 256)
+    start_gen: int = 0          # resume: generation number of the initial state
+    sim_phase: int = 0          # resume: similarity counter at start_gen
+
+    def resolved_layout(self) -> str:
+        if self.layout == "auto":
+            return "bits" if self.width % 32 == 0 else "u8"
+        if self.layout not in ("bits", "u8"):
+            raise ValueError(f"unknown layout {self.layout!r}")
+        return self.layout
+
+    def to_native(self):
+        C = native()
+        c = C.EngineConfig()
+        c.W = int(self.width)
+        c.H = int(self.height)
+        c.layout = C.Layout.Bits if self.resolved_layout() == "bits" else C.Layout.U8
+        c.decomp = self.decomp
+        c.gen_limit = int(self.gen_limit)
+        c.check_similarity = bool(self.check_similarity)
+        c.sim_freq = int(self.sim_freq)
+        c.tmax = int(self.tmax)
+        c.epoch = int(self.epoch)
+        c.poll_gens = int(self.poll_gens)
+        c.start_gen = int(self.start_gen)
+        c.sim_phase = int(self.sim_phase)
+        return c
+
+
+def make_backend(engine: str = "auto", device: int = 0, threads: int = 0):
+    """``hip`` -> MI355X backend on ``device``; ``cpu`` -> threaded host backend."""
+    C = native()
+    if engine == "auto":
+        engine = "hip" if C.hip_available() else "cpu"
+    if engine == "hip":
+        return C.hip_backend(int(device))
+    if engine == "cpu":
+        return C.cpu_backend(int(threads))
+    raise ValueError(f"unknown engine {engine!r} (want hip, cpu or auto)")
+
+
+@dataclasses.dataclass
+class RunReport:
+    generations: int
+    executed: int
+    stop_reason: str
+    loop_ms: float
+    first_unchanged: int = -1
+    extinct: bool = False
+    exchanges: int = 0
+    polls: int = 0
+    kernel_launches: int = 0
+    cells: int = 0
+
+    @property
+    def cell_updates_per_s(self) -> float:
+        return self.cells * self.executed / (self.loop_ms * 1e-3) if self.loop_ms > 0 else 0.0
+
+    def as_dict(self) -> dict[str, Any]:
+        d = dataclasses.asdict(self)
+        d["cell_updates_per_s"] = self.cell_updates_per_s
+        return d
+
+
+class Simulation:
+    """One rank's view of a (possibly decomposed) Game of Life run.
+
+    Single GPU / CPU::
+
+        sim = Simulation(LifeConfig(1024, 1024), engine="hip")
+        sim.load(grid)                    # numpy uint8 H x W (0/1 or ASCII)
+        report = sim.run()                # reference termination semantics
+        out = sim.gather()                # final grid (rank-local tile if distributed)
+    """
+
+    def __init__(self, config: LifeConfig, engine: str = "auto", device: int = 0, threads: int = 0,
+                 transport=None, backend=None):
+        C = native()
+        self.config = config
+        self.engine_name = engine
+        self.backend = backend if backend is not None else make_backend(engine, device, threads)
+        self.transport = transport if transport is not None else C.self_transport()
+        self._eng = C.Engine(config.to_native(), self.backend, self.transport)
+        self.last_report: Optional[RunReport] = None
+
+    # -- geometry --------------------------------------------------------
+    @property
+    def rank(self) -> int:
+        return self._eng.rank
+
+    @property
+    def rows(self) -> tuple[int, int]:
+        r = self._eng.rows
+        return (r.begin, r.end)
+
+    @property
+    def cols(self) -> tuple[int, int]:
+        c = self._eng.cols
+        return (c.begin, c.end)
+
+    @property
+    def generation(self) -> int:
+        return self._eng.generation
+
+    @property
+    def native_engine(self):
+        return self._eng
+
+    @property
+    def epoch_depth(self) -> int:
+        return self._eng.epoch_depth
+
+    def describe(self) -> dict[str, Any]:
+        d = self._eng.decomp
+        g = self._eng.geom
+        return {"backend": self.backend.name(), "transport": self.transport.name(),
+                "layout": self.config.resolved_layout(), "decomp": d.describe(),
+                "rank": self.rank, "ranks": d.nranks(), "tile_rows": g.H, "tile_cols": g.W,
+                "halo_rows": g.Dv, "halo_words": g.hw, "tmax": self._eng.tmax,
+                "epoch": self._eng.epoch_depth, "pitch": g.pitch}
+
+    # -- state -----------------------------------------------------------
+    def load(self, grid: np.ndarray) -> None:
+        """Load the full global grid (each rank copies out its own tile)."""
+        g = np.ascontiguousarray(grid, dtype=np.uint8)
+        self._eng.load_global(g)
+
+    def load_tile(self, tile: np.ndarray) -> None:
+        self._eng.load_cells(np.ascontiguousarray(tile, dtype=np.uint8))
+
+    def load_text(self, path: str) -> None:
+        """Parallel subarray read of a text grid (MPI-IO view equivalent)."""
+        self._eng.read_text(str(path))
+
+    def init_random(self, seed: int = 1, density: float = 0.5) -> None:
+        """Counter-based random init on the device (independent of layout and
+        decomposition; equal to ``gol_gen`` / ``generate_text``)."""
+        self._eng.init_random(int(seed), float(density))
+
+    def tile(self, ascii: bool = False) -> np.ndarray:
+        return self._eng.store_cells(ascii)
+
+    def write_text(self, path: str, create: bool = True) -> None:
+        self._eng.write_text(str(path), create)
+
+    def alive_count(self) -> int:
+        return int(self._eng.alive_count())
+
+    # -- running ---------------------------------------------------------
+    def _report(self, r) -> RunReport:
+        rep = RunReport(generations=r.generations, executed=r.executed, stop_reason=r.stop_reason,
+                        loop_ms=r.loop_ms, first_unchanged=r.first_unchanged, extinct=r.extinct,
+                        exchanges=r.exchanges, polls=r.polls, kernel_launches=r.kernel_launches,
+                        cells=self.config.width * self.config.height)
+        self.last_report = rep
+        return rep
+
+    def run(self) -> RunReport:
+        """Evolve up to ``gen_limit`` with the reference's termination rules."""
+        return self._report(self._eng.run())
+
+    def advance(self, n: int) -> RunReport:
+        """Evolve exactly ``n`` generations (no early stop)."""
+        return self._report(self._eng.advance(int(n)))
+
+
+def simulate(grid: np.ndarray, gens: int, engine: str = "auto", layout: str = "auto",
+             check_similarity: bool = True, sim_freq: int = 3, **kw) -> tuple[np.ndarray, RunReport]:
+    """Convenience: run a grid to ``gens`` (reference semantics) on one rank."""
+    grid = np.ascontiguousarray(grid, dtype=np.uint8)
+    H, W = grid.shape
+    cfg = LifeConfig(W, H, gen_limit=gens, check_similarity=check_similarity, sim_freq=sim_freq,
+                     layout=layout, **kw)
+    sim = Simulation(cfg, engine=engine)
+    sim.load(grid)
+    rep = sim.run()
+    return sim.tile(), rep
+
+
+def reference_run(grid: np.ndarray, gen_limit: int = 1000, check_similarity: bool = True,
+                  sim_freq: int = 3, threads: int = 1) -> tuple[np.ndarray, int, float]:
+    """Exact eager serial loop of src/game.c (native).  Returns (grid, gens, ms)."""
+    gens, ms, out = native().cpu_reference_run(np.ascontiguousarray(grid, dtype=np.uint8), int(gen_limit),
+                                               bool(check_similarity), int(sim_freq), int(threads))
+    return out, int(gens), float(ms)
+
+
+def timed(fn, *a, **kw):
+    t0 = time.perf_counter()
+    r = fn(*a, **kw)
+    return r, (time.perf_counter() - t0) * 1e3

@@ -1,0 +1,159 @@
+"""Multi-process runs: one process per GPU, torch.distributed bootstrap.
+
+Reference: ``MPI_Init`` inside ``game()`` (src/game_mpi.c:158-160), one
+MPICH rank per core, persistent point-to-point halos and Allreduce flags.
+Here every process owns one MI355X (``LOCAL_RANK``), the process group is
+``torch.distributed`` (``nccl`` = RCCL on ROCm, ``gloo`` on CPU) and the halo
+transport is one of:
+
+* ``rccl``  - native RCCL communicator inside the C++ engine; its
+  ``ncclUniqueId`` is created by rank 0 and broadcast through the torch
+  process group.  Halos and flag reductions are enqueued on the engine's
+  HIP stream with no Python on the hot path (default on GPU).
+* ``torch`` - the engine calls back into Python, which runs
+  ``torch.distributed.batch_isend_irecv`` / ``all_reduce`` on zero-copy tensor
+  views of the engine's buffers (works with ``nccl`` and ``gloo``; default
+  on CPU, used by the multi-process CPU tests).
+"""
+from __future__ import annotations
+
+import ctypes
+import datetime
+import os
+from typing import Optional
+
+import numpy as np
+
+from .._native import native
+
+
+def env_rank() -> tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def init_process_group(backend: Optional[str] = None, timeout_s: int = 600):
+    """Initialise torch.distributed from the torchrun environment (idempotent)."""
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+
+    if dist.is_available() and dist.is_initialized():
+        return dist
+    rank, world, local = env_rank()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        kw["device_id"] = torch.device("cuda", local)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return dist
+
+
+# ---------------------------------------------------------------------------
+# Zero-copy tensor views of engine buffers
+# ---------------------------------------------------------------------------
+class _DeviceBuf:
+    """Minimal ``__cuda_array_interface__`` provider for a raw device pointer."""
+
+    def __init__(self, ptr: int, nbytes: int, typestr: str = "|u1", itemsize: int = 1):
+        self.__cuda_array_interface__ = {
+            "shape": (nbytes // itemsize,), "typestr": typestr, "data": (int(ptr), False),
+            "version": 2, "strides": None,
+        }
+
+
+def _host_view(ptr: int, nbytes: int, dtype=np.uint8):
+    buf = (ctypes.c_uint8 * nbytes).from_address(int(ptr))
+    return np.frombuffer(buf, dtype=dtype)
+
+
+def tensor_view(ptr: int, nbytes: int, on_device: bool, dtype: str = "u1"):
+    import torch  # noqa: PLC0415
+
+    if on_device:
+        typestr, item = ("|u1", 1) if dtype == "u1" else ("<i4", 4)
+        return torch.as_tensor(_DeviceBuf(ptr, nbytes, typestr, item), device="cuda")
+    arr = _host_view(ptr, nbytes, np.uint8 if dtype == "u1" else np.int32)
+    return torch.from_numpy(arr)
+
+
+def torch_transport(backend_obj, group=None):
+    """Engine transport implemented with torch.distributed collectives."""
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+
+    on_dev = bool(backend_obj.is_device())
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+
+    def _stream_ctx(stream_ptr: int):
+        if on_dev and stream_ptr:
+            return torch.cuda.stream(torch.cuda.ExternalStream(int(stream_ptr)))
+        import contextlib  # noqa: PLC0415
+        return contextlib.nullcontext()
+
+    def exchange(ops, stream_ptr):
+        with _stream_ctx(stream_ptr):
+            p2p = []
+            for send, peer, addr, nbytes in ops:
+                t = tensor_view(addr, nbytes, on_dev)
+                p2p.append(dist.P2POp(dist.isend if send else dist.irecv, t, int(peer), group))
+            if p2p:
+                for w in dist.batch_isend_irecv(p2p):
+                    w.wait()
+
+    def allreduce(addr, n, stream_ptr):
+        with _stream_ctx(stream_ptr):
+            t = tensor_view(addr, 4 * n, on_dev, dtype="i4")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            if not on_dev:
+                return
+
+    def barrier():
+        dist.barrier(group=group)
+
+    return native().callback_transport(rank, world, exchange, allreduce, barrier)
+
+
+def rccl_transport(device: int, group=None):
+    """Native RCCL communicator, uid broadcast over the torch process group."""
+    import torch.distributed as dist  # noqa: PLC0415
+
+    C = native()
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    obj = [C.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return C.rccl_transport(obj[0], rank, world, int(device))
+
+
+def make_transport(kind: str, backend_obj, device: int = 0):
+    """``self`` (1 rank) | ``rccl`` | ``torch``; ``auto`` -> rccl on GPU, torch on CPU."""
+    import torch.distributed as dist  # noqa: PLC0415
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return native().self_transport()
+    if kind == "auto":
+        kind = "rccl" if backend_obj.is_device() else "torch"
+    if kind == "rccl":
+        return rccl_transport(device)
+    if kind == "torch":
+        return torch_transport(backend_obj)
+    raise ValueError(f"unknown transport {kind!r}")
+
+
+def allreduce_max_float(x: float) -> float:
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -1,0 +1,137 @@
+"""GPU tier (MI355X): the CDNA4 kernels against the PyTorch fp32 oracle and the
+CPU backend, golden semantics on the device, multi-subdomain runs on one GPU
+(T3) and the RCCL / torch.distributed transport plumbing."""
+import numpy as np
+import pytest
+
+from gol_amd import LifeConfig, Simulation, life_step, life_step_numpy, life_step_torch, random_grid, \
+    reference_run, simulate
+from gol_amd.parallel import InProcessGroup
+
+from golden import CASES, CONVERGING, GLIDER
+
+pytestmark = pytest.mark.gpu
+
+
+def test_hip_backend_is_native_gfx950(gpu):
+    be = gpu.hip_backend(0)
+    assert be.is_device()
+    assert "gfx950" in be.name()
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (2, 2), (3, 5), (31, 7), (33, 33), (65, 40), (100, 1), (257, 129)])
+def test_u8_kernel_awkward_sizes_vs_torch(gpu, W, H):
+    g = random_grid(W, H, W * 7 + H)
+    for gens in (1, 3, 17):
+        want = life_step_torch(g, gens, device="cuda")
+        assert (life_step(g, gens, engine="hip", layout="u8") == want).all(), gens
+
+
+@pytest.mark.parametrize("W,H", [(32, 1), (32, 32), (64, 5), (96, 70), (2048, 40), (4000 - 4000 % 32, 130)])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_kernel_word_sizes_vs_torch(gpu, W, H, layout):
+    g = random_grid(W, H, W + H)
+    want = life_step_torch(g, 21, device="cuda")
+    assert (life_step(g, 21, engine="hip", layout=layout) == want).all()
+
+
+@pytest.mark.parametrize("tmax", [1, 2, 4, 8, 16, 32])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_every_temporal_block_size(gpu, tmax, layout):
+    # Wide enough for several column waves (62 words each) and tall enough
+    # for several row segments per wave.
+    W, H = 32 * 200, 700
+    g = random_grid(W, H, tmax)
+    want = life_step_torch(g, 2 * tmax + 3, device="cuda")
+    got = life_step(g, 2 * tmax + 3, engine="hip", layout=layout, tmax=tmax)
+    assert (got == want).all()
+
+
+def test_hip_matches_cpu_backend_long_run(gpu):
+    g = random_grid(1024, 512, 5)
+    a = life_step(g, 300, engine="hip")
+    b = life_step(g, 300, engine="cpu")
+    assert (a == b).all()
+
+
+@pytest.mark.parametrize("name,grid,gens", CASES)
+@pytest.mark.parametrize("layout", ["auto", "u8"])
+def test_golden_patterns_gpu(gpu, name, grid, gens, layout):
+    out, rep = simulate(grid, 1000, engine="hip", layout=layout)
+    ref, rgens, _ = reference_run(grid)
+    assert rep.generations == gens == rgens
+    assert (out == ref).all()
+
+
+def test_glider_gpu(gpu):
+    out, rep = simulate(GLIDER, 1000, engine="hip")
+    assert (out == np.roll(np.roll(GLIDER, 2, 0), 2, 1)).all()
+
+
+@pytest.mark.parametrize("W,H,seed,density", CONVERGING)
+def test_termination_gpu(gpu, W, H, seed, density):
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    for tmax, epoch, poll in [(16, 0, 0), (4, 7, 5), (32, 64, 1000)]:
+        out, rep = simulate(g, 1000, engine="hip", tmax=tmax, epoch=epoch, poll_gens=poll)
+        assert rep.generations == rgens
+        assert (out == ref).all()
+
+
+@pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("2x2", 4), ("2x4", 8), ("3x3", 9)])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_multi_subdomain_one_gpu(gpu, spec, P, layout):
+    W, H = 32 * 12, 300
+    g = random_grid(W, H, 42)
+    want = life_step_numpy(g, 150)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=150, decomp=spec, layout=layout, tmax=16), P,
+                         engine="hip", devices=[0])
+    grp.load(g)
+    reps = grp.run()
+    assert all(r.generations == 150 for r in reps)
+    assert (grp.gather() == want).all()
+
+
+def test_random_init_on_device_matches_host(gpu):
+    s = Simulation(LifeConfig(4096, 100), engine="hip")
+    s.init_random(11, 0.5)
+    assert (s.tile() == random_grid(4096, 100, 11, 0.5)).all()
+    assert s.alive_count() == int(random_grid(4096, 100, 11, 0.5).sum())
+
+
+def test_text_io_on_device(gpu, tmp_path):
+    from gol_amd.utils import io
+
+    p = tmp_path / "in.txt"
+    io.generate(str(p), 300, 200, seed=3)
+    s = Simulation(LifeConfig(300, 200, gen_limit=50), engine="hip")
+    s.load_text(str(p))
+    s.run()
+    out = tmp_path / "out.txt"
+    s.write_text(str(out))
+    ref, _, _ = reference_run(io.read_grid(str(p), 300, 200), 50)
+    assert out.read_text() == io.format_text(ref)
+
+
+def test_rccl_single_rank_self_exchange(gpu):
+    """RCCL transport plumbing on one GPU: a 1-rank communicator with
+    send/recv to itself and a MAX all-reduce."""
+    import torch
+
+    C = gpu
+    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0)
+    assert tr.size() == 1 and tr.name() == "rccl"
+    tr.barrier()
+
+
+def test_torch_tensor_views_of_engine_buffers(gpu):
+    import torch
+
+    from gol_amd.parallel.dist import tensor_view
+
+    x = torch.arange(256, dtype=torch.uint8, device="cuda")
+    v = tensor_view(x.data_ptr(), 256, True)
+    assert v.device.type == "cuda" and v.data_ptr() == x.data_ptr()
+    v[0] = 7
+    torch.cuda.synchronize()
+    assert int(x[0].item()) == 7

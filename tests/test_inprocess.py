@@ -1,0 +1,54 @@
+"""T3 on CPU: several subdomains in one process (ThreadTransport), covering
+pack/unpack, neighbour routing, deep halos and distributed lazy termination.
+The same tests run on one GPU in test_gpu.py."""
+import pytest
+
+from gol_amd import LifeConfig, random_grid, reference_run
+from gol_amd.parallel import InProcessGroup
+
+from golden import CONVERGING
+
+DECOMPS = [("1x2", 2), ("2x1", 2), ("1x4", 4), ("2x2", 4), ("1x8", 8), ("2x4", 8), ("4x2", 8), ("3x3", 9)]
+
+
+@pytest.mark.parametrize("spec,P", DECOMPS)
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_decompositions_match_serial(native, spec, P, layout):
+    W, H = 160, 96
+    g = random_grid(W, H, 1234)
+    ref, rgens, _ = reference_run(g, 120)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=120, decomp=spec, layout=layout, tmax=8), P, engine="cpu")
+    grp.load(g)
+    reps = grp.run()
+    assert all(r.generations == rgens for r in reps)
+    assert (grp.gather() == ref).all()
+
+
+@pytest.mark.parametrize("W,H,seed,density", CONVERGING[:4])
+@pytest.mark.parametrize("spec,P", [("1x2", 2), ("2x2", 4)])
+def test_distributed_termination(native, W, H, seed, density, spec, P):
+    if spec == "2x2" and W < 64:
+        pytest.skip("tiles narrower than 32 cells")
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    grp = InProcessGroup(LifeConfig(W, H, decomp=spec, layout="u8", epoch=3, poll_gens=2), P, engine="cpu")
+    grp.load(g)
+    reps = grp.run()
+    assert {r.generations for r in reps} == {rgens}
+    assert (grp.gather() == ref).all()
+
+
+def test_uneven_tiles_u8(native):
+    W, H = 100, 37  # 100 not a multiple of 32 -> u8 with cell-granular splits
+    g = random_grid(W, H, 5)
+    ref, rgens, _ = reference_run(g, 64)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=64, decomp="1x3", layout="u8", epoch=12), 3, engine="cpu")
+    grp.load(g)
+    grp.run()
+    assert (grp.gather() == ref).all()
+
+
+def test_random_init_decomposition_independent(native):
+    grp = InProcessGroup(LifeConfig(128, 64, decomp="2x2"), 4, engine="cpu")
+    grp.init_random(99)
+    assert (grp.gather() == random_grid(128, 64, 99)).all()

@@ -1,0 +1,81 @@
+"""T0: text I/O contract."""
+import os
+
+import numpy as np
+import pytest
+
+from gol_amd.ops.life_ops import random_grid
+from gol_amd.utils import io
+
+
+def test_roundtrip_and_size(tmp_path, native):
+    g = random_grid(37, 21, 3)
+    p = tmp_path / "g.txt"
+    io.write_grid(str(p), g)
+    assert os.path.getsize(p) == 21 * (37 + 1)  # H*(W+1) bytes
+    txt = p.read_text()
+    assert txt == io.format_text(g)
+    assert (io.read_grid(str(p), 37, 21) == g).all()
+    assert (io.parse_text(txt, 37, 21) == g).all()
+
+
+def test_subarray_reads_match_full(tmp_path, native):
+    W, H = 100, 60
+    p = tmp_path / "g.txt"
+    io.generate(str(p), W, H, seed=9)
+    full = io.read_grid(str(p), W, H)
+    for rows, cols in [((0, H), (0, W)), ((7, 31), (5, 77)), ((59, 60), (99, 100)), ((0, 1), (0, 1))]:
+        t = io.read_tile(str(p), W, H, rows, cols)
+        assert (t == full[rows[0]:rows[1], cols[0]:cols[1]]).all()
+
+
+def test_generator_matches_device_rng(tmp_path, native):
+    p = tmp_path / "g.txt"
+    io.generate(str(p), 64, 16, seed=42, density=0.3)
+    assert (io.read_grid(str(p), 64, 16) == random_grid(64, 16, 42, 0.3)).all()
+    d = random_grid(512, 512, 1, 0.3).mean()
+    assert 0.27 < d < 0.33
+
+
+def test_short_file_is_an_error_not_a_hang(tmp_path, native):
+    # The reference's fgetc loop spins forever on a short file (quirk Q8).
+    p = tmp_path / "short.txt"
+    p.write_text("0101\n0101\n")
+    with pytest.raises(RuntimeError, match="cells"):
+        io.read_grid(str(p), 4, 3)
+
+
+def test_fgetc_semantics_and_crlf(tmp_path, native):
+    # Non-exact layouts are read like the reference's sequential parser: the
+    # first W*H non-newline bytes in order, '1' alive, anything else dead.
+    p = tmp_path / "odd.txt"
+    p.write_text("0110\r\n1x01\r\n0011\r\n")
+    g = io.read_grid(str(p), 4, 3)
+    assert g.tolist() == [[0, 1, 1, 0], [1, 0, 0, 1], [0, 0, 1, 1]]
+    q = tmp_path / "flat.txt"
+    q.write_text("011010010011")  # one line holding all 12 cells
+    assert (io.read_grid(str(q), 4, 3) == g).all()
+
+
+def test_tile_writes_assemble_the_file(tmp_path, native):
+    W, H = 70, 45
+    g = random_grid(W, H, 5)
+    p = tmp_path / "out.txt"
+    io.create_text_file(str(p), W, H)
+    # 2x3 decomposition, written in a scrambled order like independent ranks
+    rows = [(0, 20), (20, 45)]
+    cols = [(0, 30), (30, 50), (50, 70)]
+    for (r0, r1) in rows[::-1]:
+        for (c0, c1) in cols[::-1]:
+            io.write_tile(str(p), W, H, r0, c0, g[r0:r1, c0:c1])
+    assert p.read_text() == io.format_text(g)
+
+
+def test_ascii_and_binary_inputs_equivalent(native):
+    g = random_grid(40, 10, 2)
+    ascii_grid = (g + ord("0")).astype(np.uint8)
+    from gol_amd import reference_run
+
+    a = reference_run(g, 50)[0]
+    b = reference_run(ascii_grid, 50)[0]
+    assert (a == b).all()
