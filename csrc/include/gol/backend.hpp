@@ -42,6 +42,9 @@ class Backend {
 
   // Kernels.
   virtual void run_block(const BlockArgs& a) = 0;
+  // Largest temporal block size (generations per run_block) the backend runs
+  // at full occupancy for this layout; the engine's default tmax.
+  virtual int preferred_tmax(Layout) const { return 16; }
   // Periodic self-fill of halo regions of a single tile (any tile size):
   // columns (left/right halo words of owned rows) and/or rows (full padded
   // rows of the top/bottom halo, which also fills the corners).

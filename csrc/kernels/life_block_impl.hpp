@@ -1,0 +1,491 @@
+// life_block: T generations of B3/S23 in one pass over a tile, on MI355X.
+//
+// What the reference does per generation (src/game_cuda.cu:213-276): five
+// kernel launches (halo_rows, halo_cols, evolve, compare, empty), one thread
+// per cell in 32x32 blocks, nine byte loads per cell from global memory, four
+// device-wide synchronisations and one or two 4-byte D2H copies.
+//
+// What this kernel does instead (CDNA4-first design):
+//   * Cells are processed 32 at a time as bit planes: a lane owns W adjacent
+//     32-cell words of a row; a wave64 owns 64*W adjacent words (the outermost
+//     word on each side is its halo).  The neighbour count is a bit-sliced
+//     adder tree built from v_bitop3_b32 (any 3-input boolean function in ONE
+//     full-rate VALU op on gfx950) and v_alignbit_b32 funnel shifts; the two
+//     bits that cross a lane boundary move with one cross-lane op per side
+//     (DPP wave_shr/wave_shl, or ds_bpermute on the LDS crossbar).  Per word
+//     and generation: 10 bitop3 + 2 alignbit + 2/W cross-lane ops.
+//     Measured on MI355X (csrc/tools/ubench_level.hip): a DPP wave shift costs
+//     ~10 cycles inside a VALU stream vs ~2.5 for bitop3, so the bit layout
+//     uses W=2 words per lane to halve that overhead.
+//   * Temporal blocking in registers: the wave streams down its column strip
+//     one row at a time and carries T generation levels, each with a 3-row
+//     sliding window of horizontal partial sums.  Every input row is read
+//     from HBM once per T generations and every output row written once
+//     (0.03 B/cell-update at T=8 vs 2 B/cell-update for a byte-per-cell
+//     single-step stencil).  Input rows are prefetched 3 row-steps ahead.
+//   * Optional skewed (software-pipelined) level schedule: iteration i
+//     evaluates level L at row step i-L, so the T levels are independent.
+//   * The per-generation "changed" flags that replace the reference's
+//     compare/empty kernels (src/game_cuda.cu:76-126) are fused: one bitop3
+//     per word per level, reduced with __ballot at the end of the wave.
+//   * Two storage layouts share the compute core: Bits (1 bit per cell) and
+//     U8 (1 byte per cell, packed to bits on load with v_dot4_u32_u8 and
+//     unpacked on store with v_mul_u32_u24).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "gol/common.hpp"
+#include "gol/tile.hpp"
+#include "life_kernels.hpp"
+
+
+namespace gol {
+namespace hipk {
+
+namespace lb {
+
+template <unsigned TT>
+__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+}
+
+template <int W>
+struct Vec {
+  uint32_t w[W];
+};
+
+// Words of the neighbouring lanes: lane i gets lane i-1's last word (left)
+// and lane i+1's first word (right).  Edge lanes receive don't-care values;
+// they only feed the wave's halo words.
+template <int XL, int W>
+__device__ __forceinline__ void neighbours(const Vec<W>& c, uint32_t& lw, uint32_t& rw) {
+  if constexpr (XL == kXlaneBpermute) {
+    const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    lw = uint32_t(__builtin_amdgcn_ds_bpermute((lane - 1) * 4, int(c.w[W - 1])));
+    rw = uint32_t(__builtin_amdgcn_ds_bpermute((lane + 1) * 4, int(c.w[0])));
+  } else {
+    lw = __builtin_amdgcn_mov_dpp(c.w[W - 1], 0x138, 0xF, 0xF, true);  // wave_shr:1
+    rw = __builtin_amdgcn_mov_dpp(c.w[0], 0x130, 0xF, 0xF, true);      // wave_shl:1
+  }
+}
+
+// Horizontal 3-sums (h1:h0) = left + centre + right for every word.
+template <int XL, int W>
+__device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1) {
+  uint32_t lw, rw;
+  neighbours<XL>(c, lw, rw);
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const uint32_t lo = i == 0 ? lw : c.w[i - 1];
+    const uint32_t hi = i == W - 1 ? rw : c.w[i + 1];
+    const uint32_t l = __builtin_amdgcn_alignbit(c.w[i], lo, 31);  // cell x-1
+    const uint32_t r = __builtin_amdgcn_alignbit(hi, c.w[i], 1);   // cell x+1
+    h0.w[i] = bop3<tt::XOR3>(l, c.w[i], r);
+    h1.w[i] = bop3<tt::MAJ>(l, c.w[i], r);
+  }
+}
+
+// next = (S == 3) | (ctr & S == 4), S = 3x3 sum (see common.hpp rule_host).
+__device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
+                                         uint32_t c0, uint32_t c1, uint32_t ctr) {
+  const uint32_t x0 = bop3<tt::XOR3>(a0, b0, c0);
+  const uint32_t x1 = bop3<tt::MAJ>(a0, b0, c0);
+  const uint32_t y0 = bop3<tt::XOR3>(a1, b1, c1);
+  const uint32_t y1 = bop3<tt::MAJ>(a1, b1, c1);
+  const uint32_t s3 = bop3<tt::ANDN_XOR>(y1, x1, y0);
+  const uint32_t s4 = bop3<tt::EQ_NE>(x1, y0, y1);
+  return bop3<tt::SEL>(x0, s3, ctr & s4);
+}
+
+// ---- storage layouts -------------------------------------------------------
+// load_raw() issues the global loads for one lane's W words of a row;
+// convert() turns them into bit words.  Splitting the two lets the row reader
+// keep three rows of loads in flight.
+template <int W_, int XL_>
+struct BitsIO {
+  static constexpr int W = W_, XL = XL_;
+  struct Raw {
+    uint32_t w[W];
+  };
+  __device__ static __forceinline__ Raw load_raw(const uint8_t* row, int col) {
+    Raw r;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(row) + col;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = p[i];
+    return r;
+  }
+  __device__ static __forceinline__ Vec<W> convert(const Raw& r, const bool (&ok)[W]) {
+    Vec<W> v;
+#pragma unroll
+    for (int i = 0; i < W; ++i) v.w[i] = ok[i] ? r.w[i] : 0u;
+    return v;
+  }
+  __device__ static __forceinline__ void store(uint8_t* row, int col, int i, uint32_t w) {
+    reinterpret_cast<uint32_t*>(row)[col + i] = w;
+  }
+};
+
+template <int W_, int XL_>
+struct U8IO {
+  static constexpr int W = W_, XL = XL_;
+  struct Raw {
+    uint4 q[2 * W];
+  };
+  __device__ static __forceinline__ Raw load_raw(const uint8_t* row, int col) {
+    Raw r;
+    const uint4* p = reinterpret_cast<const uint4*>(row + 32 * int64_t(col));
+#pragma unroll
+    for (int i = 0; i < 2 * W; ++i) r.q[i] = p[i];
+    return r;
+  }
+  // 32 bytes (0/1 each) -> 32 bits.  x_k holds cells 4k..4k+3 in its bytes;
+  // (x_{2j} | x_{2j+1} << 4) dotted with bytes (1,2,4,8) is the 8-bit pattern
+  // of cells 8j..8j+7.
+  __device__ static __forceinline__ uint32_t pack(const uint4& a, const uint4& b) {
+    constexpr uint32_t kW = 0x08040201u;
+    const uint32_t b0 = __builtin_amdgcn_udot4(a.x | (a.y << 4), kW, 0u, false);
+    const uint32_t b1 = __builtin_amdgcn_udot4(a.z | (a.w << 4), kW, 0u, false);
+    const uint32_t b2 = __builtin_amdgcn_udot4(b.x | (b.y << 4), kW, 0u, false);
+    const uint32_t b3 = __builtin_amdgcn_udot4(b.z | (b.w << 4), kW, 0u, false);
+    return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+  }
+  __device__ static __forceinline__ Vec<W> convert(const Raw& r, const bool (&ok)[W]) {
+    Vec<W> v;
+#pragma unroll
+    for (int i = 0; i < W; ++i) v.w[i] = ok[i] ? pack(r.q[2 * i], r.q[2 * i + 1]) : 0u;
+    return v;
+  }
+  // nibble n -> bytes (n&1, n>>1&1, n>>2&1, n>>3&1): n * 0x204081 puts bit i
+  // at bit 8i (plus non-colliding cross terms), masked by 0x01010101.
+  __device__ static __forceinline__ uint32_t spread(uint32_t w, int k) {
+    return __umul24((w >> (4 * k)) & 0xFu, 0x204081u) & 0x01010101u;
+  }
+  __device__ static __forceinline__ void store(uint8_t* row, int col, int i, uint32_t w) {
+    uint4* p = reinterpret_cast<uint4*>(row + 32 * int64_t(col + i));
+    p[0] = make_uint4(spread(w, 0), spread(w, 1), spread(w, 2), spread(w, 3));
+    p[1] = make_uint4(spread(w, 4), spread(w, 5), spread(w, 6), spread(w, 7));
+  }
+};
+
+// Row reader with a 3-deep register prefetch: the row for step k sits in
+// slot k % 3 and is replaced by the load for step k + 3 when consumed.
+template <class IO>
+struct RowReader {
+  static constexpr int W = IO::W;
+  typename IO::Raw buf[3];
+  const uint8_t* base;
+  int64_t pitch;
+  int kmax, col;
+  bool ok[W];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) buf[s] = IO::load_raw(base + int64_t(min(s, kmax)) * pitch, col);
+  }
+  template <int S>
+  __device__ __forceinline__ Vec<W> take(int k) {
+    const typename IO::Raw r = buf[S];
+    buf[S] = IO::load_raw(base + int64_t(min(k + 3, kmax)) * pitch, col);
+    return IO::convert(r, ok);
+  }
+};
+
+// Per-wave state.  Level L (0..T-1) keeps, for its last three rows (slot =
+// row index mod 3), the horizontal sums h0/h1 and the cells themselves.
+template <int T, int W>
+struct Levels {
+  Vec<W> h0[T][3], h1[T][3], cc[T][3];
+  Vec<W> acc[T];   // per word: OR of (new ^ old) per produced level L+1
+  Vec<W> pipe[T];  // skewed schedule: pending input row of level L
+};
+
+// Level L at a step in slot S: push the new level-L row `cur` into the
+// window and produce the level-(L+1) row one row above it.
+template <int T, class IO, int S, int L, int W = IO::W>
+__device__ __forceinline__ Vec<W> level_full(Levels<T, W>& st, const Vec<W>& cur) {
+  constexpr int s1 = (S + 1) % 3, s2 = (S + 2) % 3;
+  Vec<W> h0, h1, nxt;
+  hsum<IO::XL>(cur, h0, h1);
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const uint32_t ctr = st.cc[L][s2].w[i];
+    nxt.w[i] = rule(st.h0[L][s1].w[i], st.h1[L][s1].w[i], st.h0[L][s2].w[i], st.h1[L][s2].w[i], h0.w[i],
+                    h1.w[i], ctr);
+    st.acc[L].w[i] = bop3<tt::OR_XOR>(st.acc[L].w[i], nxt.w[i], ctr);
+  }
+  st.h0[L][S] = h0;
+  st.h1[L][S] = h1;
+  st.cc[L][S] = cur;
+  return nxt;
+}
+
+// Window fill only (the level's output row would still be invalid).
+template <int T, class IO, int S, int L, int W = IO::W>
+__device__ __forceinline__ void level_store(Levels<T, W>& st, const Vec<W>& cur) {
+  Vec<W> h0, h1;
+  hsum<IO::XL>(cur, h0, h1);
+  st.h0[L][S] = h0;
+  st.h1[L][S] = h1;
+  st.cc[L][S] = cur;
+}
+
+template <int T, class IO, int S, int L, int LEND, int W = IO::W>
+__device__ __forceinline__ Vec<W> levels_full(Levels<T, W>& st, const Vec<W>& cur) {
+  if constexpr (L < LEND) {
+    return levels_full<T, IO, S, L + 1, LEND>(st, level_full<T, IO, S, L>(st, cur));
+  } else {
+    return cur;
+  }
+}
+
+// Triangular prologue, fully unrolled: at step K only levels 1..K/2 hold
+// valid rows, so only those are evaluated; level K/2+1 just fills its
+// window.
+template <int T, class IO, int K>
+__device__ __forceinline__ void prologue_tri(Levels<T, IO::W>& st, RowReader<IO>& rd) {
+  if constexpr (K < 2 * T) {
+    constexpr int S = K % 3;
+    constexpr int nfull = K / 2;
+    const Vec<IO::W> cur = levels_full<T, IO, S, 0, nfull>(st, rd.template take<S>(K));
+    if constexpr (nfull < T) level_store<T, IO, S, nfull>(st, cur);
+    prologue_tri<T, IO, K + 1>(st, rd);
+  }
+}
+
+// Output of one row: lanes store the words they own (not the wave halos).
+template <class IO>
+struct Writer {
+  static constexpr int W = IO::W;
+  uint8_t* out;
+  int64_t pitch;
+  int col;
+  bool own[W];
+  __device__ __forceinline__ void row(int64_t r, const Vec<W>& v) const {
+    uint8_t* p = out + r * pitch;
+#pragma unroll
+    for (int i = 0; i < W; ++i)
+      if (own[i]) IO::store(p, col, i, v.w[i]);
+  }
+};
+
+// ---- skewed (software-pipelined) schedule ----------------------------------
+// Iteration i evaluates level L at row step i - L; level L's input is level
+// L-1's output from the previous iteration (pipe[L]).  Phases after the 2T
+// straight prologue steps: ramp r = 1..T-1 (step 2T-1+r for levels
+// 0..T-1-r), steady i = 3T-1..kend-1, drain (levels L > i-kend only).
+template <int U, int L>
+constexpr int skew_slot() {
+  return ((U - L) % 3 + 3) % 3;
+}
+
+template <int T, class IO, int U, int L, int LO, int W = IO::W>
+__device__ __forceinline__ Vec<W> skew_levels(Levels<T, W>& st, const Vec<W>& row0, Vec<W> top) {
+  if constexpr (L < LO) {
+    return top;
+  } else {
+    const Vec<W> o = level_full<T, IO, skew_slot<U, L>(), L>(st, L == 0 ? row0 : st.pipe[L]);
+    if constexpr (L == T - 1) {
+      top = o;
+    } else {
+      st.pipe[L + 1] = o;
+    }
+    return skew_levels<T, IO, U, L - 1, LO>(st, row0, top);
+  }
+}
+
+template <int T, class IO, int R>
+__device__ __forceinline__ void ramp(Levels<T, IO::W>& st, RowReader<IO>& rd) {
+  if constexpr (R < T) {
+    constexpr int K = 2 * T - 1 + R;
+    constexpr int S = K % 3;
+    st.pipe[T - R] = levels_full<T, IO, S, 0, T - R>(st, rd.template take<S>(K));
+    ramp<T, IO, R + 1>(st, rd);
+  }
+}
+
+template <int T, class IO, int D, int U>
+__device__ __forceinline__ void drain_all(Levels<T, IO::W>& st, int i, const Writer<IO>& wr) {
+  if constexpr (D < T - 1) {
+    const Vec<IO::W> zero{};
+    wr.row(i - (T - 1) - T, skew_levels<T, IO, U, T - 1, D + 1>(st, zero, zero));
+    drain_all<T, IO, D + 1, (U + 1) % 3>(st, i + 1, wr);
+  }
+}
+
+template <int T, class IO, int U>
+__device__ __forceinline__ void skew_steady_and_drain(Levels<T, IO::W>& st, RowReader<IO>& rd, int kend,
+                                                      const Writer<IO>& wr) {
+  constexpr int W = IO::W;
+  constexpr int U0 = U, U1 = (U + 1) % 3, U2 = (U + 2) % 3;
+  const Vec<W> zero{};
+  int i = 3 * T - 1;
+  for (; i + 3 <= kend; i += 3) {
+    wr.row(i - (T - 1) - T, skew_levels<T, IO, U0, T - 1, 0>(st, rd.template take<U0>(i), zero));
+    wr.row(i + 1 - (T - 1) - T, skew_levels<T, IO, U1, T - 1, 0>(st, rd.template take<U1>(i + 1), zero));
+    wr.row(i + 2 - (T - 1) - T, skew_levels<T, IO, U2, T - 1, 0>(st, rd.template take<U2>(i + 2), zero));
+  }
+  const int rem = kend - i;
+  if (rem == 0) {
+    drain_all<T, IO, 0, U0>(st, i, wr);
+  } else if (rem == 1) {
+    wr.row(i - (T - 1) - T, skew_levels<T, IO, U0, T - 1, 0>(st, rd.template take<U0>(i), zero));
+    drain_all<T, IO, 0, U1>(st, i + 1, wr);
+  } else {
+    wr.row(i - (T - 1) - T, skew_levels<T, IO, U0, T - 1, 0>(st, rd.template take<U0>(i), zero));
+    wr.row(i + 1 - (T - 1) - T, skew_levels<T, IO, U1, T - 1, 0>(st, rd.template take<U1>(i + 1), zero));
+    drain_all<T, IO, 0, U2>(st, i + 2, wr);
+  }
+}
+
+template <int T, class IO, bool SKEW>
+__global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p) {
+  constexpr int W = IO::W;
+  constexpr int kWaveOut = 64 * W - 2;  // words produced per wave
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= p.ncolw * p.nseg) return;  // wave-uniform
+  const int kcol = gw / p.nseg;
+  const int seg = gw - kcol * p.nseg;
+  // Balanced segments: the first `seg_rem` segments get one extra row.
+  const int64_t o0 = p.row_lo + int64_t(seg) * p.seg_rows + min(seg, p.seg_rem);
+  const int64_t o1 = o0 + p.seg_rows + (seg < p.seg_rem ? 1 : 0);
+  if (o0 >= o1) return;  // wave-uniform
+
+  // Lane words: col .. col+W-1 (padded word index); the wave's first and
+  // last words are halo words.
+  const int col = kcol * kWaveOut - 1 + W * lane;
+  const int64_t pitch = p.pitch;
+  RowReader<IO> rd;
+  Writer<IO> wr;
+  uint32_t fmask[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const int c = col + i;
+    const bool ok = c >= 0 && c < p.Wp;
+    const bool halo = (lane == 0 && i == 0) || (lane == 63 && i == W - 1);
+    rd.ok[i] = ok;
+    wr.own[i] = ok && !halo;
+    fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
+  }
+
+  Levels<T, W> st;
+#pragma unroll
+  for (int L = 0; L < T; ++L) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) st.h0[L][s].w[i] = st.h1[L][s].w[i] = st.cc[L][s].w[i] = 0u;
+      st.pipe[L].w[i] = st.acc[L].w[i] = 0u;
+    }
+  }
+
+  constexpr int kPro = 2 * T;
+  const int kend = kPro + int(o1 - o0);
+  rd.base = p.in + (o0 - T) * pitch;  // input row of step k: o0 - T + k
+  rd.pitch = pitch;
+  rd.kmax = kend - 1;
+  rd.col = min(max(col, 0), p.Wp - W);  // clamped in-bounds; values of !ok words are discarded
+  rd.init();
+  wr.out = p.out + (o0 - T) * pitch;  // level-T row of step k: o0 - 2T + k
+  wr.pitch = pitch;
+  wr.col = col;
+
+  // Prologue: 2T steps, no stores.
+  prologue_tri<T, IO, 0>(st, rd);
+
+  if constexpr (SKEW && T > 1) {
+    // Requires o1 - o0 >= T (guaranteed by plan()).
+    ramp<T, IO, 1>(st, rd);
+    skew_steady_and_drain<T, IO, (3 * T - 1) % 3>(st, rd, kend, wr);
+  } else {
+    int k = kPro;
+    constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
+    for (; k + 3 <= kend; k += 3) {
+      wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
+      wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
+      wr.row(k + 2 - T, levels_full<T, IO, S2, 0, T>(st, rd.template take<S2>(k + 2)));
+    }
+    if (k < kend) {
+      wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
+      if (k + 1 < kend) wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
+    }
+  }
+
+  // Fused termination flags: one bit per generation level, counting only
+  // owned cells (fmask excludes wave-halo words and the tail beyond W).
+  if (p.changed) {
+    uint32_t mask = 0;
+#pragma unroll
+    for (int L = 0; L < T; ++L) {
+      uint32_t any = 0;
+#pragma unroll
+      for (int i = 0; i < W; ++i) any |= st.acc[L].w[i] & fmask[i];
+      mask |= (__ballot(any != 0u) != 0ull ? 1u : 0u) << L;
+    }
+    if (lane < T && ((mask >> lane) & 1u)) p.changed[lane] = 1u;
+  }
+}
+
+
+// Segment planning.  A wave owns a column strip and a segment of output
+// rows; its prologue is redundant work, so segments should be long, but the
+// launch must fill every SIMD: aim for one round of resident waves
+// (occupancy-limited), balanced segments no shorter than min_seg.
+// Returns whether the skewed schedule applies (every segment >= T rows).
+inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int waves_per_round, int min_seg) {
+  const int64_t segs_round = std::max<int64_t>(1, waves_per_round / std::max(1, p.ncolw));
+  const int64_t smin = std::max<int64_t>(min_seg, 2 * int64_t(T));
+  int64_t nseg = std::min<int64_t>(segs_round, out_rows / smin);
+  nseg = std::max<int64_t>(1, nseg);
+  p.nseg = int(nseg);
+  p.seg_rows = int(out_rows / nseg);
+  p.seg_rem = int(out_rows % nseg);
+  return p.seg_rows >= T;
+}
+
+template <int T, class IO, bool SKEW>
+int waves_per_round(const LifeTuning& tune) {
+  static int cached = 0;
+  if (!cached) {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, life_block_kernel<T, IO, SKEW>, 256, 0) !=
+            hipSuccess ||
+        blocks <= 0)
+      blocks = 1;
+    cached = blocks * 4 * std::max(1, tune.cus);
+  }
+  return tune.target_waves > 0 ? tune.target_waves : cached;
+}
+
+template <int T, class IO>
+void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
+  p.ncolw = int(ceil_div(p.Wp, 64 * IO::W - 2));
+  const int wpr = tune.skew ? waves_per_round<T, IO, true>(tune) : waves_per_round<T, IO, false>(tune);
+  const bool skew = plan(p, T, out_rows, wpr, tune.min_seg_rows) && tune.skew;
+  const int waves = p.ncolw * p.nseg;
+  const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
+  if (skew)
+    hipLaunchKernelGGL((life_block_kernel<T, IO, true>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((life_block_kernel<T, IO, false>), grid, block, 0, s, p);
+}
+
+// Host entry point of one compiled variant (instantiated once per
+// translation unit, life_block_*.hip).
+template <class IO>
+void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const LifeTuning& tune, hipStream_t s) {
+  switch (T) {
+    case 1: launch_T<1, IO>(p, out_rows, tune, s); break;
+    case 2: launch_T<2, IO>(p, out_rows, tune, s); break;
+    case 4: launch_T<4, IO>(p, out_rows, tune, s); break;
+    case 8: launch_T<8, IO>(p, out_rows, tune, s); break;
+    case 16: launch_T<16, IO>(p, out_rows, tune, s); break;
+    default: fail("life_block: unsupported temporal block size " + std::to_string(T));
+  }
+}
+
+}  // namespace lb
+}  // namespace hipk
+}  // namespace gol

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "gol/tile.hpp"
 
 namespace gol {
@@ -14,20 +16,42 @@ struct LifeBlockParams {
   int64_t pitch;
   int64_t row_lo, row_hi;
   int Wp;          // padded words per row
-  int ncolw;       // column waves (62 output words each)
+  int ncolw;       // column waves (64*W-2 output words each)
   int nseg;        // row segments
-  int seg_rows;    // output rows per segment
+  int seg_rows;    // output rows per segment (balanced: first seg_rem get +1)
+  int seg_rem;
   int own_w0, own_w1;
   uint32_t last_mask;
   uint32_t* changed;  // changed[L] <-> generation gen_base + 1 + L
 };
 
+// Cross-lane primitive that moves the edge words between lanes.
+enum Xlane : int { kXlaneDpp = 0, kXlaneBpermute = 1 };
+
 struct LifeTuning {
-  int target_waves = 4096;  // waves per launch to aim for (256 CUs x 16)
+  int cus = 256;            // compute units of the device
+  int target_waves = 0;     // waves per launch round (0 = occupancy x CUs x 4 SIMDs)
   int min_seg_rows = 64;    // lower bound on rows per wave segment
+  bool skew = false;        // software-pipelined (skewed) level schedule
+  int wpl_bits = 2;         // 32-cell words per lane, bit layout (1 or 2)
+  int xlane = kXlaneDpp;    // cross-lane primitive
 };
 
 void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream);
+// Description of the kernel variant the tuning selects for a layout.
+std::string life_block_variant(Layout layout, const LifeTuning& tune);
+// Largest T that keeps 2 waves/SIMD for the variant's words-per-lane.
+int life_block_max_T(Layout layout, const LifeTuning& tune);
+
+// Compiled variants (one translation unit each): bit layout with 1 or 2
+// words per lane and DPP or ds_bpermute lane shifts; byte layout with 1.
+#define GOL_LIFE_VARIANT(name) \
+  void name(const LifeBlockParams& p, int64_t out_rows, int T, const LifeTuning& tune, hipStream_t s)
+GOL_LIFE_VARIANT(launch_bits_w1_dpp);
+GOL_LIFE_VARIANT(launch_bits_w1_bperm);
+GOL_LIFE_VARIANT(launch_bits_w2_dpp);
+GOL_LIFE_VARIANT(launch_bits_w2_bperm);
+GOL_LIFE_VARIANT(launch_u8_w1_dpp);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

@@ -47,8 +47,12 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
     cus_ = prop.multiProcessorCount;
-    tune_.target_waves = env_int("GOL_TARGET_WAVES", std::max(1024, cus_ * 16));
+    tune_.cus = cus_;
+    tune_.target_waves = env_int("GOL_TARGET_WAVES", 0);
     tune_.min_seg_rows = env_int("GOL_MIN_SEG_ROWS", 64);
+    tune_.skew = env_int("GOL_SKEW", 0) != 0;
+    tune_.wpl_bits = env_int("GOL_WPL", 2);
+    tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneDpp);
   }
   ~HipBackend() override {
     hipSetDevice(dev_);
@@ -57,7 +61,11 @@ class HipBackend final : public Backend {
     if (stream_) hipStreamDestroy(stream_);
   }
 
-  std::string name() const override { return "hip:" + std::to_string(dev_) + ":" + arch_; }
+  std::string name() const override {
+    return "hip:" + std::to_string(dev_) + ":" + arch_ + " [" + hipk::life_block_variant(Layout::Bits, tune_) +
+           "; " + hipk::life_block_variant(Layout::U8, tune_) + "]";
+  }
+  int preferred_tmax(Layout l) const override { return hipk::life_block_max_T(l, tune_); }
   bool is_device() const override { return true; }
   int device() const override { return dev_; }
   void* stream() const override { return stream_; }

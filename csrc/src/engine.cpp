@@ -7,7 +7,7 @@
 namespace gol {
 
 namespace {
-constexpr int kTSizes[] = {32, 16, 8, 4, 2, 1};  // temporal block sizes built for every backend
+constexpr int kTSizes[] = {16, 8, 4, 2, 1};  // temporal block sizes built for every backend
 
 int64_t min_tile_rows(const Decomposition& d) { return d.H / d.Py; }
 int64_t min_tile_cols(const Decomposition& d) { return (d.W / d.col_unit / d.Px) * d.col_unit; }
@@ -25,8 +25,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     GOL_REQUIRE(cfg_.W % 32 == 0, "bit-packed layout needs width % 32 == 0 (use the u8 layout)");
   dec_ = Decomposition::make(cfg_.W, cfg_.H, tr_->size(), cfg_.decomp, unit);
 
-  tmax_ = cfg_.tmax > 0 ? cfg_.tmax : 16;
-  tmax_ = std::min(tmax_, 32);
+  tmax_ = cfg_.tmax > 0 ? cfg_.tmax : be_->preferred_tmax(cfg_.layout);
+  tmax_ = std::min(tmax_, 16);
   int D = cfg_.epoch > 0 ? cfg_.epoch : 4 * tmax_;
   if (dec_.Py > 1) D = int(std::min<int64_t>(D, min_tile_rows(dec_)));
   if (dec_.Px > 1) {

@@ -31,8 +31,9 @@ ARCH = os.environ.get("GOL_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/transport.cpp",
              "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp"]
+LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w2_dpp", "bits_w2_bperm", "u8_w1_dpp"]
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
-            "kernels/tile_ops.hip"]
+            *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/tile_ops.hip"]
 BIND_SRCS = ["src/bindings.cpp"]
 CLI_MAIN = "tools/gol_main.cpp"
 GEN_MAIN = "tools/gol_gen.cpp"
@@ -57,9 +58,16 @@ def _headers_mtime() -> float:
 def _compile_cmd(src: Path, obj: Path) -> list[str]:
     inc = [f"-I{CSRC / 'include'}", f"-I{CSRC}"]
     if src.suffix == ".hip":
+        extra = []
+        if src.name.startswith("life_block_"):
+            # Scheduler for the temporal-blocking kernels: max-ILP interleaves the
+            # independent generation levels.  Measured on MI355X it is on par
+            # with the default strategy (the kernel is VALU-throughput bound);
+            # GOL_SCHED_STRATEGY selects another one for experiments.
+            extra = ["-mllvm", f"-amdgpu-sched-strategy={os.environ.get('GOL_SCHED_STRATEGY', 'max-ilp')}"]
         return [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                 "-Wall", "-Wno-unused-result", "-munsafe-fp-atomics", *inc, f"-I{ROCM / 'include'}",
-                "-c", str(src), "-o", str(obj)]
+                *extra, "-c", str(src), "-o", str(obj)]
     extra = []
     if src.name == "bindings.cpp":
         import pybind11  # noqa: PLC0415

@@ -47,6 +47,28 @@ def test_every_temporal_block_size(gpu, tmax, layout):
     assert (got == want).all()
 
 
+@pytest.mark.parametrize("wpl,xlane,skew", [(1, 0, 0), (1, 1, 0), (2, 0, 0), (2, 1, 0), (1, 0, 1), (2, 0, 1)])
+@pytest.mark.parametrize("tmax", [1, 4, 8, 16])
+def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
+    """Every compiled life_block variant (words/lane x DPP|bpermute x schedule)
+    against the fp32 conv oracle, including the changed-flag termination."""
+    monkeypatch.setenv("GOL_WPL", str(wpl))
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    monkeypatch.setenv("GOL_SKEW", str(skew))
+    # 4000 cells wide: 125 words -> tail handling in the last column wave.
+    W, H = 4000 - 4000 % 32, 333
+    g = random_grid(W, H, 11 * wpl + tmax)
+    gens = 3 * tmax + 1
+    want = life_step_torch(g, gens, device="cuda")
+    assert (life_step(g, gens, engine="hip", layout="bits", tmax=tmax) == want).all()
+    for cw, ch, seed, density in [c for c in CONVERGING if c[0] % 32 == 0]:
+        grid = random_grid(cw, ch, seed, density)
+        out, rep = simulate(grid, 1000, engine="hip", layout="bits", tmax=tmax)
+        ref, rgens, _ = reference_run(grid)
+        assert rep.generations == rgens, seed
+        assert (out == ref).all(), seed
+
+
 def test_hip_matches_cpu_backend_long_run(gpu):
     g = random_grid(1024, 512, 5)
     a = life_step(g, 300, engine="hip")
