@@ -18,11 +18,25 @@ int words_per_lane(Layout layout, const LifeTuning& tune) {
 
 }  // namespace
 
+namespace {
+
+// Cross-lane primitive actually compiled for (layout, words per lane).
+int xlane_of(Layout layout, int w, const LifeTuning& tune) {
+  if (tune.xlane == kXlaneCarry) return kXlaneCarry;
+  if (tune.xlane == kXlaneBpermute && layout == Layout::Bits && w == 1) return kXlaneBpermute;
+  return kXlaneDpp;
+}
+
+const char* xlane_name(int x) {
+  return x == kXlaneCarry ? "carry" : x == kXlaneBpermute ? "bpermute" : "dpp";
+}
+
+}  // namespace
+
 std::string life_block_variant(Layout layout, const LifeTuning& tune) {
-  const bool bperm = layout == Layout::Bits && tune.xlane == kXlaneBpermute;
-  return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=" +
-         std::to_string(words_per_lane(layout, tune)) + (bperm ? " bpermute" : " dpp") +
-         (tune.skew ? " skew" : "");
+  const int w = words_per_lane(layout, tune);
+  return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=" + std::to_string(w) + " " +
+         xlane_name(xlane_of(layout, w, tune)) + (tune.skew ? " skew" : "");
 }
 
 int life_block_max_T(Layout layout, const LifeTuning& tune) {
@@ -51,12 +65,14 @@ void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t s
   p.last_mask = tail ? (0xFFFFFFFFu >> (32 - tail)) : 0xFFFFFFFFu;
   p.changed = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
   const int64_t rows = a.row_hi - a.row_lo;
+  const int x = xlane_of(g.layout, w, tune);
   if (g.layout == Layout::U8) {
-    launch_u8_w1_dpp(p, rows, a.T, tune, stream);
+    (x == kXlaneCarry ? launch_u8_w1_carry : launch_u8_w1_dpp)(p, rows, a.T, tune, stream);
   } else if (w == 2) {
-    (tune.xlane == kXlaneBpermute ? launch_bits_w2_bperm : launch_bits_w2_dpp)(p, rows, a.T, tune, stream);
+    (x == kXlaneCarry ? launch_bits_w2_carry : launch_bits_w2_dpp)(p, rows, a.T, tune, stream);
   } else {
-    (tune.xlane == kXlaneBpermute ? launch_bits_w1_bperm : launch_bits_w1_dpp)(p, rows, a.T, tune, stream);
+    (x == kXlaneCarry ? launch_bits_w1_carry
+                      : x == kXlaneBpermute ? launch_bits_w1_bperm : launch_bits_w1_dpp)(p, rows, a.T, tune, stream);
   }
 }
 

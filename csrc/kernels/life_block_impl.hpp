@@ -72,17 +72,43 @@ __device__ __forceinline__ void neighbours(const Vec<W>& c, uint32_t& lw, uint32
   }
 }
 
+// Cell x-1 for the lane's first word via the carry chain instead of a DPP
+// move: v_add_co (last + last) leaves every lane's top bit in VCC, the SALU
+// shifts the lane mask up by one lane (s_lshl_b64, off the VALU), and
+// v_addc adds it in as bit 0 of (first << 1).  Lane 0 gets 0 (a halo word).
+// Measured (csrc/tools/ubench_xlane.hip): 67 vs 80 cycles per level body at
+// 2 waves/SIMD, because the DPP wave shift stalls the VALU stream.
+__device__ __forceinline__ uint32_t left_in_carry(uint32_t first, uint32_t last) {
+  uint32_t l, t;
+  asm(
+      "v_add_co_u32 %1, vcc, %3, %3\n\t"
+      "s_lshl_b64 vcc, vcc, 1\n\t"
+      "v_lshlrev_b32 %0, 1, %2\n\t"
+      "v_addc_co_u32 %0, vcc, 0, %0, vcc"
+      : "=&v"(l), "=&v"(t)
+      : "v"(first), "v"(last)
+      : "vcc");
+  return l;
+}
+
 // Horizontal 3-sums (h1:h0) = left + centre + right for every word.
 template <int XL, int W>
 __device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1) {
-  uint32_t lw, rw;
-  neighbours<XL>(c, lw, rw);
+  uint32_t lw = 0, rw;
+  if constexpr (XL == kXlaneCarry) {
+    rw = __builtin_amdgcn_mov_dpp(c.w[0], 0x130, 0xF, 0xF, true);  // wave_shl:1
+  } else {
+    neighbours<XL>(c, lw, rw);
+  }
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    const uint32_t lo = i == 0 ? lw : c.w[i - 1];
     const uint32_t hi = i == W - 1 ? rw : c.w[i + 1];
-    const uint32_t l = __builtin_amdgcn_alignbit(c.w[i], lo, 31);  // cell x-1
-    const uint32_t r = __builtin_amdgcn_alignbit(hi, c.w[i], 1);   // cell x+1
+    uint32_t l;
+    if (XL == kXlaneCarry && i == 0)
+      l = left_in_carry(c.w[0], c.w[W - 1]);
+    else
+      l = __builtin_amdgcn_alignbit(c.w[i], i == 0 ? lw : c.w[i - 1], 31);  // cell x-1
+    const uint32_t r = __builtin_amdgcn_alignbit(hi, c.w[i], 1);            // cell x+1
     h0.w[i] = bop3<tt::XOR3>(l, c.w[i], r);
     h1.w[i] = bop3<tt::MAJ>(l, c.w[i], r);
   }
@@ -110,11 +136,12 @@ struct BitsIO {
   struct Raw {
     uint32_t w[W];
   };
-  __device__ static __forceinline__ Raw load_raw(const uint8_t* row, int col) {
+  // off[i]: in-bounds (clamped) word index of the lane's word i.
+  __device__ static __forceinline__ Raw load_raw(const uint8_t* row, const int (&off)[W]) {
     Raw r;
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(row) + col;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(row);
 #pragma unroll
-    for (int i = 0; i < W; ++i) r.w[i] = p[i];
+    for (int i = 0; i < W; ++i) r.w[i] = p[off[i]];
     return r;
   }
   __device__ static __forceinline__ Vec<W> convert(const Raw& r, const bool (&ok)[W]) {
@@ -134,11 +161,14 @@ struct U8IO {
   struct Raw {
     uint4 q[2 * W];
   };
-  __device__ static __forceinline__ Raw load_raw(const uint8_t* row, int col) {
+  __device__ static __forceinline__ Raw load_raw(const uint8_t* row, const int (&off)[W]) {
     Raw r;
-    const uint4* p = reinterpret_cast<const uint4*>(row + 32 * int64_t(col));
 #pragma unroll
-    for (int i = 0; i < 2 * W; ++i) r.q[i] = p[i];
+    for (int i = 0; i < W; ++i) {
+      const uint4* p = reinterpret_cast<const uint4*>(row + 32 * int64_t(off[i]));
+      r.q[2 * i] = p[0];
+      r.q[2 * i + 1] = p[1];
+    }
     return r;
   }
   // 32 bytes (0/1 each) -> 32 bits.  x_k holds cells 4k..4k+3 in its bytes;
@@ -178,16 +208,17 @@ struct RowReader {
   typename IO::Raw buf[3];
   const uint8_t* base;
   int64_t pitch;
-  int kmax, col;
+  int kmax;
+  int off[W];  // clamped word index per lane word (values of !ok words are discarded)
   bool ok[W];
   __device__ __forceinline__ void init() {
 #pragma unroll
-    for (int s = 0; s < 3; ++s) buf[s] = IO::load_raw(base + int64_t(min(s, kmax)) * pitch, col);
+    for (int s = 0; s < 3; ++s) buf[s] = IO::load_raw(base + int64_t(min(s, kmax)) * pitch, off);
   }
   template <int S>
   __device__ __forceinline__ Vec<W> take(int k) {
     const typename IO::Raw r = buf[S];
-    buf[S] = IO::load_raw(base + int64_t(min(k + 3, kmax)) * pitch, col);
+    buf[S] = IO::load_raw(base + int64_t(min(k + 3, kmax)) * pitch, off);
     return IO::convert(r, ok);
   }
 };
@@ -386,7 +417,8 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
   rd.base = p.in + (o0 - T) * pitch;  // input row of step k: o0 - T + k
   rd.pitch = pitch;
   rd.kmax = kend - 1;
-  rd.col = min(max(col, 0), p.Wp - W);  // clamped in-bounds; values of !ok words are discarded
+#pragma unroll
+  for (int i = 0; i < W; ++i) rd.off[i] = min(max(col + i, 0), p.Wp - 1);
   rd.init();
   wr.out = p.out + (o0 - T) * pitch;  // level-T row of step k: o0 - 2T + k
   wr.pitch = pitch;

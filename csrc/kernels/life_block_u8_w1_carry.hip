@@ -1,0 +1,10 @@
+// life_block variant: U8IO<1, kXlaneCarry> (see life_block_impl.hpp).
+#include "life_block_impl.hpp"
+
+namespace gol {
+namespace hipk {
+
+GOL_LIFE_VARIANT(launch_u8_w1_carry) { lb::launch_variant<lb::U8IO<1, kXlaneCarry>>(p, out_rows, T, tune, s); }
+
+}  // namespace hipk
+}  // namespace gol

@@ -26,14 +26,14 @@ struct LifeBlockParams {
 };
 
 // Cross-lane primitive that moves the edge words between lanes.
-enum Xlane : int { kXlaneDpp = 0, kXlaneBpermute = 1 };
+enum Xlane : int { kXlaneDpp = 0, kXlaneBpermute = 1, kXlaneCarry = 2 };
 
 struct LifeTuning {
   int cus = 256;            // compute units of the device
   int target_waves = 0;     // waves per launch round (0 = occupancy x CUs x 4 SIMDs)
   int min_seg_rows = 64;    // lower bound on rows per wave segment
   bool skew = false;        // software-pipelined (skewed) level schedule
-  int wpl_bits = 2;         // 32-cell words per lane, bit layout (1 or 2)
+  int wpl_bits = 1;         // 32-cell words per lane, bit layout (1 or 2)
   int xlane = kXlaneDpp;    // cross-lane primitive
 };
 
@@ -44,14 +44,17 @@ std::string life_block_variant(Layout layout, const LifeTuning& tune);
 int life_block_max_T(Layout layout, const LifeTuning& tune);
 
 // Compiled variants (one translation unit each): bit layout with 1 or 2
-// words per lane and DPP or ds_bpermute lane shifts; byte layout with 1.
+// words per lane and DPP / ds_bpermute / carry-chain lane shifts; byte
+// layout with 1.
 #define GOL_LIFE_VARIANT(name) \
   void name(const LifeBlockParams& p, int64_t out_rows, int T, const LifeTuning& tune, hipStream_t s)
 GOL_LIFE_VARIANT(launch_bits_w1_dpp);
 GOL_LIFE_VARIANT(launch_bits_w1_bperm);
 GOL_LIFE_VARIANT(launch_bits_w2_dpp);
-GOL_LIFE_VARIANT(launch_bits_w2_bperm);
+GOL_LIFE_VARIANT(launch_bits_w1_carry);
+GOL_LIFE_VARIANT(launch_bits_w2_carry);
 GOL_LIFE_VARIANT(launch_u8_w1_dpp);
+GOL_LIFE_VARIANT(launch_u8_w1_carry);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

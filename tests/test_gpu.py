@@ -47,11 +47,13 @@ def test_every_temporal_block_size(gpu, tmax, layout):
     assert (got == want).all()
 
 
-@pytest.mark.parametrize("wpl,xlane,skew", [(1, 0, 0), (1, 1, 0), (2, 0, 0), (2, 1, 0), (1, 0, 1), (2, 0, 1)])
+@pytest.mark.parametrize("wpl,xlane,skew", [(1, 0, 0), (1, 1, 0), (1, 2, 0), (2, 0, 0), (2, 2, 0), (1, 0, 1),
+                                            (1, 2, 1), (2, 0, 1)])
 @pytest.mark.parametrize("tmax", [1, 4, 8, 16])
 def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
-    """Every compiled life_block variant (words/lane x DPP|bpermute x schedule)
-    against the fp32 conv oracle, including the changed-flag termination."""
+    """Every compiled life_block variant (words/lane x DPP|bpermute|carry x
+    schedule) against the fp32 conv oracle, including the changed-flag
+    termination."""
     monkeypatch.setenv("GOL_WPL", str(wpl))
     monkeypatch.setenv("GOL_XLANE", str(xlane))
     monkeypatch.setenv("GOL_SKEW", str(skew))
@@ -67,6 +69,17 @@ def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
         ref, rgens, _ = reference_run(grid)
         assert rep.generations == rgens, seed
         assert (out == ref).all(), seed
+
+
+@pytest.mark.parametrize("xlane", [0, 2])
+@pytest.mark.parametrize("tmax", [1, 8, 16])
+def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    W, H = 1999, 301
+    g = random_grid(W, H, 5 + tmax)
+    gens = 2 * tmax + 5
+    want = life_step_torch(g, gens, device="cuda")
+    assert (life_step(g, gens, engine="hip", layout="u8", tmax=tmax) == want).all()
 
 
 def test_hip_matches_cpu_backend_long_run(gpu):
