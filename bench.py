@@ -53,6 +53,7 @@ def main() -> int:
     ap.add_argument("--tmax", type=int, default=0)
     ap.add_argument("--epoch", type=int, default=0)
     ap.add_argument("--poll", type=int, default=0)
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--repeats", type=int, default=1, help="timed repetitions (best is reported)")
     a = ap.parse_args()
@@ -83,7 +84,7 @@ def main() -> int:
     S = a.size
     total = a.warmup + a.steps * a.repeats
     cfg = LifeConfig(S, S, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
-                     poll_gens=a.poll)
+                     poll_gens=a.poll, overlap=a.overlap)
     sim = Simulation(cfg, transport=transport, backend=backend)
     eng = sim.native_engine
     sim.init_random(a.seed, 0.5)

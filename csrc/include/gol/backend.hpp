@@ -39,6 +39,13 @@ class Backend {
   virtual void* event_record() = 0;
   virtual void event_wait(void* ev) = 0;  // host blocks until the event completes
   virtual void event_destroy(void* ev) = 0;
+  // Second queue for communication that overlaps compute (HIP: a separate
+  // non-blocking stream; synchronous backends return nullptr and run
+  // everything in program order).  stream_mark() records a point on `from`
+  // (nullptr = the compute stream) that stream_wait() makes `on` wait for.
+  virtual void* comm_stream() { return nullptr; }
+  virtual void* stream_mark(void* /*from*/) { return nullptr; }
+  virtual void stream_wait(void* /*on*/, void* /*mark*/) {}
 
   // Kernels.
   virtual void run_block(const BlockArgs& a) = 0;

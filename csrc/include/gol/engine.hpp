@@ -38,6 +38,13 @@ struct EngineConfig {
   int tmax = 0;                    // max generations per kernel launch (0 = backend default)
   int epoch = 0;                   // generations per halo exchange (0 = auto)
   int poll_gens = 0;               // generations between termination polls (0 = auto)
+  // Overlap the north/south halo exchange with the interior of the epoch
+  // (edge strips recomputed in scratch tiles): -1 auto (Py > 1 and tiles
+  // tall enough), 0 off, 1 on when possible.
+  int overlap = -1;
+  // Check each termination poll one poll window later, so the host never
+  // drains the device queue (stops are absorbing, so running past is exact).
+  bool lagged_poll = true;
 };
 
 struct RunResult {
@@ -50,6 +57,7 @@ struct RunResult {
   int64_t exchanges = 0;         // halo exchanges performed
   int64_t polls = 0;             // termination polls performed
   int64_t kernel_launches = 0;
+  bool overlapped = false;       // epochs ran with the overlapped halo exchange
 };
 
 class Engine {
@@ -67,6 +75,7 @@ class Engine {
   Extent cols() const { return dec_.cols(rank_); }
   int epoch_depth() const { return D_; }
   int tmax() const { return tmax_; }
+  bool overlap() const { return overlap_; }
   int64_t generation() const { return gen_; }
   void set_generation(int64_t g) { gen_ = g; }
   Backend* backend() const { return be_; }
@@ -96,9 +105,20 @@ class Engine {
   void step_block(int T, int64_t row_lo, int64_t row_hi);
 
  private:
+  struct Poll {
+    int64_t from = 0, to = 0;
+    void* ev = nullptr;
+  };
   RunResult run_impl(int64_t limit, bool stop_early);
-  bool poll(int64_t from, int64_t to, int64_t* first_unchanged);
+  Poll poll_issue(int64_t from, int64_t to);
+  bool poll_check(Poll& p, int64_t* first_unchanged);
   int pick_T(int64_t remaining) const;
+  // One temporal block in <in> -> <out> for generations (gen_base, gen_base+T].
+  void launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
+              int64_t gen_base);
+  void exchange_columns(void* buf);
+  // d generations (d <= D_) with the row exchange overlapped (see engine.cpp).
+  void epoch_overlapped(int64_t d);
 
   EngineConfig cfg_;
   Backend* be_;
@@ -114,6 +134,9 @@ class Engine {
   int64_t flags_base_ = 0, flags_len_ = 0;
   uint32_t* alive_dev_ = nullptr;
   void* colbuf_[4] = {nullptr, nullptr, nullptr, nullptr};  // send W, send E, recv W, recv E
+  bool overlap_ = false;
+  TileGeom gs_;                     // edge scratch tile: D owned rows + D halo rows each side
+  void* edge_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [top|bottom][parity]
   int64_t gen_ = 0;
   int64_t exchanges_ = 0, polls_ = 0, launches_ = 0;
 };

@@ -79,15 +79,16 @@ __device__ __forceinline__ void neighbours(const Vec<W>& c, uint32_t& lw, uint32
 // Measured (csrc/tools/ubench_xlane.hip): 67 vs 80 cycles per level body at
 // 2 waves/SIMD, because the DPP wave shift stalls the VALU stream.
 __device__ __forceinline__ uint32_t left_in_carry(uint32_t first, uint32_t last) {
-  uint32_t l, t;
-  asm(
-      "v_add_co_u32 %1, vcc, %3, %3\n\t"
-      "s_lshl_b64 vcc, vcc, 1\n\t"
-      "v_lshlrev_b32 %0, 1, %2\n\t"
-      "v_addc_co_u32 %0, vcc, 0, %0, vcc"
-      : "=&v"(l), "=&v"(t)
-      : "v"(first), "v"(last)
-      : "vcc");
+  // Separate statements with SGPR-pair carries (not VCC) so the scheduler
+  // can interleave the chains of different levels.
+  uint32_t t, l;
+  uint64_t m;
+  asm("v_add_co_u32_e64 %0, %1, %2, %2" : "=v"(t), "=s"(m) : "v"(last));
+  m <<= 1;  // s_lshl_b64: lane j <- top bit of lane j-1
+  uint64_t co;
+  asm("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(l), "=s"(co) : "v"(first << 1), "s"(m));
+  (void)t;
+  (void)co;
   return l;
 }
 

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -57,7 +58,11 @@ class HipBackend final : public Backend {
   ~HipBackend() override {
     hipSetDevice(dev_);
     if (stream_) hipStreamSynchronize(stream_);
+    if (comm_) hipStreamSynchronize(comm_);
     if (stage_) hipFree(stage_);
+    for (auto& e : marks_)
+      if (e) hipEventDestroy(e);
+    if (comm_) hipStreamDestroy(comm_);
     if (stream_) hipStreamDestroy(stream_);
   }
 
@@ -121,6 +126,21 @@ class HipBackend final : public Backend {
   }
   void event_wait(void* ev) override { HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(ev))); }
   void event_destroy(void* ev) override { hipEventDestroy(static_cast<hipEvent_t>(ev)); }
+  void* comm_stream() override {
+    if (!comm_) HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+    return comm_;
+  }
+  // Marks come from a small ring of reusable timing-free events: a mark is
+  // only waited on by the next few operations of an epoch.
+  void* stream_mark(void* from) override {
+    hipEvent_t& e = marks_[mark_next_++ % marks_.size()];
+    if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(e, from ? static_cast<hipStream_t>(from) : stream_));
+    return e;
+  }
+  void stream_wait(void* on, void* mark) override {
+    HIP_CHECK(hipStreamWaitEvent(on ? static_cast<hipStream_t>(on) : stream_, static_cast<hipEvent_t>(mark), 0));
+  }
 
   void run_block(const BlockArgs& a) override {
     hipk::launch_life_block(a, tune_, stream_);
@@ -204,6 +224,9 @@ class HipBackend final : public Backend {
   std::string arch_;
   int cus_ = 256;
   hipk::LifeTuning tune_;
+  hipStream_t comm_ = nullptr;
+  std::array<hipEvent_t, 16> marks_{};
+  size_t mark_next_ = 0;
   void* stage_ = nullptr;
   int64_t stage_bytes_ = 0;
 };

@@ -176,7 +176,9 @@ PYBIND11_MODULE(_gol, m) {
       .def_readwrite("sim_phase", &EngineConfig::sim_phase)
       .def_readwrite("tmax", &EngineConfig::tmax)
       .def_readwrite("epoch", &EngineConfig::epoch)
-      .def_readwrite("poll_gens", &EngineConfig::poll_gens);
+      .def_readwrite("poll_gens", &EngineConfig::poll_gens)
+      .def_readwrite("overlap", &EngineConfig::overlap)
+      .def_readwrite("lagged_poll", &EngineConfig::lagged_poll);
 
   py::class_<RunResult>(m, "RunResult")
       .def_readonly("generations", &RunResult::generations)
@@ -188,6 +190,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_readonly("exchanges", &RunResult::exchanges)
       .def_readonly("polls", &RunResult::polls)
       .def_readonly("kernel_launches", &RunResult::kernel_launches)
+      .def_readonly("overlapped", &RunResult::overlapped)
       .def("as_dict", [](const RunResult& r) {
         py::dict d;
         d["generations"] = r.generations;
@@ -199,6 +202,7 @@ PYBIND11_MODULE(_gol, m) {
         d["exchanges"] = r.exchanges;
         d["polls"] = r.polls;
         d["kernel_launches"] = r.kernel_launches;
+        d["overlapped"] = r.overlapped;
         return d;
       });
 
@@ -214,6 +218,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("geom", &Engine::geom)
       .def_property_readonly("epoch_depth", &Engine::epoch_depth)
       .def_property_readonly("tmax", &Engine::tmax)
+      .def("overlap", &Engine::overlap)
       .def_property("generation", &Engine::generation, &Engine::set_generation)
       .def("current_buffer", [](const Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })
       .def("load_cells",

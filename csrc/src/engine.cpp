@@ -47,6 +47,15 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     size_t n = size_t(g_.span_bytes(32 * int64_t(g_.hw)) * g_.H);
     for (auto& b : colbuf_) b = be_->alloc(n);
   }
+  // The overlapped schedule needs a non-empty interior (H > 2D) and pays
+  // about 2D extra rows of compute per epoch, so auto mode wants H >= 4D.
+  overlap_ = dec_.Py > 1 && cfg_.overlap != 0 && g_.H >= (cfg_.overlap > 0 ? 2 : 4) * int64_t(D_) + 1;
+  if (overlap_) {
+    gs_ = TileGeom::make(cfg_.layout, D_, g_.W, D_, g_.hw);
+    GOL_REQUIRE(gs_.pitch == g_.pitch, "edge scratch pitch mismatch");
+    for (auto& e : edge_)
+      for (auto& b : e) b = be_->alloc(size_t(gs_.bytes()));
+  }
   gen_ = cfg_.start_gen;
 }
 
@@ -55,6 +64,9 @@ Engine::~Engine() {
     if (b) be_->release(b);
   for (auto& b : colbuf_)
     if (b) be_->release(b);
+  for (auto& e : edge_)
+    for (auto& b : e)
+      if (b) be_->release(b);
   if (flags_) be_->release(flags_);
   if (flags_host_) be_->release_host(flags_host_);
   if (alive_dev_) be_->release(alive_dev_);
@@ -95,30 +107,41 @@ int Engine::pick_T(int64_t remaining) const {
 // cells travel with the rows): 4 messages instead of the reference's 8
 // per-generation messages with a strided MPI_Type_vector column
 // (src/game_mpi.c:335-383).
+void Engine::exchange_columns(void* buf) {
+  auto* base = static_cast<uint8_t*>(buf);
+  auto nb = dec_.neighbors(rank_);
+  const int64_t H = g_.H, pitch = g_.pitch;
+  if (dec_.Px == 1) {
+    be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/false);
+    return;
+  }
+  const int64_t halo = 32 * int64_t(g_.hw);
+  const int64_t span = g_.span_bytes(halo);
+  const int64_t r0 = g_.row0();
+  be_->copy_2d_async(colbuf_[0], span, base + g_.offset(r0, g_.cell0()), pitch, span, H);
+  be_->copy_2d_async(colbuf_[1], span, base + g_.offset(r0, g_.cell0() + g_.W - halo), pitch, span, H);
+  std::vector<P2POp> ops = {
+      {true, nb[kWest], colbuf_[0], size_t(span * H)},
+      {false, nb[kEast], colbuf_[3], size_t(span * H)},
+      {true, nb[kEast], colbuf_[1], size_t(span * H)},
+      {false, nb[kWest], colbuf_[2], size_t(span * H)},
+  };
+  tr_->exchange(ops, be_->stream());
+  be_->copy_2d_async(base + g_.offset(r0, 0), pitch, colbuf_[2], span, span, H);
+  be_->copy_2d_async(base + g_.offset(r0, g_.cell0() + g_.W), pitch, colbuf_[3], span, span, H);
+}
+
+// Two-phase halo exchange (columns, then full-width rows so the corner
+// cells travel with the rows): 4 messages instead of the reference's 8
+// per-generation messages with a strided MPI_Type_vector column
+// (src/game_mpi.c:335-383).
 void Engine::halo_exchange() {
   void* buf = buf_[cur_];
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
   const int64_t H = g_.H, pitch = g_.pitch;
   // Phase A: west/east halo columns of the owned rows.
-  if (dec_.Px == 1) {
-    be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/false);
-  } else {
-    const int64_t halo = 32 * int64_t(g_.hw);
-    const int64_t span = g_.span_bytes(halo);
-    const int64_t r0 = g_.row0();
-    be_->copy_2d_async(colbuf_[0], span, base + g_.offset(r0, g_.cell0()), pitch, span, H);
-    be_->copy_2d_async(colbuf_[1], span, base + g_.offset(r0, g_.cell0() + g_.W - halo), pitch, span, H);
-    std::vector<P2POp> ops = {
-        {true, nb[kWest], colbuf_[0], size_t(span * H)},
-        {false, nb[kEast], colbuf_[3], size_t(span * H)},
-        {true, nb[kEast], colbuf_[1], size_t(span * H)},
-        {false, nb[kWest], colbuf_[2], size_t(span * H)},
-    };
-    tr_->exchange(ops, be_->stream());
-    be_->copy_2d_async(base + g_.offset(r0, 0), pitch, colbuf_[2], span, span, H);
-    be_->copy_2d_async(base + g_.offset(r0, g_.cell0() + g_.W), pitch, colbuf_[3], span, span, H);
-  }
+  exchange_columns(buf);
   // Phase B: north/south halo rows over the full padded width.
   if (dec_.Py == 1) {
     be_->fill_periodic(buf, g_, /*cols=*/false, /*rows=*/true);
@@ -136,37 +159,128 @@ void Engine::halo_exchange() {
   ++exchanges_;
 }
 
-void Engine::step_block(int T, int64_t row_lo, int64_t row_hi) {
+// Overlapped epoch (Py > 1).  The reference exchanges halos and then waits
+// (MPI_Startall + MPI_Waitall, src/game_mpi.c:392-401) before computing.
+// Here the D-generation dependence cone splits the tile in three:
+//   interior  owned rows only; after d gens rows [Dv+d, Dv+H-d) are exact.
+//             Needs no halo, so it runs while the rows are in flight.
+//   top edge  scratch tile [north halo (D) | owned rows Dv..Dv+2D) ]; after
+//             d <= D gens its rows [D, 2D) = owned rows [Dv, Dv+D) are exact.
+//   bottom    mirror image.
+// The edges are copied to scratch first, so the sends read the scratch and
+// the interior may overwrite the main buffers at once.  Stream order:
+//   compute: cols -> copy edges -> mark A -> interior blocks -> wait B ->
+//            edge blocks -> copy edge results back
+//   comm:    wait A -> send/recv rows (into the scratch halos) -> mark B
+// Every computed row holds real cells, so the changed flags of all three
+// regions OR together exactly as in the plain schedule.
+void Engine::epoch_overlapped(int64_t d) {
+  auto nb = dec_.neighbors(rank_);
+  const int64_t D = D_, H = g_.H, Dv = g_.Dv, pitch = g_.pitch;
+  auto* main_in = static_cast<uint8_t*>(buf_[cur_]);
+  exchange_columns(main_in);
+  auto* top = static_cast<uint8_t*>(edge_[0][0]);
+  auto* bot = static_cast<uint8_t*>(edge_[1][0]);
+  be_->copy_2d_async(top + D * pitch, pitch, main_in + Dv * pitch, pitch, pitch, 2 * D);
+  be_->copy_2d_async(bot, pitch, main_in + (Dv + H - 2 * D) * pitch, pitch, pitch, 2 * D);
+  void* comm = be_->comm_stream();
+  be_->stream_wait(comm, be_->stream_mark(nullptr));
+  const size_t bytes = size_t(D * pitch);
+  std::vector<P2POp> ops = {
+      {true, nb[kNorth], top + D * pitch, bytes},      // my top rows -> north's bottom-edge halo
+      {false, nb[kSouth], bot + 2 * D * pitch, bytes},  // south's top rows -> my bottom-edge halo
+      {true, nb[kSouth], bot + D * pitch, bytes},       // my bottom rows -> south's top-edge halo
+      {false, nb[kNorth], top, bytes},                  // north's bottom rows -> my top-edge halo
+  };
+  tr_->exchange(ops, comm ? comm : be_->stream());
+  void* rows_done = be_->stream_mark(comm);
+  ++exchanges_;
+
+  // Interior: trapezoid over the owned rows.
+  int64_t a = 0, rem = d;
+  int par = 0;
+  std::vector<int> Ts;
+  while (rem > 0) {
+    const int T = pick_T(rem);
+    Ts.push_back(T);
+    launch(buf_[cur_ ^ par], buf_[cur_ ^ par ^ 1], g_, T, Dv + a + T, Dv + H - a - T, gen_ + a);
+    a += T;
+    rem -= T;
+    par ^= 1;
+  }
+  // Edges, once their halos have arrived.
+  be_->stream_wait(nullptr, rows_done);
+  for (int e = 0; e < 2; ++e) {
+    int64_t ea = 0;
+    int ep = 0;
+    for (int T : Ts) {
+      launch(edge_[e][ep], edge_[e][ep ^ 1], gs_, T, ea + T, gs_.R() - ea - T, gen_ + ea);
+      ea += T;
+      ep ^= 1;
+    }
+  }
+  auto* main_out = static_cast<uint8_t*>(buf_[cur_ ^ par]);
+  be_->copy_2d_async(main_out + Dv * pitch, pitch, static_cast<uint8_t*>(edge_[0][par]) + D * pitch, pitch,
+                     pitch, D);
+  be_->copy_2d_async(main_out + (Dv + H - D) * pitch, pitch, static_cast<uint8_t*>(edge_[1][par]) + D * pitch,
+                     pitch, pitch, D);
+  cur_ ^= par;
+  gen_ += d;
+}
+
+void Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
+                    int64_t gen_base) {
   BlockArgs a;
-  a.in = buf_[cur_];
-  a.out = buf_[cur_ ^ 1];
-  a.g = g_;
+  a.in = in;
+  a.out = out;
+  a.g = g;
   a.row_lo = row_lo;
   a.row_hi = row_hi;
   a.T = T;
-  a.gen_base = gen_;
-  a.changed = (flags_ && gen_ + T < flags_base_ + flags_len_ && gen_ >= flags_base_) ? flags_ : nullptr;
+  a.gen_base = gen_base;
+  a.changed =
+      (flags_ && gen_base + T < flags_base_ + flags_len_ && gen_base >= flags_base_) ? flags_ : nullptr;
   a.flags_base = flags_base_;
   be_->run_block(a);
   ++launches_;
+}
+
+void Engine::step_block(int T, int64_t row_lo, int64_t row_hi) {
+  launch(buf_[cur_], buf_[cur_ ^ 1], g_, T, row_lo, row_hi, gen_);
   cur_ ^= 1;
   gen_ += T;
 }
 
-bool Engine::poll(int64_t from, int64_t to, int64_t* first_unchanged) {
-  // Flags for generations (from, to]; MAX over ranks == logical OR.
+// Termination polls.  poll_issue() reduces the flags of generations
+// (from, to] over ranks (MAX == logical OR) and starts their copy to the
+// pinned mirror; poll_check() waits for that copy and scans it.  With lagged
+// polling a window is checked only when the next one has been issued, by
+// which time the device has long passed it, so the host never drains the
+// queue; stopping up to one window late is exact because both stop
+// conditions are absorbing.
+Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
+  Poll p;
+  p.from = from;
+  p.to = to;
   const int64_t n = to - from;
-  if (n <= 0) return false;
+  if (n <= 0) return p;
   uint32_t* dev = flags_ + (from + 1 - flags_base_);
   if (tr_->size() > 1) tr_->allreduce_max_u32(dev, size_t(n), be_->stream());
-  be_->copy_d2h_async(flags_host_, dev, size_t(n) * sizeof(uint32_t));
-  void* ev = be_->event_record();
-  be_->event_wait(ev);
-  be_->event_destroy(ev);
+  be_->copy_d2h_async(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t));
+  p.ev = be_->event_record();
   ++polls_;
-  for (int64_t i = 0; i < n; ++i)
-    if (flags_host_[i] == 0) {
-      *first_unchanged = from + 1 + i;
+  return p;
+}
+
+bool Engine::poll_check(Poll& p, int64_t* first_unchanged) {
+  if (p.to <= p.from) return false;
+  be_->event_wait(p.ev);
+  be_->event_destroy(p.ev);
+  p.ev = nullptr;
+  const uint32_t* h = flags_host_ + (p.from + 1 - flags_base_);
+  for (int64_t i = 0; i < p.to - p.from; ++i)
+    if (h[i] == 0) {
+      *first_unchanged = p.from + 1 + i;
       return true;
     }
   return false;
@@ -203,22 +317,40 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   int64_t checked = start, found = -1;
   const int64_t poll_epochs = std::max<int64_t>(1, poll_gens_ / D_);
   int64_t epoch = 0;
+  Poll pending;
+  bool have_pending = false;
   while (gen_ < limit) {
     int64_t d = std::min<int64_t>(D_, limit - gen_);
-    halo_exchange();
-    int64_t a = 0;
-    while (d > 0) {
-      int T = pick_T(d);
-      step_block(T, a + T, g_.R() - a - T);
-      a += T;
-      d -= T;
+    if (overlap_) {
+      epoch_overlapped(d);
+    } else {
+      halo_exchange();
+      int64_t a = 0;
+      while (d > 0) {
+        int T = pick_T(d);
+        step_block(T, a + T, g_.R() - a - T);
+        a += T;
+        d -= T;
+      }
     }
     ++epoch;
     if (stop_early && (epoch % poll_epochs == 0 || gen_ == limit)) {
-      if (poll(checked, gen_, &found)) break;
+      Poll p = poll_issue(checked, gen_);
       checked = gen_;
+      if (have_pending && poll_check(pending, &found)) {
+        have_pending = false;
+        if (p.ev) be_->event_destroy(p.ev);
+        break;
+      }
+      pending = p;
+      have_pending = true;
+      if (!cfg_.lagged_poll || gen_ == limit) {
+        have_pending = false;
+        if (poll_check(pending, &found)) break;
+      }
     }
   }
+  if (have_pending) poll_check(pending, &found);
   be_->synchronize();
   tr_->barrier();
   auto t1 = std::chrono::steady_clock::now();
@@ -227,6 +359,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.exchanges = exchanges_ - e0;
   res.polls = polls_ - p0;
   res.kernel_launches = launches_ - l0;
+  res.overlapped = overlap_;
   res.generations = limit;
   if (found >= 0) {
     res.first_unchanged = found;

@@ -47,7 +47,7 @@ struct Options {
   bool random = false;
   uint64_t seed = 1;
   double density = 0.5;
-  int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0;
+  int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0, overlap = -1;
   bool show = false;
 };
 
@@ -66,6 +66,7 @@ struct Options {
                "  --comm thread|rccl          in-process halo transport\n"
                "  --decomp auto|PxQ           process grid (Px columns x Py rows)\n"
                "  --tmax T --epoch D --poll N temporal block, halo depth, poll interval\n"
+               "  --overlap auto|on|off       overlap the row halo exchange with the interior\n"
                "  --threads N                 host threads for the cpu engine\n"
                "  --style serial|mpi|openmp|cuda   stdout format of the matching reference build\n"
                "  --metrics-json PATH         write run metrics as JSON\n"
@@ -99,6 +100,10 @@ Options parse(int argc, char** argv) {
     else if (a == "--tmax") o.tmax = std::atoi(next().c_str());
     else if (a == "--epoch") o.epoch = std::atoi(next().c_str());
     else if (a == "--poll") o.poll = std::atoi(next().c_str());
+    else if (a == "--overlap") {
+      std::string v = next();
+      o.overlap = v == "on" ? 1 : v == "off" ? 0 : -1;
+    }
     else if (a == "--show") o.show = true;
     else if (a == "--random") {
       std::string v = next();
@@ -187,6 +192,7 @@ int run(const Options& o) {
     cfg.tmax = o.tmax;
     cfg.epoch = o.epoch;
     cfg.poll_gens = o.poll;
+    cfg.overlap = o.overlap;
     int ndev = 1;
     if (engine == "hip") {
       GOL_REQUIRE(hip_available(), "--engine hip: no HIP device available");

@@ -36,6 +36,8 @@ def parse_args(argv=None):
     p.add_argument("--tmax", type=int, default=0)
     p.add_argument("--epoch", type=int, default=0)
     p.add_argument("--poll", type=int, default=0)
+    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                   help="overlap the row halo exchange with interior compute")
     p.add_argument("--threads", type=int, default=0)
     p.add_argument("--style", default="serial", choices=["serial", "mpi", "openmp", "cuda"])
     p.add_argument("--metrics-json", default=None)
@@ -92,7 +94,7 @@ def main(argv=None) -> int:
 
     cfg = LifeConfig(a.width, a.height, gen_limit=a.gens, check_similarity=not a.no_similarity,
                      sim_freq=a.sim_freq, layout=a.layout, decomp=a.decomp, tmax=a.tmax,
-                     epoch=a.epoch, poll_gens=a.poll)
+                     epoch=a.epoch, poll_gens=a.poll, overlap=a.overlap)
     src = a.input_file
     if a.resume:
         from .utils.checkpoint import load_checkpoint  # noqa: PLC0415

@@ -41,6 +41,8 @@ class LifeConfig:
     tmax: int = 0               # generations per kernel launch (0 = default 16)
     epoch: int = 0              # generations per halo exchange (0 = 4*tmax)
     poll_gens: int = 0          # generations between termination polls (0 = 256)
+    overlap: str = "auto"       # auto | on | off: overlap row halo exchange with the interior
+    lagged_poll: bool = True    # check termination polls one window late (no queue drain)
     start_gen: int = 0          # resume: generation number of the initial state
     sim_phase: int = 0          # resume: similarity counter at start_gen
 
@@ -64,6 +66,8 @@ class LifeConfig:
         c.tmax = int(self.tmax)
         c.epoch = int(self.epoch)
         c.poll_gens = int(self.poll_gens)
+        c.overlap = {"auto": -1, "off": 0, "on": 1}[self.overlap]
+        c.lagged_poll = bool(self.lagged_poll)
         c.start_gen = int(self.start_gen)
         c.sim_phase = int(self.sim_phase)
         return c
@@ -93,6 +97,7 @@ class RunReport:
     polls: int = 0
     kernel_launches: int = 0
     cells: int = 0
+    overlapped: bool = False
 
     @property
     def cell_updates_per_s(self) -> float:
@@ -193,7 +198,7 @@ class Simulation:
         rep = RunReport(generations=r.generations, executed=r.executed, stop_reason=r.stop_reason,
                         loop_ms=r.loop_ms, first_unchanged=r.first_unchanged, extinct=r.extinct,
                         exchanges=r.exchanges, polls=r.polls, kernel_launches=r.kernel_launches,
-                        cells=self.config.width * self.config.height)
+                        cells=self.config.width * self.config.height, overlapped=r.overlapped)
         self.last_report = rep
         return rep
 

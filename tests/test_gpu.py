@@ -115,15 +115,17 @@ def test_termination_gpu(gpu, W, H, seed, density):
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("2x2", 4), ("2x4", 8), ("3x3", 9)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_multi_subdomain_one_gpu(gpu, spec, P, layout):
+@pytest.mark.parametrize("overlap", ["off", "on"])
+def test_multi_subdomain_one_gpu(gpu, spec, P, layout, overlap):
     W, H = 32 * 12, 300
     g = random_grid(W, H, 42)
     want = life_step_numpy(g, 150)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=150, decomp=spec, layout=layout, tmax=16), P,
-                         engine="hip", devices=[0])
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=150, decomp=spec, layout=layout, tmax=16, epoch=16,
+                                    overlap=overlap), P, engine="hip", devices=[0])
     grp.load(g)
     reps = grp.run()
     assert all(r.generations == 150 for r in reps)
+    assert all(r.overlapped == (overlap == "on") for r in reps)
     assert (grp.gather() == want).all()
 
 

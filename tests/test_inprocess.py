@@ -52,3 +52,46 @@ def test_random_init_decomposition_independent(native):
     grp = InProcessGroup(LifeConfig(128, 64, decomp="2x2"), 4, engine="cpu")
     grp.init_random(99)
     assert (grp.gather() == random_grid(128, 64, 99)).all()
+
+
+@pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x3", 3), ("2x2", 4), ("2x3", 6)])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+@pytest.mark.parametrize("tmax,epoch", [(4, 8), (8, 8), (4, 12), (2, 5)])
+def test_overlapped_exchange_matches_serial(native, spec, P, layout, tmax, epoch):
+    """Overlapped epochs (interior during the row exchange, edge strips in
+    scratch tiles) are bit-identical to the serial reference, including a
+    short final epoch (gens not a multiple of the epoch depth)."""
+    W, H = 192, 150
+    g = random_grid(W, H, 77 + tmax)
+    gens = 3 * epoch + epoch // 2 + 1
+    ref, _, _ = reference_run(g, gens)
+    cfg = LifeConfig(W, H, gen_limit=gens, decomp=spec, layout=layout, tmax=tmax, epoch=epoch, overlap="on")
+    grp = InProcessGroup(cfg, P, engine="cpu")
+    grp.load(g)
+    reps = grp.run()
+    assert all(r.overlapped for r in reps)
+    assert (grp.gather() == ref).all()
+
+
+@pytest.mark.parametrize("W,H,seed,density", CONVERGING)
+@pytest.mark.parametrize("lagged", [True, False])
+def test_overlapped_termination(native, W, H, seed, density, lagged):
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    cfg = LifeConfig(W, H, decomp="1x2", layout="u8", tmax=2, epoch=3, poll_gens=4, overlap="on",
+                     lagged_poll=lagged)
+    grp = InProcessGroup(cfg, 2, engine="cpu")
+    grp.load(g)
+    reps = grp.run()
+    assert {r.generations for r in reps} == {rgens}
+    assert all(r.overlapped == (H // 2 >= 7) for r in reps)
+    assert (grp.gather() == ref).all()
+
+
+def test_overlap_auto_needs_tall_tiles(native):
+    small = InProcessGroup(LifeConfig(64, 64, decomp="1x2", tmax=4, epoch=16), 2, engine="cpu")
+    tall = InProcessGroup(LifeConfig(64, 512, decomp="1x2", tmax=4, epoch=16), 2, engine="cpu")
+    assert not small.sims[0].native_engine.overlap()
+    assert tall.sims[0].native_engine.overlap()
+    off = InProcessGroup(LifeConfig(64, 512, decomp="1x2", tmax=4, epoch=16, overlap="off"), 2, engine="cpu")
+    assert not off.sims[0].native_engine.overlap()
