@@ -46,6 +46,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=1000, help="timed generations")
     ap.add_argument("--warmup", type=int, default=100, help="untimed generations")
     ap.add_argument("--size", type=int, default=32768, help="grid side (cells)")
+    ap.add_argument("--height", type=int, default=0, help="grid height if not square (experiments only)")
     ap.add_argument("--layout", default="bits", choices=["bits", "u8"])
     ap.add_argument("--engine", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
@@ -82,8 +83,9 @@ def main() -> int:
         transport = native().self_transport()
 
     S = a.size
+    Hg = a.height or S
     total = a.warmup + a.steps * a.repeats
-    cfg = LifeConfig(S, S, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
+    cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
                      poll_gens=a.poll, overlap=a.overlap)
     sim = Simulation(cfg, transport=transport, backend=backend)
     eng = sim.native_engine
@@ -112,7 +114,7 @@ def main() -> int:
             best = (dt, r)
     dt, r = best
     gens = max(1, executed)
-    value = float(S) * float(S) * gens / dt
+    value = float(S) * float(Hg) * gens / dt
     desc = sim.describe()
     if rank == 0:
         rec = {
@@ -130,11 +132,11 @@ def main() -> int:
                      if a.layout == "bits" else "u8 byte-per-cell (exact)",
             "data": "synthetic: on-device counter-based RNG random grid, density 0.5 (generate.sh distribution)",
             "config": {
-                "model": f"Game of Life B3/S23 torus {S}x{S}",
+                "model": f"Game of Life B3/S23 torus {S}x{Hg}",
                 "global_batch": 1,
-                "seq_len": S * S,
+                "seq_len": S * Hg,
                 "parallelism": f"{desc['decomp']} row/col tiles, {'rccl' if world > 1 else 'single'} halos",
-                "grid": f"{S}x{S}",
+                "grid": f"{S}x{Hg}",
                 "layout": a.layout,
                 "engine": backend.name(),
                 "tmax": desc["tmax"],
@@ -144,6 +146,7 @@ def main() -> int:
                 "exchanges": r.exchanges,
                 "polls": r.polls,
                 "kernel_launches": r.kernel_launches,
+                "overlapped_halo_exchange": r.overlapped,
                 "baseline": "8.9e8 cell-updates/s (best reference run in BASELINE.md: MPI, 4 ranks, 2048^2, CPU)",
             },
         }

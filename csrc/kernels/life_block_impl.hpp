@@ -462,24 +462,49 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
 }
 
 
-// Segment planning.  A wave owns a column strip and a segment of output
-// rows; its prologue is redundant work, so segments should be long, but the
-// launch must fill every SIMD: aim for one round of resident waves
-// (occupancy-limited), balanced segments no shorter than min_seg.
+// Segment planning.  A wave owns a column strip and a balanced segment of
+// output rows.  Its 2T-row prologue is redundant work (about T/2 rows' worth
+// of level bodies), so segments want to be long; the launch wants every SIMD
+// busy, and two resident waves per SIMD issue ~1.2x faster than one
+// (csrc/tools/ubench_level.hip: 97 vs 80 cycles per level body).  The
+// planner scores each segment count by the makespan of the most loaded SIMD:
+//     rounds * (seg_rows + T/2 + 2) * k * t(k),   k = resident waves/SIMD
+// and keeps the cheapest.  (Filling 1122 waves into 1024 SIMDs would put two
+// waves on a tenth of them and nearly double the kernel time; the model
+// prefers 1020 or 2040 waves there.)
 // Returns whether the skewed schedule applies (every segment >= T rows).
-inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int waves_per_round, int min_seg) {
-  const int64_t segs_round = std::max<int64_t>(1, waves_per_round / std::max(1, p.ncolw));
-  const int64_t smin = std::max<int64_t>(min_seg, 2 * int64_t(T));
-  int64_t nseg = std::min<int64_t>(segs_round, out_rows / smin);
-  nseg = std::max<int64_t>(1, nseg);
-  p.nseg = int(nseg);
-  p.seg_rows = int(out_rows / nseg);
-  p.seg_rem = int(out_rows % nseg);
+inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int simds, int occ, int min_seg,
+                 int target_waves) {
+  const int64_t smin = std::max<int64_t>({int64_t(min_seg), 2 * int64_t(T), 1});
+  const int64_t max_nseg = std::max<int64_t>(1, out_rows / smin);
+  int64_t best_n = 1;
+  if (target_waves > 0) {
+    best_n = std::min<int64_t>(max_nseg, std::max<int64_t>(1, target_waves / std::max(1, p.ncolw)));
+  } else {
+    static constexpr double kT[] = {0, 1.2, 1.0, 0.97, 0.95};
+    double best = 1e300;
+    for (int64_t n = 1; n <= max_nseg; ++n) {
+      const int64_t waves = int64_t(p.ncolw) * n;
+      const int64_t k = ceil_div(waves, int64_t(simds));
+      const int64_t rounds = ceil_div(k, int64_t(occ));
+      const int64_t kk = std::min<int64_t>(k, occ);
+      const double seg = double(ceil_div(out_rows, n));
+      const double cost = double(rounds) * (seg + 0.5 * T + 2) * double(kk) * kT[std::min<int64_t>(kk, 4)];
+      if (cost < best * 0.999) {
+        best = cost;
+        best_n = n;
+      }
+    }
+  }
+  p.nseg = int(best_n);
+  p.seg_rows = int(out_rows / best_n);
+  p.seg_rem = int(out_rows % best_n);
   return p.seg_rows >= T;
 }
 
+// Resident waves per SIMD (one 4-wave workgroup spreads over a CU's 4 SIMDs).
 template <int T, class IO, bool SKEW>
-int waves_per_round(const LifeTuning& tune) {
+int waves_per_simd() {
   static int cached = 0;
   if (!cached) {
     int blocks = 0;
@@ -487,16 +512,17 @@ int waves_per_round(const LifeTuning& tune) {
             hipSuccess ||
         blocks <= 0)
       blocks = 1;
-    cached = blocks * 4 * std::max(1, tune.cus);
+    cached = blocks;
   }
-  return tune.target_waves > 0 ? tune.target_waves : cached;
+  return cached;
 }
 
 template <int T, class IO>
 void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
   p.ncolw = int(ceil_div(p.Wp, 64 * IO::W - 2));
-  const int wpr = tune.skew ? waves_per_round<T, IO, true>(tune) : waves_per_round<T, IO, false>(tune);
-  const bool skew = plan(p, T, out_rows, wpr, tune.min_seg_rows) && tune.skew;
+  const int occ = tune.skew ? waves_per_simd<T, IO, true>() : waves_per_simd<T, IO, false>();
+  const bool skew =
+      plan(p, T, out_rows, 4 * std::max(1, tune.cus), occ, tune.min_seg_rows, tune.target_waves) && tune.skew;
   const int waves = p.ncolw * p.nseg;
   const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
   if (skew)

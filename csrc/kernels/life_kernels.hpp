@@ -31,7 +31,7 @@ enum Xlane : int { kXlaneDpp = 0, kXlaneBpermute = 1, kXlaneCarry = 2 };
 struct LifeTuning {
   int cus = 256;            // compute units of the device
   int target_waves = 0;     // waves per launch round (0 = occupancy x CUs x 4 SIMDs)
-  int min_seg_rows = 64;    // lower bound on rows per wave segment
+  int min_seg_rows = 16;    // lower bound on rows per wave segment
   bool skew = false;        // software-pipelined (skewed) level schedule
   int wpl_bits = 1;         // 32-cell words per lane, bit layout (1 or 2)
   int xlane = kXlaneDpp;    // cross-lane primitive

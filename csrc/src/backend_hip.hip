@@ -50,7 +50,7 @@ class HipBackend final : public Backend {
     cus_ = prop.multiProcessorCount;
     tune_.cus = cus_;
     tune_.target_waves = env_int("GOL_TARGET_WAVES", 0);
-    tune_.min_seg_rows = env_int("GOL_MIN_SEG_ROWS", 64);
+    tune_.min_seg_rows = env_int("GOL_MIN_SEG_ROWS", 16);
     tune_.skew = env_int("GOL_SKEW", 0) != 0;
     tune_.wpl_bits = env_int("GOL_WPL", 1);
     tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneDpp);

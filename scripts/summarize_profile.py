@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 outputs (kernel stats + PMC counter CSVs) into a
+markdown table for profiles/.  Usage: summarize_profile.py PROF_DIR > out.md"""
+import collections
+import csv
+import os
+import sys
+
+
+def short(name: str) -> str:
+    n = name.replace("gol::hipk::", "").replace("(anonymous namespace)::", "").replace("lb::", "")
+    return n.split("(")[0][:90] if "life_block_kernel" not in n else n[:110]
+
+
+def main(d: str) -> None:
+    stats = os.path.join(d, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        rows = list(csv.DictReader(open(stats)))
+        print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
+        print("| kernel | calls | total ms | avg us | % |")
+        print("|---|---:|---:|---:|---:|")
+        for r in rows:
+            print(f"| `{short(r['Name'])}` | {r['Calls']} | {int(r['TotalDurationNs'])/1e6:.3f} | "
+                  f"{float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.2f} |")
+        print()
+    for sub in sorted(os.listdir(d)):
+        f = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        agg = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if "life_block_kernel" not in r["Kernel_Name"]:
+                continue
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+        if not agg:
+            continue
+        print(f"## PMC set `{sub}` (summed over all life_block_kernel dispatches)\n")
+        print("| counter | value |")
+        print("|---|---:|")
+        for k, v in sorted(agg.items()):
+            print(f"| {k} | {v:.4g} |")
+        print()
+        derived = []
+        if "SQ_INSTS_VALU" in agg and "SQ_WAVES" in agg:
+            derived.append(("VALU instructions per wave", agg["SQ_INSTS_VALU"] / agg["SQ_WAVES"]))
+        if "SQ_ACTIVE_INST_VALU" in agg and "SQ_BUSY_CYCLES" in agg:
+            derived.append(("SQ_ACTIVE_INST_VALU / SQ_BUSY_CYCLES", agg["SQ_ACTIVE_INST_VALU"] / agg["SQ_BUSY_CYCLES"]))
+        if "SQ_WAIT_INST_ANY" in agg and "SQ_WAVE_CYCLES" in agg:
+            derived.append(("wave cycles waiting on any instruction (fraction)",
+                            agg["SQ_WAIT_INST_ANY"] / agg["SQ_WAVE_CYCLES"]))
+        if "FETCH_SIZE" in agg:
+            derived.append(("HBM fetch, GB (FETCH_SIZE is KB)", agg["FETCH_SIZE"] / 1e6))
+        if derived:
+            print("| derived | value |")
+            print("|---|---:|")
+            for k, v in derived:
+                print(f"| {k} | {v:.4g} |")
+            print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
