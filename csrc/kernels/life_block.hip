@@ -35,11 +35,13 @@ const char* xlane_name(int x) {
 
 std::string life_block_variant(Layout layout, const LifeTuning& tune) {
   const int w = words_per_lane(layout, tune);
+  if (layout == Layout::U8 && tune.u8_lds) return "u8 lds-tiled single-step";
   return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=" + std::to_string(w) + " " +
          xlane_name(xlane_of(layout, w, tune)) + (tune.skew ? " skew" : "");
 }
 
 int life_block_max_T(Layout layout, const LifeTuning& tune) {
+  if (layout == Layout::U8 && tune.u8_lds) return 1;
   // Register budget for 2 waves/SIMD (<= 256 VGPRs): T * words-per-lane <= 16.
   return words_per_lane(layout, tune) >= 2 ? 8 : 16;
 }
@@ -66,7 +68,9 @@ void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t s
   p.changed = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
   const int64_t rows = a.row_hi - a.row_lo;
   const int x = xlane_of(g.layout, w, tune);
-  if (g.layout == Layout::U8) {
+  if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {
+    launch_life_step_lds(a, stream);
+  } else if (g.layout == Layout::U8) {
     (x == kXlaneCarry ? launch_u8_w1_carry : launch_u8_w1_dpp)(p, rows, a.T, tune, stream);
   } else if (w == 2) {
     (x == kXlaneCarry ? launch_bits_w2_carry : launch_bits_w2_dpp)(p, rows, a.T, tune, stream);

@@ -35,6 +35,7 @@ struct LifeTuning {
   bool skew = false;        // software-pipelined (skewed) level schedule
   int wpl_bits = 1;         // 32-cell words per lane, bit layout (1 or 2)
   int xlane = kXlaneDpp;    // cross-lane primitive
+  bool u8_lds = false;      // byte layout: single-step LDS-tiled kernel (T = 1)
 };
 
 void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream);
@@ -55,6 +56,9 @@ GOL_LIFE_VARIANT(launch_bits_w1_carry);
 GOL_LIFE_VARIANT(launch_bits_w2_carry);
 GOL_LIFE_VARIANT(launch_u8_w1_dpp);
 GOL_LIFE_VARIANT(launch_u8_w1_carry);
+
+// Single-generation LDS-tiled byte-layout kernel (life_step_lds.hip).
+void launch_life_step_lds(const BlockArgs& a, hipStream_t stream);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

@@ -1,0 +1,157 @@
+// life_step_lds: one generation of B3/S23 on the byte-per-cell layout,
+// staged through LDS - the direct MI355X counterpart of the reference's CUDA
+// evolve kernel (src/game_cuda.cu:128-148: one thread per cell, 32x32
+// blocks, nine 1-byte global loads per cell, no shared memory) with its
+// compare/empty reductions (src/game_cuda.cu:76-126) fused in.
+//
+// Design (CDNA4):
+//   * A 256-thread workgroup (4 x wave64) owns a 64-row x 1024-cell tile.
+//     The tile plus a 1-row / 16-byte halo is loaded with 16-byte vector
+//     loads into LDS (66 x 1056 B = 68 KiB, two workgroups per CU), so every
+//     input byte is fetched from HBM once per generation.
+//   * Thread (tx, ty) owns 16 consecutive cells (one uint4) of 16 rows and
+//     slides a 3-row window down them: each LDS row is read once per thread
+//     (one ds_read_b128 + two ds_read_b32 for the neighbour bytes).
+//   * SWAR byte arithmetic: cells are 0/1 bytes, so horizontal 3-sums
+//     (v_alignbyte funnel shifts + v_add3) and the 3x3 sum S <= 9 never carry
+//     across bytes; "S == 3" / "S == 4" per byte come from
+//     ((S ^ k) + 0x7f7f7f7f) & 0x80808080 (bytes of S ^ k are <= 15).
+//   * The changed flag (next != current over owned cells) is reduced with
+//     __ballot and one atomicOr per wave.
+// It is HBM-bound (1 B read + 1 B write per cell-update); the temporal
+// blocking kernel (life_block_impl.hpp) is the fast path.  This one is kept
+// as the single-step u8 baseline ("8192^2 LDS-tiled u8 kernel")
+// and selected with GOL_U8_KERNEL=lds (forces T = 1).
+#include <hip/hip_runtime.h>
+
+#include "gol/common.hpp"
+#include "life_kernels.hpp"
+
+namespace gol {
+namespace hipk {
+namespace {
+
+constexpr int kTileW = 1024;           // cells per workgroup tile
+constexpr int kTileH = 64;             // rows per workgroup tile
+constexpr int kRowsPerThread = 16;     // 4 row groups of 16
+constexpr int kHaloB = 16;             // bytes of column halo on each side
+constexpr int kLdsStride = kTileW + 2 * kHaloB;  // 1056
+constexpr int kLdsRows = kTileH + 2;
+constexpr int kChunksPerRow = kLdsStride / 16;   // 66
+
+__device__ __forceinline__ uint32_t is_val(uint32_t s, uint32_t k) {
+  // bit 7 of each byte set where the byte of s != k (bytes of s ^ k <= 15)
+  return ((s ^ k) + 0x7F7F7F7Fu) & 0x80808080u;
+}
+
+__device__ __forceinline__ uint32_t rule_bytes(uint32_t s, uint32_t c) {
+  const uint32_t ne3 = is_val(s, 0x03030303u), ne4 = is_val(s, 0x04040404u);
+  // next = (S == 3) | (c & S == 4), computed in bit 7 of every byte
+  const uint32_t hi = (~ne3 | (~ne4 & (c << 7))) & 0x80808080u;
+  return hi >> 7;
+}
+
+__global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __restrict__ in,
+                                                            uint8_t* __restrict__ out, int64_t pitch,
+                                                            int64_t row_lo, int64_t row_hi, int64_t Wc,
+                                                            int64_t own_c0, int64_t own_c1,
+                                                            uint32_t* changed) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kLdsRows * kLdsStride];
+  const int64_t r0 = row_lo + int64_t(blockIdx.y) * kTileH;   // first output row
+  const int64_t c0 = int64_t(blockIdx.x) * kTileW;            // first output cell
+  const int tid = threadIdx.x;
+
+  // Stage rows r0-1 .. r0+64 and cells c0-16 .. c0+1040 (16-byte chunks).
+  for (int idx = tid; idx < kLdsRows * kChunksPerRow; idx += 256) {
+    const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
+    const int64_t gr = r0 - 1 + lr;
+    const int64_t gc = c0 - kHaloB + 16 * int64_t(ch);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (gr < row_hi + 1 && gc >= 0 && gc + 16 <= pitch)
+      v = *reinterpret_cast<const uint4*>(in + gr * pitch + gc);
+    *reinterpret_cast<uint4*>(tile + lr * kLdsStride + 16 * ch) = v;
+  }
+  __syncthreads();
+
+  const int tx = tid & 63, ty = tid >> 6;
+  const int64_t cell = c0 + 16 * int64_t(tx);
+  const int lcol = kHaloB + 16 * tx;
+  // Owned-cell byte masks for the changed flag.
+  uint32_t own[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int64_t x = cell + 4 * k + b;
+      if (x >= own_c0 && x < own_c1) m |= 0xFFu << (8 * b);
+    }
+    own[k] = m;
+  }
+
+  auto hrow = [&](int lr, uint32_t (&h)[4], uint32_t (&c)[4]) {
+    const uint8_t* p = tile + lr * kLdsStride + lcol;
+    const uint4 w = *reinterpret_cast<const uint4*>(p);
+    const uint32_t lw = *reinterpret_cast<const uint32_t*>(p - 4);
+    const uint32_t rw = *reinterpret_cast<const uint32_t*>(p + 16);
+    c[0] = w.x;
+    c[1] = w.y;
+    c[2] = w.z;
+    c[3] = w.w;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t prev = k == 0 ? lw : c[k - 1];
+      const uint32_t next = k == 3 ? rw : c[k + 1];
+      const uint32_t l = __builtin_amdgcn_alignbyte(c[k], prev, 3);  // cell x-1
+      const uint32_t r = __builtin_amdgcn_alignbyte(next, c[k], 1);  // cell x+1
+      h[k] = l + c[k] + r;
+    }
+  };
+
+  uint32_t ha[4], hb[4], hc[4], ca[4], cb[4], cc[4];
+  const int lr0 = ty * kRowsPerThread;  // LDS row of (first output row - 1)
+  hrow(lr0, ha, ca);
+  hrow(lr0 + 1, hb, cb);
+  uint32_t diff = 0;
+  for (int i = 0; i < kRowsPerThread; ++i) {
+    const int64_t row = r0 + ty * kRowsPerThread + i;
+    if (row >= row_hi) break;
+    hrow(lr0 + i + 2, hc, cc);
+    uint32_t nx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      nx[k] = rule_bytes(ha[k] + hb[k] + hc[k], cb[k]);
+      diff |= (nx[k] ^ cb[k]) & own[k];
+    }
+    if (cell < Wc) *reinterpret_cast<uint4*>(out + row * pitch + cell) = make_uint4(nx[0], nx[1], nx[2], nx[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ha[k] = hb[k];
+      hb[k] = hc[k];
+      ca[k] = cb[k];
+      cb[k] = cc[k];
+    }
+  }
+  if (changed && __ballot(diff != 0u) != 0ull && (tid & 63) == 0) atomicOr(changed, 1u);
+}
+
+}  // namespace
+
+void launch_life_step_lds(const BlockArgs& a, hipStream_t stream) {
+  const TileGeom& g = a.g;
+  GOL_REQUIRE(g.layout == Layout::U8, "life_step_lds: byte layout only");
+  GOL_REQUIRE(a.T == 1, "life_step_lds: single-step kernel (T = 1)");
+  GOL_REQUIRE(a.row_lo >= 1 && a.row_hi + 1 <= g.R() && a.row_lo < a.row_hi,
+              "life_step_lds: row range outside the tile");
+  GOL_REQUIRE(g.pitch % 16 == 0, "life_step_lds: pitch must be 16-byte aligned");
+  const int64_t rows = a.row_hi - a.row_lo;
+  const dim3 grid(unsigned(ceil_div(g.Wc(), int64_t(kTileW))), unsigned(ceil_div(rows, int64_t(kTileH))));
+  GOL_REQUIRE(ceil_div(rows, int64_t(kTileH)) < (int64_t(1) << 31), "life_step_lds: too many rows");
+  uint32_t* changed = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
+  hipLaunchKernelGGL(life_step_lds_kernel, grid, dim3(256), 0, stream, static_cast<const uint8_t*>(a.in),
+                     static_cast<uint8_t*>(a.out), g.pitch, a.row_lo, a.row_hi, g.Wc(), g.cell0(),
+                     g.cell0() + g.W, changed);
+}
+
+}  // namespace hipk
+}  // namespace gol

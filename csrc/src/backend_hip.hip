@@ -54,6 +54,7 @@ class HipBackend final : public Backend {
     tune_.skew = env_int("GOL_SKEW", 0) != 0;
     tune_.wpl_bits = env_int("GOL_WPL", 1);
     tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneDpp);
+    if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
   }
   ~HipBackend() override {
     hipSetDevice(dev_);

@@ -164,7 +164,7 @@ class Simulation:
                 "layout": self.config.resolved_layout(), "decomp": d.describe(),
                 "rank": self.rank, "ranks": d.nranks(), "tile_rows": g.H, "tile_cols": g.W,
                 "halo_rows": g.Dv, "halo_words": g.hw, "tmax": self._eng.tmax,
-                "epoch": self._eng.epoch_depth, "pitch": g.pitch}
+                "epoch": self._eng.epoch_depth, "pitch": g.pitch, "overlap": self._eng.overlap()}
 
     # -- state -----------------------------------------------------------
     def load(self, grid: np.ndarray) -> None:

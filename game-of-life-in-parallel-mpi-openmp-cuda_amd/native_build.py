@@ -34,7 +34,8 @@ HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/t
 LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "u8_w1_dpp",
                  "u8_w1_carry"]
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
-            *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/tile_ops.hip"]
+            *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
+            "kernels/tile_ops.hip"]
 BIND_SRCS = ["src/bindings.cpp"]
 CLI_MAIN = "tools/gol_main.cpp"
 GEN_MAIN = "tools/gol_gen.cpp"

@@ -82,6 +82,27 @@ def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
     assert (life_step(g, gens, engine="hip", layout="u8", tmax=tmax) == want).all()
 
 
+@pytest.mark.parametrize("W,H", [(1, 1), (5, 3), (100, 70), (1023, 65), (1025, 200), (3000, 129)])
+def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H):
+    """The LDS-tiled single-step byte kernel (GOL_U8_KERNEL=lds, T = 1)."""
+    monkeypatch.setenv("GOL_U8_KERNEL", "lds")
+    g = random_grid(W, H, W ^ H)
+    want = life_step_torch(g, 9, device="cuda")
+    assert (life_step(g, 9, engine="hip", layout="u8") == want).all()
+    sim = Simulation(LifeConfig(W, H, layout="u8"), engine="hip")
+    assert "lds" in sim.describe()["backend"] and sim.describe()["tmax"] == 1
+
+
+@pytest.mark.parametrize("W,H,seed,density", CONVERGING)
+def test_u8_lds_termination(gpu, monkeypatch, W, H, seed, density):
+    monkeypatch.setenv("GOL_U8_KERNEL", "lds")
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    out, rep = simulate(g, 1000, engine="hip", layout="u8")
+    assert rep.generations == rgens
+    assert (out == ref).all()
+
+
 def test_hip_matches_cpu_backend_long_run(gpu):
     g = random_grid(1024, 512, 5)
     a = life_step(g, 300, engine="hip")
