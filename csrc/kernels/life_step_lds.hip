@@ -11,7 +11,7 @@
 //     input byte is fetched from HBM once per generation.
 //   * Thread (tx, ty) owns 16 consecutive cells (one uint4) of 16 rows and
 //     slides a 3-row window down them: each LDS row is read once per thread
-//     (one ds_read_b128 + two ds_read_b32 for the neighbour bytes).
+//     (one ds_read_b128; the neighbour words move between lanes with DPP).
 //   * SWAR byte arithmetic: cells are 0/1 bytes, so horizontal 3-sums
 //     (v_alignbyte funnel shifts + v_add3) and the 3x3 sum S <= 9 never carry
 //     across bytes; "S == 3" / "S == 4" per byte come from
@@ -61,15 +61,32 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
   const int64_t c0 = int64_t(blockIdx.x) * kTileW;            // first output cell
   const int tid = threadIdx.x;
 
-  // Stage rows r0-1 .. r0+64 and cells c0-16 .. c0+1040 (16-byte chunks).
-  for (int idx = tid; idx < kLdsRows * kChunksPerRow; idx += 256) {
+  // Stage rows r0-1 .. r0+64 and cells c0-16 .. c0+1040 (16-byte chunks):
+  // all 17 loads of a thread are issued before the first LDS write.
+  constexpr int kChunks = kLdsRows * kChunksPerRow;      // 4356
+  constexpr int kPerThread = (kChunks + 255) / 256;      // 18
+  uint4 v[kPerThread];
+  bool ok[kPerThread];
+#pragma unroll
+  for (int k = 0; k < kPerThread; ++k) {
+    const int idx = tid + 256 * k;
     const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
     const int64_t gr = r0 - 1 + lr;
     const int64_t gc = c0 - kHaloB + 16 * int64_t(ch);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (gr < row_hi + 1 && gc >= 0 && gc + 16 <= pitch)
-      v = *reinterpret_cast<const uint4*>(in + gr * pitch + gc);
-    *reinterpret_cast<uint4*>(tile + lr * kLdsStride + 16 * ch) = v;
+    // Unconditional load from a clamped address, zeroed afterwards, so the
+    // loads are not serialised behind branches.
+    const int64_t grc = gr < row_hi + 1 ? gr : row_hi;
+    const int64_t gcc = gc < 0 ? 0 : (gc + 16 <= pitch ? gc : pitch - 16);
+    v[k] = *reinterpret_cast<const uint4*>(in + grc * pitch + gcc);
+    ok[k] = idx < kChunks && gr < row_hi + 1 && gc >= 0 && gc + 16 <= pitch;
+  }
+#pragma unroll
+  for (int k = 0; k < kPerThread; ++k)
+    if (!ok[k]) v[k] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < kPerThread; ++k) {
+    const int idx = tid + 256 * k;
+    if (idx < kChunks) *reinterpret_cast<uint4*>(tile + idx * 16) = v[k];
   }
   __syncthreads();
 
@@ -89,15 +106,20 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
     own[k] = m;
   }
 
+  // Neighbour words come from the adjacent lanes (DPP wave shifts); only the
+  // wave's edge lanes read them from LDS (strided b32 reads would conflict).
+  const bool edge_l = tx == 0, edge_r = tx == 63;
   auto hrow = [&](int lr, uint32_t (&h)[4], uint32_t (&c)[4]) {
     const uint8_t* p = tile + lr * kLdsStride + lcol;
     const uint4 w = *reinterpret_cast<const uint4*>(p);
-    const uint32_t lw = *reinterpret_cast<const uint32_t*>(p - 4);
-    const uint32_t rw = *reinterpret_cast<const uint32_t*>(p + 16);
     c[0] = w.x;
     c[1] = w.y;
     c[2] = w.z;
     c[3] = w.w;
+    uint32_t lw = __builtin_amdgcn_mov_dpp(c[3], 0x138, 0xF, 0xF, true);  // wave_shr:1
+    uint32_t rw = __builtin_amdgcn_mov_dpp(c[0], 0x130, 0xF, 0xF, true);  // wave_shl:1
+    if (edge_l) lw = *reinterpret_cast<const uint32_t*>(p - 4);
+    if (edge_r) rw = *reinterpret_cast<const uint32_t*>(p + 16);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t prev = k == 0 ? lw : c[k - 1];

@@ -29,7 +29,7 @@ def main(d: str) -> None:
             continue
         agg = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
-            if "life_block_kernel" not in r["Kernel_Name"]:
+            if not any(k in r["Kernel_Name"] for k in ("life_block_kernel", "life_step_lds")):
                 continue
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
         if not agg:
