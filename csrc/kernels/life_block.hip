@@ -69,7 +69,7 @@ void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t s
   const int64_t rows = a.row_hi - a.row_lo;
   const int x = xlane_of(g.layout, w, tune);
   if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {
-    launch_life_step_lds(a, stream);
+    launch_life_step_lds(a, tune.lds_rows, stream);
   } else if (g.layout == Layout::U8) {
     (x == kXlaneCarry ? launch_u8_w1_carry : launch_u8_w1_dpp)(p, rows, a.T, tune, stream);
   } else if (w == 2) {

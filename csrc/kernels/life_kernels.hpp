@@ -36,6 +36,7 @@ struct LifeTuning {
   int wpl_bits = 1;         // 32-cell words per lane, bit layout (1 or 2)
   int xlane = kXlaneDpp;    // cross-lane primitive
   bool u8_lds = false;      // byte layout: single-step LDS-tiled kernel (T = 1)
+  int lds_rows = 32;        // rows per LDS tile (32 or 64)
 };
 
 void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream);
@@ -58,7 +59,7 @@ GOL_LIFE_VARIANT(launch_u8_w1_dpp);
 GOL_LIFE_VARIANT(launch_u8_w1_carry);
 
 // Single-generation LDS-tiled byte-layout kernel (life_step_lds.hip).
-void launch_life_step_lds(const BlockArgs& a, hipStream_t stream);
+void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

@@ -32,11 +32,8 @@ namespace hipk {
 namespace {
 
 constexpr int kTileW = 1024;           // cells per workgroup tile
-constexpr int kTileH = 64;             // rows per workgroup tile
-constexpr int kRowsPerThread = 16;     // 4 row groups of 16
 constexpr int kHaloB = 16;             // bytes of column halo on each side
 constexpr int kLdsStride = kTileW + 2 * kHaloB;  // 1056
-constexpr int kLdsRows = kTileH + 2;
 constexpr int kChunksPerRow = kLdsStride / 16;   // 66
 
 __device__ __forceinline__ uint32_t is_val(uint32_t s, uint32_t k) {
@@ -51,20 +48,25 @@ __device__ __forceinline__ uint32_t rule_bytes(uint32_t s, uint32_t c) {
   return hi >> 7;
 }
 
+// kTileH rows per workgroup tile (4 row groups of kTileH / 4): 64 rows use
+// 68 KiB of LDS (2 workgroups per CU), 32 rows 35 KiB (4 per CU).
+template <int kTileH>
 __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __restrict__ in,
                                                             uint8_t* __restrict__ out, int64_t pitch,
                                                             int64_t row_lo, int64_t row_hi, int64_t Wc,
                                                             int64_t own_c0, int64_t own_c1,
                                                             uint32_t* changed) {
+  constexpr int kLdsRows = kTileH + 2;
+  constexpr int kRowsPerThread = kTileH / 4;
   __shared__ __attribute__((aligned(16))) uint8_t tile[kLdsRows * kLdsStride];
   const int64_t r0 = row_lo + int64_t(blockIdx.y) * kTileH;   // first output row
   const int64_t c0 = int64_t(blockIdx.x) * kTileW;            // first output cell
   const int tid = threadIdx.x;
 
   // Stage rows r0-1 .. r0+64 and cells c0-16 .. c0+1040 (16-byte chunks):
-  // all 17 loads of a thread are issued before the first LDS write.
-  constexpr int kChunks = kLdsRows * kChunksPerRow;      // 4356
-  constexpr int kPerThread = (kChunks + 255) / 256;      // 18
+  // all loads of a thread are issued before the first LDS write.
+  constexpr int kChunks = kLdsRows * kChunksPerRow;
+  constexpr int kPerThread = (kChunks + 255) / 256;
   uint4 v[kPerThread];
   bool ok[kPerThread];
 #pragma unroll
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
 
 }  // namespace
 
-void launch_life_step_lds(const BlockArgs& a, hipStream_t stream) {
+void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream) {
   const TileGeom& g = a.g;
   GOL_REQUIRE(g.layout == Layout::U8, "life_step_lds: byte layout only");
   GOL_REQUIRE(a.T == 1, "life_step_lds: single-step kernel (T = 1)");
@@ -167,12 +169,13 @@ void launch_life_step_lds(const BlockArgs& a, hipStream_t stream) {
               "life_step_lds: row range outside the tile");
   GOL_REQUIRE(g.pitch % 16 == 0, "life_step_lds: pitch must be 16-byte aligned");
   const int64_t rows = a.row_hi - a.row_lo;
-  const dim3 grid(unsigned(ceil_div(g.Wc(), int64_t(kTileW))), unsigned(ceil_div(rows, int64_t(kTileH))));
-  GOL_REQUIRE(ceil_div(rows, int64_t(kTileH)) < (int64_t(1) << 31), "life_step_lds: too many rows");
   uint32_t* changed = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
-  hipLaunchKernelGGL(life_step_lds_kernel, grid, dim3(256), 0, stream, static_cast<const uint8_t*>(a.in),
-                     static_cast<uint8_t*>(a.out), g.pitch, a.row_lo, a.row_hi, g.Wc(), g.cell0(),
-                     g.cell0() + g.W, changed);
+  const int th = lds_rows == 32 ? 32 : 64;
+  GOL_REQUIRE(ceil_div(rows, int64_t(th)) < (int64_t(1) << 31), "life_step_lds: too many rows");
+  const dim3 grid(unsigned(ceil_div(g.Wc(), int64_t(kTileW))), unsigned(ceil_div(rows, int64_t(th))));
+  auto k = th == 32 ? life_step_lds_kernel<32> : life_step_lds_kernel<64>;
+  hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
+                     g.pitch, a.row_lo, a.row_hi, g.Wc(), g.cell0(), g.cell0() + g.W, changed);
 }
 
 }  // namespace hipk

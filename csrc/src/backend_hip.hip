@@ -55,6 +55,7 @@ class HipBackend final : public Backend {
     tune_.wpl_bits = env_int("GOL_WPL", 1);
     tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneDpp);
     if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
+    tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
   }
   ~HipBackend() override {
     hipSetDevice(dev_);

@@ -83,9 +83,11 @@ def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
 
 
 @pytest.mark.parametrize("W,H", [(1, 1), (5, 3), (100, 70), (1023, 65), (1025, 200), (3000, 129)])
-def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H):
+@pytest.mark.parametrize("lds_rows", [32, 64])
+def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H, lds_rows):
     """The LDS-tiled single-step byte kernel (GOL_U8_KERNEL=lds, T = 1)."""
     monkeypatch.setenv("GOL_U8_KERNEL", "lds")
+    monkeypatch.setenv("GOL_LDS_ROWS", str(lds_rows))
     g = random_grid(W, H, W ^ H)
     want = life_step_torch(g, 9, device="cuda")
     assert (life_step(g, 9, engine="hip", layout="u8") == want).all()
