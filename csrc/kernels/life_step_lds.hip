@@ -17,7 +17,7 @@
 //     across bytes; "S == 3" / "S == 4" per byte come from
 //     ((S ^ k) + 0x7f7f7f7f) & 0x80808080 (bytes of S ^ k are <= 15).
 //   * The changed flag (next != current over owned cells) is reduced with
-//     __ballot and one atomicOr per wave.
+//     __ballot and one plain store per wave.
 // It is HBM-bound (1 B read + 1 B write per cell-update); the temporal
 // blocking kernel (life_block_impl.hpp) is the fast path.  This one is kept
 // as the single-step u8 baseline ("8192^2 LDS-tiled u8 kernel")
@@ -156,7 +156,8 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
       cb[k] = cc[k];
     }
   }
-  if (changed && __ballot(diff != 0u) != 0ull && (tid & 63) == 0) atomicOr(changed, 1u);
+  // Idempotent plain store (an atomic per wave to one address serialises in L2).
+  if (changed && __ballot(diff != 0u) != 0ull && (tid & 63) == 0) *changed = 1u;
 }
 
 }  // namespace

@@ -87,7 +87,7 @@ __global__ void alive_k(const uint8_t* buf, int64_t pitch, int64_t row0, int64_t
   for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
   if ((threadIdx.x & 63) == 0 && local) {
     if (count) atomicAdd(count, local);
-    if (any_flag) atomicOr(any_flag, 1u);
+    if (any_flag) *any_flag = 1u;  // idempotent: no atomic needed
   }
 }
 
