@@ -1,0 +1,87 @@
+"""Checkpoint / resume: a run interrupted at a checkpoint and
+resumed reproduces the uninterrupted run exactly - final grid and the
+reference's "Generations" line, including the similarity-counter phase."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from gol_amd import LifeConfig, Simulation, random_grid, reference_run
+from gol_amd.utils import io
+from gol_amd.utils.checkpoint import load_checkpoint, run_with_checkpoints, save_checkpoint
+
+from golden import CONVERGING
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _cli(args, cwd):
+    env = dict(os.environ, PYTHONPATH=REPO, GOL_NO_AUTOBUILD="1")
+    r = subprocess.run([sys.executable, "-m", "gol_amd", *map(str, args)], cwd=cwd, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+def _gens(stdout):
+    return int(next(ln for ln in stdout.splitlines() if ln.startswith("Generations")).split()[-1])
+
+
+def test_resume_matches_uninterrupted_random(native, tmp_path):
+    W, H = 96, 64
+    g = random_grid(W, H, 3)
+    inp = tmp_path / "in.txt"
+    io.write_grid(str(inp), g)
+    ck = tmp_path / "ck"
+    _cli([W, H, inp, "--engine", "cpu", "--gens", 20, "--checkpoint-every", 7, "--checkpoint-dir", ck,
+          "--output", tmp_path / "a.out"], tmp_path)
+    meta = json.loads((ck / "meta.json").read_text())
+    assert meta["generation"] == 14
+    out = _cli([W, H, "--engine", "cpu", "--resume", ck, "--gens", 50, "--output", tmp_path / "b.out"], tmp_path)
+    ref, rgens, _ = reference_run(g, 50)
+    assert _gens(out) == rgens == 50
+    assert (io.read_grid(str(tmp_path / "b.out"), W, H) == ref).all()
+
+
+@pytest.mark.parametrize("W,H,seed,density", CONVERGING[:5])
+def test_resume_keeps_generation_count_and_phase(native, tmp_path, W, H, seed, density):
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    assert rgens < 1000
+    # checkpoint at a generation that is not a multiple of the similarity period
+    k = max(1, min(rgens - 1, 5))
+    sim = Simulation(LifeConfig(W, H, gen_limit=1000, layout="u8"), engine="cpu")
+    sim.load(g)
+    sim.native_engine.run_until(k)
+    save_checkpoint(sim, str(tmp_path / "ck"))
+    cfg, grid = load_checkpoint(str(tmp_path / "ck"))
+    assert cfg.start_gen == k
+    sim2 = Simulation(cfg, engine="cpu")
+    sim2.load_text(str(grid))
+    rep = sim2.run()
+    assert rep.generations == rgens
+    assert (sim2.tile() == ref).all()
+
+
+def test_run_with_checkpoints_equals_plain_run(native, tmp_path):
+    for W, H, seed, density in CONVERGING[:3]:
+        g = random_grid(W, H, seed, density)
+        ref, rgens, _ = reference_run(g)
+        sim = Simulation(LifeConfig(W, H, gen_limit=1000), engine="cpu")
+        sim.load(g)
+        rep = run_with_checkpoints(sim, 4, str(tmp_path / f"ck{seed}"))
+        assert rep.generations == rgens
+        assert (sim.tile() == ref).all()
+
+
+def test_checkpoint_grid_is_a_valid_reference_input(native, tmp_path):
+    g = random_grid(40, 30, 9)
+    sim = Simulation(LifeConfig(40, 30), engine="cpu")
+    sim.load(g)
+    sim.advance(13)
+    d = save_checkpoint(sim, str(tmp_path / "ck"))
+    text = (d / "grid.txt").read_text()
+    assert text == io.format_text(np.asarray(sim.tile()))
