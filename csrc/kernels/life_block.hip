@@ -37,7 +37,8 @@ std::string life_block_variant(Layout layout, const LifeTuning& tune) {
   const int w = words_per_lane(layout, tune);
   if (layout == Layout::U8 && tune.u8_lds) return "u8 lds-tiled single-step";
   return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=" + std::to_string(w) + " " +
-         xlane_name(xlane_of(layout, w, tune)) + (tune.skew ? " skew" : "");
+         xlane_name(xlane_of(layout, w, tune)) + (tune.skew ? " skew" : "") +
+         (tune.split > 0 ? " split" : tune.split < 0 ? " split=auto" : "");
 }
 
 int life_block_max_T(Layout layout, const LifeTuning& tune) {

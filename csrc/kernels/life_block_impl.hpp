@@ -275,16 +275,71 @@ __device__ __forceinline__ Vec<W> levels_full(Levels<T, W>& st, const Vec<W>& cu
 // Triangular prologue, fully unrolled: at step K only levels 1..K/2 hold
 // valid rows, so only those are evaluated; level K/2+1 just fills its
 // window.
-template <int T, class IO, int K>
-__device__ __forceinline__ void prologue_tri(Levels<T, IO::W>& st, RowReader<IO>& rd) {
+template <int T, class IO, int K, class Save, class Bottom>
+__device__ __forceinline__ void prologue_tri(Levels<T, IO::W>& st, RowReader<IO>& rd, const Save& save,
+                                             const Bottom& bottom) {
   if constexpr (K < 2 * T) {
     constexpr int S = K % 3;
     constexpr int nfull = K / 2;
     const Vec<IO::W> cur = levels_full<T, IO, S, 0, nfull>(st, rd.template take<S>(K));
+    // Split schedule: level `nfull` rows in0 + nfull (K even) and
+    // in0 + nfull + 1 (K odd) are the top boundary state.
+    if constexpr (nfull >= 1 && nfull < T) save(nfull, K - 2 * nfull, cur);
     if constexpr (nfull < T) level_store<T, IO, S, nfull>(st, cur);
-    prologue_tri<T, IO, K + 1>(st, rd);
+    prologue_tri<T, IO, K + 1, Save, Bottom>(st, rd, save, bottom);
   }
 }
+
+struct NoSave {
+  template <class V>
+  __device__ __forceinline__ void operator()(int, int, const V&) const {}
+};
+
+struct NoBottom {
+  template <int S, class St>
+  __device__ __forceinline__ void at(const St&, int) const {}
+};
+
+// Boundary level states of the split schedule.  side 0 = bottom of the
+// segment above boundary bnd (level L rows b-L-2, b-L-1 as j = 0, 1), side 1
+// = top of the segment below (rows b+L, b+L+1).  Layout is column-major:
+// the 2(T-1) states of one word are contiguous, so a lane addresses all of
+// them from one base pointer with immediate offsets (per-state row pointers
+// would each need their own 64-bit address registers).
+template <int T>
+__device__ __forceinline__ uint32_t* state_base(const LifeBlockParams& p, int bnd, int side, int c) {
+  return p.state + ((int64_t(bnd) * 2 + side) * p.state_pitch + c) * (2 * (T - 1));
+}
+
+// Lanes without a real target (no boundary, wave-halo or out-of-tile words)
+// store into a dummy slot (boundary index nseg - 1) instead of branching:
+// divergent branches in the unrolled prologue cost ~160 extra VGPRs.
+template <int T, int W>
+struct StateSaver {
+  uint32_t* base[W];
+  __device__ __forceinline__ void operator()(int L, int j, const Vec<W>& v) const {
+#pragma unroll
+    for (int i = 0; i < W; ++i) base[i][2 * (L - 1) + j] = v.w[i];
+  }
+};
+
+// Bottom boundary state: after step k = kend-2 (kend-1) window slot S holds
+// level L row s1-2-L (s1-1-L) for every level; saved as j = 0 (1).
+template <int T, int W>
+struct BottomSaver {
+  uint32_t* base[W];
+  bool any;  // wave-uniform: this segment has a boundary below
+  int kend;
+  template <int S, class St>
+  __device__ __forceinline__ void at(const St& st, int k) const {
+    if (!any || k < kend - 2) return;  // wave-uniform
+    const int j = k - (kend - 2);
+#pragma unroll
+    for (int L = 1; L < T; ++L)
+#pragma unroll
+      for (int i = 0; i < W; ++i) base[i][2 * (L - 1) + j] = st.cc[L][S].w[i];
+  }
+};
 
 // Output of one row: lanes store the words they own (not the wave halos).
 template <class IO>
@@ -371,19 +426,29 @@ __device__ __forceinline__ void skew_steady_and_drain(Levels<T, IO::W>& st, RowR
   }
 }
 
-template <int T, class IO, bool SKEW>
+// SPLIT = true: phase 1 of the split schedule.  Segments tile the input rows
+// [row_lo - T, row_hi + T) without overlap; each wave computes the
+// trapezoid its own rows determine (level L on [in0 + L, in1 - L)), stores
+// the level-T rows [in0 + T, in1 - T) and saves, per level, the two rows
+// next to each boundary for phase 2 (life_split_down_kernel).
+template <int T, class IO, bool SKEW, bool SPLIT = false>
 __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
   constexpr int kWaveOut = 64 * W - 2;  // words produced per wave
   const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // readfirstlane: the wave index is uniform, so everything derived from it
+  // (segment bounds, loop trip counts) lives in SGPRs with scalar branches.
+  const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (gw >= p.ncolw * p.nseg) return;  // wave-uniform
   const int kcol = gw / p.nseg;
   const int seg = gw - kcol * p.nseg;
   // Balanced segments: the first `seg_rem` segments get one extra row.
-  const int64_t o0 = p.row_lo + int64_t(seg) * p.seg_rows + min(seg, p.seg_rem);
-  const int64_t o1 = o0 + p.seg_rows + (seg < p.seg_rem ? 1 : 0);
-  if (o0 >= o1) return;  // wave-uniform
+  const int64_t base = SPLIT ? p.row_lo - T : p.row_lo;
+  const int64_t s0 = base + int64_t(seg) * p.seg_rows + min(seg, p.seg_rem);
+  const int64_t s1 = s0 + p.seg_rows + (seg < p.seg_rem ? 1 : 0);
+  const int64_t o0 = SPLIT ? s0 + T : s0;  // level-T output rows [o0, o1)
+  const int64_t o1 = SPLIT ? s1 - T : s1;
+  if (!SPLIT && o0 >= o1) return;  // wave-uniform
 
   // Lane words: col .. col+W-1 (padded word index); the wave's first and
   // last words are halo words.
@@ -426,7 +491,21 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
   wr.col = col;
 
   // Prologue: 2T steps, no stores.
-  prologue_tri<T, IO, 0>(st, rd);
+  StateSaver<T, W> saver;
+  BottomSaver<T, W> bottom;
+  bottom.any = SPLIT && seg < p.nseg - 1;
+  bottom.kend = kend;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const int c = min(max(col + i, 0), p.Wp - 1);
+    uint32_t* dummy = SPLIT ? state_base<T>(p, p.nseg - 1, 0, c) : nullptr;
+    saver.base[i] = SPLIT && seg > 0 && wr.own[i] ? state_base<T>(p, seg - 1, 1, c) : dummy;
+    bottom.base[i] = bottom.any && wr.own[i] ? state_base<T>(p, seg, 0, c) : dummy;
+  }
+  if constexpr (SPLIT)
+    prologue_tri<T, IO, 0>(st, rd, saver, bottom);
+  else
+    prologue_tri<T, IO, 0>(st, rd, NoSave{}, NoBottom{});
 
   if constexpr (SKEW && T > 1) {
     // Requires o1 - o0 >= T (guaranteed by plan()).
@@ -437,12 +516,19 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
     constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
     for (; k + 3 <= kend; k += 3) {
       wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
+      if constexpr (SPLIT) bottom.template at<S0>(st, k);
       wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
+      if constexpr (SPLIT) bottom.template at<S1>(st, k + 1);
       wr.row(k + 2 - T, levels_full<T, IO, S2, 0, T>(st, rd.template take<S2>(k + 2)));
+      if constexpr (SPLIT) bottom.template at<S2>(st, k + 2);
     }
     if (k < kend) {
       wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
-      if (k + 1 < kend) wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
+      if constexpr (SPLIT) bottom.template at<S0>(st, k);
+      if (k + 1 < kend) {
+        wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
+        if constexpr (SPLIT) bottom.template at<S1>(st, k + 1);
+      }
     }
   }
 
@@ -462,6 +548,138 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
 }
 
 
+// Phase 2 of the split schedule: the inverted triangle at the boundary b
+// between segments bnd and bnd+1.  Level L+1 (L = 0..T-1) is computed on rows
+// [b-L-1, b+L+1) from level L rows [b-L-2, b+L+2): the inner 2L rows were
+// computed here one level earlier, the two outer rows on each side are
+// phase 1's saved states (level 0: the input rows).  Evaluated level by
+// level with every row of a level in registers, so all rows of a level are
+// independent (the streaming order of phase 1 would chain the levels).
+// Every level-row is computed exactly once over both phases, so the
+// per-generation flags stay exact.
+template <int N, int W>
+struct Rows {
+  Vec<W> r[N];
+};
+
+template <int T, class IO>
+struct DownCtx {
+  static constexpr int W = IO::W;
+  const LifeBlockParams* p;
+  int64_t b;
+  bool ok[W];
+  int off[W];
+  const uint32_t* sbase[2][W];
+  uint32_t fmask[W];
+  __device__ __forceinline__ Vec<W> input(int64_t row) const {
+    return IO::convert(IO::load_raw(p->in + row * p->pitch, off), ok);
+  }
+  __device__ __forceinline__ Vec<W> state(int side, int L, int j) const {
+    Vec<W> v;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      const uint32_t x = sbase[side][i][2 * (L - 1) + j];  // clamped address: always valid
+      v.w[i] = ok[i] ? x : 0u;
+    }
+    return v;
+  }
+};
+
+template <int T, class IO, int L>
+__device__ __forceinline__ void down_level(const DownCtx<T, IO>& ctx, const Writer<IO>& wr,
+                                           const Rows<2 * L + 4, IO::W>& cur, Vec<IO::W> (&acc)[T]) {
+  constexpr int W = IO::W;
+  constexpr int N = 2 * L + 4;  // level L rows [b-L-2, b+L+2)
+  // Next level's boundary states, loaded before this level's arithmetic.
+  Vec<W> sb0, sb1, st0, st1;
+  if constexpr (L + 1 < T) {
+    sb0 = ctx.state(0, L + 1, 0);
+    sb1 = ctx.state(0, L + 1, 1);
+    st0 = ctx.state(1, L + 1, 0);
+    st1 = ctx.state(1, L + 1, 1);
+  }
+  Rows<N, W> h0, h1;
+#pragma unroll
+  for (int r = 0; r < N; ++r) hsum<IO::XL>(cur.r[r], h0.r[r], h1.r[r]);
+  Rows<N + 2, W> nxt;  // level L+1 rows [b-L-3, b+L+3); inner N-2 computed
+#pragma unroll
+  for (int q = 0; q < N - 2; ++q) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      const uint32_t ctr = cur.r[q + 1].w[i];
+      const uint32_t v = rule(h0.r[q].w[i], h1.r[q].w[i], h0.r[q + 1].w[i], h1.r[q + 1].w[i], h0.r[q + 2].w[i],
+                              h1.r[q + 2].w[i], ctr);
+      acc[L].w[i] = bop3<tt::OR_XOR>(acc[L].w[i], v, ctr);
+      nxt.r[q + 2].w[i] = v;
+    }
+  }
+  if constexpr (L + 1 == T) {
+#pragma unroll
+    for (int q = 0; q < N - 2; ++q) wr.row(ctx.b - T + q, nxt.r[q + 2]);
+  } else {
+    nxt.r[0] = sb0;  // level L+1 row b-L-3
+    nxt.r[1] = sb1;  //                 b-L-2
+    nxt.r[N] = st0;  //                 b+L+1
+    nxt.r[N + 1] = st1;  //             b+L+2
+    down_level<T, IO, L + 1>(ctx, wr, nxt, acc);
+  }
+}
+
+template <int T, class IO>
+__global__ __launch_bounds__(256) void life_split_down_kernel(const LifeBlockParams p) {
+  constexpr int W = IO::W;
+  constexpr int kWaveOut = 64 * W - 2;
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nb = p.nseg - 1;
+  if (gw >= p.ncolw * nb) return;  // wave-uniform
+  const int kcol = gw / nb;
+  const int bnd = gw - kcol * nb;
+
+  DownCtx<T, IO> ctx;
+  ctx.p = &p;
+  ctx.b = (p.row_lo - T) + int64_t(bnd + 1) * p.seg_rows + min(bnd + 1, p.seg_rem);
+  const int col = kcol * kWaveOut - 1 + W * lane;
+  Writer<IO> wr;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const int c = col + i;
+    const bool ok = c >= 0 && c < p.Wp;
+    const bool halo = (lane == 0 && i == 0) || (lane == 63 && i == W - 1);
+    ctx.ok[i] = ok;
+    ctx.off[i] = min(max(c, 0), p.Wp - 1);
+    ctx.sbase[0][i] = state_base<T>(p, bnd, 0, ctx.off[i]);
+    ctx.sbase[1][i] = state_base<T>(p, bnd, 1, ctx.off[i]);
+    wr.own[i] = ok && !halo;
+    ctx.fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
+  }
+  wr.out = p.out;
+  wr.pitch = p.pitch;
+  wr.col = col;
+
+  Vec<W> acc[T];
+#pragma unroll
+  for (int L = 0; L < T; ++L)
+#pragma unroll
+    for (int i = 0; i < W; ++i) acc[L].w[i] = 0u;
+  Rows<4, W> lvl0;  // input rows [b-2, b+2)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) lvl0.r[r] = ctx.input(ctx.b - 2 + r);
+  down_level<T, IO, 0>(ctx, wr, lvl0, acc);
+
+  if (p.changed) {
+    uint32_t mask = 0;
+#pragma unroll
+    for (int L = 0; L < T; ++L) {
+      uint32_t any = 0;
+#pragma unroll
+      for (int i = 0; i < W; ++i) any |= acc[L].w[i] & ctx.fmask[i];
+      mask |= (__ballot(any != 0u) != 0ull ? 1u : 0u) << L;
+    }
+    if (lane < T && ((mask >> lane) & 1u)) p.changed[lane] = 1u;
+  }
+}
+
 // Segment planning.  A wave owns a column strip and a balanced segment of
 // output rows.  Its 2T-row prologue is redundant work (about T/2 rows' worth
 // of level bodies), so segments want to be long; the launch wants every SIMD
@@ -474,7 +692,8 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
 // prefers 1020 or 2040 waves there.)
 // Returns whether the skewed schedule applies (every segment >= T rows).
 inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int simds, int occ, int min_seg,
-                 int target_waves) {
+                 int target_waves, double overhead_rows = -1) {
+  if (overhead_rows < 0) overhead_rows = 0.5 * T + 2;
   const int64_t smin = std::max<int64_t>({int64_t(min_seg), 2 * int64_t(T), 1});
   const int64_t max_nseg = std::max<int64_t>(1, out_rows / smin);
   int64_t best_n = 1;
@@ -489,7 +708,7 @@ inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int simds, int occ
       const int64_t rounds = ceil_div(k, int64_t(occ));
       const int64_t kk = std::min<int64_t>(k, occ);
       const double seg = double(ceil_div(out_rows, n));
-      const double cost = double(rounds) * (seg + 0.5 * T + 2) * double(kk) * kT[std::min<int64_t>(kk, 4)];
+      const double cost = double(rounds) * (seg + overhead_rows) * double(kk) * kT[std::min<int64_t>(kk, 4)];
       if (cost < best * 0.999) {
         best = cost;
         best_n = n;
@@ -503,26 +722,56 @@ inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int simds, int occ
 }
 
 // Resident waves per SIMD (one 4-wave workgroup spreads over a CU's 4 SIMDs).
-template <int T, class IO, bool SKEW>
+template <class K>
+int occupancy_of(K kernel) {
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kernel, 256, 0) != hipSuccess || blocks <= 0)
+    blocks = 1;
+  return blocks;
+}
+
+template <int T, class IO, bool SKEW, bool SPLIT>
 int waves_per_simd() {
-  static int cached = 0;
-  if (!cached) {
-    int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, life_block_kernel<T, IO, SKEW>, 256, 0) !=
-            hipSuccess ||
-        blocks <= 0)
-      blocks = 1;
-    cached = blocks;
-  }
+  static const int cached = occupancy_of(life_block_kernel<T, IO, SKEW, SPLIT>);
   return cached;
 }
+
+// Split schedule pays off when the classic schedule's redundant boundary
+// triangles (about T^2 level-rows per segment boundary) are a large share of
+// a segment's S*T level-rows.
+constexpr int kSplitMaxRowsPerT = 8;
 
 template <int T, class IO>
 void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
   p.ncolw = int(ceil_div(p.Wp, 64 * IO::W - 2));
-  const int occ = tune.skew ? waves_per_simd<T, IO, true>() : waves_per_simd<T, IO, false>();
-  const bool skew =
-      plan(p, T, out_rows, 4 * std::max(1, tune.cus), occ, tune.min_seg_rows, tune.target_waves) && tune.skew;
+  const int simds = 4 * std::max(1, tune.cus);
+  if constexpr (T >= 4) {
+    bool split = tune.split > 0;
+    if (tune.split < 0 && !tune.skew) {
+      LifeBlockParams q = p;
+      plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves);
+      split = q.seg_rows < kSplitMaxRowsPerT * T;
+    }
+    if (split && tune.scratch) {
+      const int64_t in_rows = out_rows + 2 * int64_t(T);
+      // Segments of >= 2T + 2 input rows: the last two steps (bottom state)
+      // then fall in the steady loop, never in the prologue.
+      plan(p, T, in_rows, simds, waves_per_simd<T, IO, false, true>(), std::max(tune.min_seg_rows, 2 * T + 2),
+           tune.target_waves, 0.0);
+      p.state_pitch = p.Wp;  // words per (boundary, side); 2(T-1) states each
+      const int64_t nb = p.nseg - 1;
+      // nb boundaries + 1 dummy slot, 2 sides, 2(T-1) states per word
+      p.state = static_cast<uint32_t*>(tune.scratch(size_t((nb + 1) * 2 * p.state_pitch * 2 * (T - 1) * 4)));
+      hipLaunchKernelGGL((life_block_kernel<T, IO, false, true>), dim3(unsigned(ceil_div(p.ncolw * p.nseg, 4))),
+                         dim3(256), 0, s, p);
+      if (nb > 0)
+        hipLaunchKernelGGL((life_split_down_kernel<T, IO>), dim3(unsigned(ceil_div(int64_t(p.ncolw) * nb, int64_t(4)))),
+                           dim3(256), 0, s, p);
+      return;
+    }
+  }
+  const int occ = tune.skew ? waves_per_simd<T, IO, true, false>() : waves_per_simd<T, IO, false, false>();
+  const bool skew = plan(p, T, out_rows, simds, occ, tune.min_seg_rows, tune.target_waves) && tune.skew;
   const int waves = p.ncolw * p.nseg;
   const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
   if (skew)

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <string>
 
 #include "gol/tile.hpp"
@@ -23,6 +24,11 @@ struct LifeBlockParams {
   int own_w0, own_w1;
   uint32_t last_mask;
   uint32_t* changed;  // changed[L] <-> generation gen_base + 1 + L
+  // Split schedule (life_block_impl.hpp): segments tile the INPUT rows
+  // [row_lo - T, row_hi + T); boundary level states go to `state`
+  // (rows of state_pitch 32-bit words).
+  uint32_t* state;
+  int64_t state_pitch;
 };
 
 // Cross-lane primitive that moves the edge words between lanes.
@@ -37,6 +43,9 @@ struct LifeTuning {
   int xlane = kXlaneDpp;    // cross-lane primitive
   bool u8_lds = false;      // byte layout: single-step LDS-tiled kernel (T = 1)
   int lds_rows = 32;        // rows per LDS tile (32 or 64)
+  int split = -1;           // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
+  // Device scratch of at least n bytes, valid until the next call (stream-ordered).
+  std::function<void*(size_t)> scratch;
 };
 
 void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream);

@@ -56,12 +56,23 @@ class HipBackend final : public Backend {
     tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneDpp);
     if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
     tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
+    tune_.split = env_int("GOL_SPLIT", -1);
+    tune_.scratch = [this](size_t n) -> void* {
+      if (n > scratch_bytes_) {
+        HIP_CHECK(hipStreamSynchronize(stream_));  // earlier kernels may still use it
+        if (scratch_) HIP_CHECK(hipFree(scratch_));
+        HIP_CHECK(hipMalloc(&scratch_, n));
+        scratch_bytes_ = n;
+      }
+      return scratch_;
+    };
   }
   ~HipBackend() override {
     hipSetDevice(dev_);
     if (stream_) hipStreamSynchronize(stream_);
     if (comm_) hipStreamSynchronize(comm_);
     if (stage_) hipFree(stage_);
+    if (scratch_) hipFree(scratch_);
     for (auto& e : marks_)
       if (e) hipEventDestroy(e);
     if (comm_) hipStreamDestroy(comm_);
@@ -227,6 +238,8 @@ class HipBackend final : public Backend {
   int cus_ = 256;
   hipk::LifeTuning tune_;
   hipStream_t comm_ = nullptr;
+  void* scratch_ = nullptr;  // split-schedule boundary states
+  size_t scratch_bytes_ = 0;
   std::array<hipEvent_t, 16> marks_{};
   size_t mark_next_ = 0;
   void* stage_ = nullptr;

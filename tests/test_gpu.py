@@ -105,6 +105,46 @@ def test_u8_lds_termination(gpu, monkeypatch, W, H, seed, density):
     assert (out == ref).all()
 
 
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+@pytest.mark.parametrize("tmax", [4, 8, 16])
+@pytest.mark.parametrize("W,H", [(4000 - 4000 % 32, 1500), (2048, 333), (96, 100)])
+def test_split_schedule_vs_torch(gpu, monkeypatch, layout, tmax, W, H):
+    """Split schedule (trapezoid per segment + inverted triangle per boundary,
+    boundary states through memory) forced on, many short segments."""
+    monkeypatch.setenv("GOL_SPLIT", "1")
+    monkeypatch.setenv("GOL_MIN_SEG_ROWS", "1")
+    g = random_grid(W, H, 3 * tmax + W)
+    gens = 3 * tmax + 2
+    want = life_step_torch(g, gens, device="cuda")
+    got = life_step(g, gens, engine="hip", layout=layout, tmax=tmax)
+    assert (got == want).all()
+
+
+@pytest.mark.parametrize("W,H,seed,density", CONVERGING)
+def test_split_schedule_termination(gpu, monkeypatch, W, H, seed, density):
+    monkeypatch.setenv("GOL_SPLIT", "1")
+    monkeypatch.setenv("GOL_MIN_SEG_ROWS", "1")
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    for tmax in (4, 8):
+        out, rep = simulate(g, 1000, engine="hip", tmax=tmax)
+        assert rep.generations == rgens
+        assert (out == ref).all()
+
+
+def test_split_schedule_tall_grid_flags(gpu, monkeypatch):
+    """Many boundaries per launch; the changed flags of both phases must OR
+    to the exact per-generation result (compare a run that stops early)."""
+    monkeypatch.setenv("GOL_SPLIT", "1")
+    g = np.zeros((4096, 512), dtype=np.uint8)
+    g[2000:2002, 100:102] = 1  # a block: still life from generation 1
+    g[3000, 200:203] = 1       # a blinker: period 2, never similar at F=3 ... until it is
+    out, rep = simulate(g, 1000, engine="hip", tmax=16)
+    ref, rgens, _ = reference_run(g)
+    assert rep.generations == rgens
+    assert (out == ref).all()
+
+
 def test_hip_matches_cpu_backend_long_run(gpu):
     g = random_grid(1024, 512, 5)
     a = life_step(g, 300, engine="hip")
