@@ -302,24 +302,30 @@ struct NoBottom {
 
 // Boundary level states of the split schedule.  side 0 = bottom of the
 // segment above boundary bnd (level L rows b-L-2, b-L-1 as j = 0, 1), side 1
-// = top of the segment below (rows b+L, b+L+1).  Layout is column-major:
-// the 2(T-1) states of one word are contiguous, so a lane addresses all of
-// them from one base pointer with immediate offsets (per-state row pointers
-// would each need their own 64-bit address registers).
+// = top of the segment below (rows b+L, b+L+1).  Row-major: one state row
+// holds the words of every column, so a wave's store / load of a state is
+// 256 contiguous bytes (a column-major layout made each of them touch 64
+// cache lines and was HBM-bound).
 template <int T>
-__device__ __forceinline__ uint32_t* state_base(const LifeBlockParams& p, int bnd, int side, int c) {
-  return p.state + ((int64_t(bnd) * 2 + side) * p.state_pitch + c) * (2 * (T - 1));
+__device__ __forceinline__ uint32_t* state_row(const LifeBlockParams& p, int bnd, int side, int L, int j) {
+  return p.state + ((((int64_t(bnd) * 2 + side) * (T - 1) + (L - 1)) * 2 + j) * p.state_pitch);
 }
 
 // Lanes without a real target (no boundary, wave-halo or out-of-tile words)
-// store into a dummy slot (boundary index nseg - 1) instead of branching:
-// divergent branches in the unrolled prologue cost ~160 extra VGPRs.
+// store into a dummy boundary slot (index nseg - 1) instead of branching.
 template <int T, int W>
 struct StateSaver {
-  uint32_t* base[W];
+  const LifeBlockParams* p;
+  int bnd;      // wave-uniform boundary index (dummy slot when none)
+  int off[W];   // word column (own words) or the same column of the dummy slot
+  int dummy_bnd;
+  bool real[W];
   __device__ __forceinline__ void operator()(int L, int j, const Vec<W>& v) const {
 #pragma unroll
-    for (int i = 0; i < W; ++i) base[i][2 * (L - 1) + j] = v.w[i];
+    for (int i = 0; i < W; ++i) {
+      uint32_t* r = state_row<T>(*p, real[i] ? bnd : dummy_bnd, 1, L, j);
+      r[off[i]] = v.w[i];
+    }
   }
 };
 
@@ -327,17 +333,22 @@ struct StateSaver {
 // level L row s1-2-L (s1-1-L) for every level; saved as j = 0 (1).
 template <int T, int W>
 struct BottomSaver {
-  uint32_t* base[W];
-  bool any;  // wave-uniform: this segment has a boundary below
+  const LifeBlockParams* p;
+  int bnd;  // wave-uniform; < 0: none
+  int off[W];
+  bool own[W];
   int kend;
   template <int S, class St>
   __device__ __forceinline__ void at(const St& st, int k) const {
-    if (!any || k < kend - 2) return;  // wave-uniform
+    if (bnd < 0 || k < kend - 2) return;  // wave-uniform
     const int j = k - (kend - 2);
 #pragma unroll
-    for (int L = 1; L < T; ++L)
+    for (int L = 1; L < T; ++L) {
+      uint32_t* r = state_row<T>(*p, bnd, 0, L, j);
 #pragma unroll
-      for (int i = 0; i < W; ++i) base[i][2 * (L - 1) + j] = st.cc[L][S].w[i];
+      for (int i = 0; i < W; ++i)
+        if (own[i]) r[off[i]] = st.cc[L][S].w[i];
+    }
   }
 };
 
@@ -493,14 +504,16 @@ __global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p
   // Prologue: 2T steps, no stores.
   StateSaver<T, W> saver;
   BottomSaver<T, W> bottom;
-  bottom.any = SPLIT && seg < p.nseg - 1;
+  saver.p = bottom.p = &p;
+  saver.bnd = seg - 1;
+  saver.dummy_bnd = p.nseg - 1;
+  bottom.bnd = SPLIT && seg < p.nseg - 1 ? seg : -1;
   bottom.kend = kend;
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    const int c = min(max(col + i, 0), p.Wp - 1);
-    uint32_t* dummy = SPLIT ? state_base<T>(p, p.nseg - 1, 0, c) : nullptr;
-    saver.base[i] = SPLIT && seg > 0 && wr.own[i] ? state_base<T>(p, seg - 1, 1, c) : dummy;
-    bottom.base[i] = bottom.any && wr.own[i] ? state_base<T>(p, seg, 0, c) : dummy;
+    saver.off[i] = bottom.off[i] = min(max(col + i, 0), p.Wp - 1);
+    saver.real[i] = seg > 0 && wr.own[i];
+    bottom.own[i] = wr.own[i];
   }
   if constexpr (SPLIT)
     prologue_tri<T, IO, 0>(st, rd, saver, bottom);
@@ -569,7 +582,7 @@ struct DownCtx {
   int64_t b;
   bool ok[W];
   int off[W];
-  const uint32_t* sbase[2][W];
+  int bnd;
   uint32_t fmask[W];
   __device__ __forceinline__ Vec<W> input(int64_t row) const {
     return IO::convert(IO::load_raw(p->in + row * p->pitch, off), ok);
@@ -578,7 +591,7 @@ struct DownCtx {
     Vec<W> v;
 #pragma unroll
     for (int i = 0; i < W; ++i) {
-      const uint32_t x = sbase[side][i][2 * (L - 1) + j];  // clamped address: always valid
+      const uint32_t x = state_row<T>(*p, bnd, side, L, j)[off[i]];  // clamped column: always valid
       v.w[i] = ok[i] ? x : 0u;
     }
     return v;
@@ -638,6 +651,7 @@ __global__ __launch_bounds__(256) void life_split_down_kernel(const LifeBlockPar
 
   DownCtx<T, IO> ctx;
   ctx.p = &p;
+  ctx.bnd = bnd;
   ctx.b = (p.row_lo - T) + int64_t(bnd + 1) * p.seg_rows + min(bnd + 1, p.seg_rem);
   const int col = kcol * kWaveOut - 1 + W * lane;
   Writer<IO> wr;
@@ -648,8 +662,6 @@ __global__ __launch_bounds__(256) void life_split_down_kernel(const LifeBlockPar
     const bool halo = (lane == 0 && i == 0) || (lane == 63 && i == W - 1);
     ctx.ok[i] = ok;
     ctx.off[i] = min(max(c, 0), p.Wp - 1);
-    ctx.sbase[0][i] = state_base<T>(p, bnd, 0, ctx.off[i]);
-    ctx.sbase[1][i] = state_base<T>(p, bnd, 1, ctx.off[i]);
     wr.own[i] = ok && !halo;
     ctx.fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
   }
@@ -758,10 +770,10 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       // then fall in the steady loop, never in the prologue.
       plan(p, T, in_rows, simds, waves_per_simd<T, IO, false, true>(), std::max(tune.min_seg_rows, 2 * T + 2),
            tune.target_waves, 0.0);
-      p.state_pitch = p.Wp;  // words per (boundary, side); 2(T-1) states each
+      p.state_pitch = round_up(int64_t(p.Wp), int64_t(64));  // words per state row
       const int64_t nb = p.nseg - 1;
-      // nb boundaries + 1 dummy slot, 2 sides, 2(T-1) states per word
-      p.state = static_cast<uint32_t*>(tune.scratch(size_t((nb + 1) * 2 * p.state_pitch * 2 * (T - 1) * 4)));
+      // nb boundaries + 1 dummy slot, 2 sides, T-1 levels, 2 rows
+      p.state = static_cast<uint32_t*>(tune.scratch(size_t((nb + 1) * 2 * (T - 1) * 2 * p.state_pitch * 4)));
       hipLaunchKernelGGL((life_block_kernel<T, IO, false, true>), dim3(unsigned(ceil_div(p.ncolw * p.nseg, 4))),
                          dim3(256), 0, s, p);
       if (nb > 0)

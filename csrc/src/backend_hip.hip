@@ -27,10 +27,13 @@
 namespace gol {
 namespace {
 
+// Integer from the environment (any value, including 0 and negatives);
+// unset, empty or unparsable -> dflt.
 int env_int(const char* name, int dflt) {
   if (const char* s = std::getenv(name)) {
-    int v = std::atoi(s);
-    if (v > 0) return v;
+    char* end = nullptr;
+    const long v = std::strtol(s, &end, 10);
+    if (end != s && *end == '\0') return int(v);
   }
   return dflt;
 }

@@ -137,8 +137,9 @@ def test_split_schedule_tall_grid_flags(gpu, monkeypatch):
     to the exact per-generation result (compare a run that stops early)."""
     monkeypatch.setenv("GOL_SPLIT", "1")
     g = np.zeros((4096, 512), dtype=np.uint8)
-    g[2000:2002, 100:102] = 1  # a block: still life from generation 1
-    g[3000, 200:203] = 1       # a blinker: period 2, never similar at F=3 ... until it is
+    g[2000:2002, 100:102] = 1  # a block (still life)
+    W, H, seed, density = CONVERGING[5]
+    g[1990:1990 + H, 300:300 + W] = random_grid(W, H, seed, density)  # settles after a while
     out, rep = simulate(g, 1000, engine="hip", tmax=16)
     ref, rgens, _ = reference_run(g)
     assert rep.generations == rgens
