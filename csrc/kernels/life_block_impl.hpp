@@ -41,6 +41,10 @@
 #include "gol/tile.hpp"
 #include "life_kernels.hpp"
 
+#ifndef GOL_T16_WAVES
+#define GOL_T16_WAVES 3
+#endif
+
 
 namespace gol {
 namespace hipk {
@@ -442,8 +446,17 @@ __device__ __forceinline__ void skew_steady_and_drain(Levels<T, IO::W>& st, RowR
 // trapezoid its own rows determine (level L on [in0 + L, in1 - L)), stores
 // the level-T rows [in0 + T, in1 - T) and saves, per level, the two rows
 // next to each boundary for phase 2 (life_split_down_kernel).
+// Occupancy target: T = 16 needs ~171 VGPRs unconstrained; asking for three
+// waves per SIMD (<= 168) costs a few extra moves but 1.5x the resident
+// waves for latency hiding.
+template <int T, class IO, bool SKEW, bool SPLIT>
+constexpr int min_waves_per_eu() {
+  return (T == 16 && IO::W == 1 && !SKEW) ? GOL_T16_WAVES : 1;
+}
+
 template <int T, class IO, bool SKEW, bool SPLIT = false>
-__global__ __launch_bounds__(256) void life_block_kernel(const LifeBlockParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<T, IO, SKEW, SPLIT>())))
+void life_block_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
   constexpr int kWaveOut = 64 * W - 2;  // words produced per wave
   const int lane = threadIdx.x & 63;
@@ -598,48 +611,54 @@ struct DownCtx {
   }
 };
 
+// sv[L][0..3]: level L rows b-L-2, b-L-1 (side 0) and b+L, b+L+1 (side 1),
+// all loaded up front: the early levels are a handful of rows each, so
+// loading per level would expose one memory latency per level.
 template <int T, class IO, int L>
 __device__ __forceinline__ void down_level(const DownCtx<T, IO>& ctx, const Writer<IO>& wr,
-                                           const Rows<2 * L + 4, IO::W>& cur, Vec<IO::W> (&acc)[T]) {
+                                           const Rows<2 * L + 4, IO::W>& cur, Vec<IO::W> (&acc)[T],
+                                           const Vec<IO::W> (&sv)[T][4]) {
   constexpr int W = IO::W;
   constexpr int N = 2 * L + 4;  // level L rows [b-L-2, b+L+2)
-  // Next level's boundary states, loaded before this level's arithmetic.
-  Vec<W> sb0, sb1, st0, st1;
-  if constexpr (L + 1 < T) {
-    sb0 = ctx.state(0, L + 1, 0);
-    sb1 = ctx.state(0, L + 1, 1);
-    st0 = ctx.state(1, L + 1, 0);
-    st1 = ctx.state(1, L + 1, 1);
-  }
-  Rows<N, W> h0, h1;
-#pragma unroll
-  for (int r = 0; r < N; ++r) hsum<IO::XL>(cur.r[r], h0.r[r], h1.r[r]);
+  // Rows are swept in order with a 3-row window of horizontal sums, so only
+  // the cells of the two levels are live (a full h0/h1 array per level needs
+  // > 256 VGPRs at T = 16).  sched_barrier every 8 rows stops the max-ILP
+  // scheduler from hoisting every row's DPP shifts to the top of the level.
   Rows<N + 2, W> nxt;  // level L+1 rows [b-L-3, b+L+3); inner N-2 computed
+  Vec<W> ha0, ha1, hb0, hb1, hc0, hc1;
+  hsum<IO::XL>(cur.r[0], ha0, ha1);
+  hsum<IO::XL>(cur.r[1], hb0, hb1);
 #pragma unroll
   for (int q = 0; q < N - 2; ++q) {
+    hsum<IO::XL>(cur.r[q + 2], hc0, hc1);
 #pragma unroll
     for (int i = 0; i < W; ++i) {
       const uint32_t ctr = cur.r[q + 1].w[i];
-      const uint32_t v = rule(h0.r[q].w[i], h1.r[q].w[i], h0.r[q + 1].w[i], h1.r[q + 1].w[i], h0.r[q + 2].w[i],
-                              h1.r[q + 2].w[i], ctr);
+      const uint32_t v = rule(ha0.w[i], ha1.w[i], hb0.w[i], hb1.w[i], hc0.w[i], hc1.w[i], ctr);
       acc[L].w[i] = bop3<tt::OR_XOR>(acc[L].w[i], v, ctr);
       nxt.r[q + 2].w[i] = v;
     }
+    ha0 = hb0;
+    ha1 = hb1;
+    hb0 = hc0;
+    hb1 = hc1;
+    if (q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (L + 1 == T) {
 #pragma unroll
     for (int q = 0; q < N - 2; ++q) wr.row(ctx.b - T + q, nxt.r[q + 2]);
   } else {
-    nxt.r[0] = sb0;  // level L+1 row b-L-3
-    nxt.r[1] = sb1;  //                 b-L-2
-    nxt.r[N] = st0;  //                 b+L+1
-    nxt.r[N + 1] = st1;  //             b+L+2
-    down_level<T, IO, L + 1>(ctx, wr, nxt, acc);
+    nxt.r[0] = sv[L + 1][0];      // level L+1 row b-L-3
+    nxt.r[1] = sv[L + 1][1];      //                 b-L-2
+    nxt.r[N] = sv[L + 1][2];      //                 b+L+1
+    nxt.r[N + 1] = sv[L + 1][3];  //                 b+L+2
+    down_level<T, IO, L + 1>(ctx, wr, nxt, acc, sv);
   }
 }
 
 template <int T, class IO>
-__global__ __launch_bounds__(256) void life_split_down_kernel(const LifeBlockParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void life_split_down_kernel(
+    const LifeBlockParams p) {
   constexpr int W = IO::W;
   constexpr int kWaveOut = 64 * W - 2;
   const int lane = threadIdx.x & 63;
@@ -677,7 +696,15 @@ __global__ __launch_bounds__(256) void life_split_down_kernel(const LifeBlockPar
   Rows<4, W> lvl0;  // input rows [b-2, b+2)
 #pragma unroll
   for (int r = 0; r < 4; ++r) lvl0.r[r] = ctx.input(ctx.b - 2 + r);
-  down_level<T, IO, 0>(ctx, wr, lvl0, acc);
+  Vec<W> sv[T][4];
+#pragma unroll
+  for (int L = 1; L < T; ++L) {
+    sv[L][0] = ctx.state(0, L, 0);
+    sv[L][1] = ctx.state(0, L, 1);
+    sv[L][2] = ctx.state(1, L, 0);
+    sv[L][3] = ctx.state(1, L, 1);
+  }
+  down_level<T, IO, 0>(ctx, wr, lvl0, acc, sv);
 
   if (p.changed) {
     uint32_t mask = 0;

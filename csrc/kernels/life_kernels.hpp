@@ -43,7 +43,7 @@ struct LifeTuning {
   int xlane = kXlaneDpp;    // cross-lane primitive
   bool u8_lds = false;      // byte layout: single-step LDS-tiled kernel (T = 1)
   int lds_rows = 32;        // rows per LDS tile (32 or 64)
-  int split = -1;           // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
+  int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).
   std::function<void*(size_t)> scratch;
 };

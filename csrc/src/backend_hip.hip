@@ -59,7 +59,7 @@ class HipBackend final : public Backend {
     tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneDpp);
     if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
     tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
-    tune_.split = env_int("GOL_SPLIT", -1);
+    tune_.split = env_int("GOL_SPLIT", 0);  // measured slower so far (profiles/)
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
         HIP_CHECK(hipStreamSynchronize(stream_));  // earlier kernels may still use it
