@@ -55,6 +55,7 @@ def main() -> int:
     ap.add_argument("--epoch", type=int, default=0)
     ap.add_argument("--poll", type=int, default=0)
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--repeats", type=int, default=1, help="timed repetitions (best is reported)")
     a = ap.parse_args()
@@ -86,7 +87,7 @@ def main() -> int:
     Hg = a.height or S
     total = a.warmup + a.steps * a.repeats
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
-                     poll_gens=a.poll, overlap=a.overlap)
+                     poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs)
     sim = Simulation(cfg, transport=transport, backend=backend)
     eng = sim.native_engine
     sim.init_random(a.seed, 0.5)
@@ -147,6 +148,7 @@ def main() -> int:
                 "polls": r.polls,
                 "kernel_launches": r.kernel_launches,
                 "overlapped_halo_exchange": r.overlapped,
+                "graph_epochs": r.graph_launches,
                 "baseline": "8.9e8 cell-updates/s (best reference run in BASELINE.md: MPI, 4 ranks, 2048^2, CPU)",
             },
         }

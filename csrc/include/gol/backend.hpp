@@ -44,6 +44,20 @@ class Backend {
   // everything in program order).  stream_mark() records a point on `from`
   // (nullptr = the compute stream) that stream_wait() makes `on` wait for.
   virtual void* comm_stream() { return nullptr; }
+  // Stream capture into replayable graphs (HIP graphs).  capture_end()
+  // returns an executable graph handle; graph_launch() enqueues it.
+  virtual bool supports_graphs() const { return false; }
+  virtual void capture_begin() {}
+  virtual void* capture_end() { return nullptr; }
+  virtual void graph_launch(void* /*graph*/) {}
+  virtual void graph_destroy(void* /*graph*/) {}
+  // Stream-ordered update of a device int64 (set, or add).
+  virtual void i64_async(int64_t* dev, int64_t v, bool add) {
+    if (add)
+      *dev += v;
+    else
+      *dev = v;
+  }
   virtual void* stream_mark(void* /*from*/) { return nullptr; }
   virtual void stream_wait(void* /*on*/, void* /*mark*/) {}
 

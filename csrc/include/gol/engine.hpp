@@ -45,6 +45,10 @@ struct EngineConfig {
   // Check each termination poll one poll window later, so the host never
   // drains the device queue (stops are absorbing, so running past is exact).
   bool lagged_poll = true;
+  // Replay full epochs as captured HIP graphs (one per buffer parity):
+  // -1 auto (single rank on a graph-capable backend), 0 off, 1 whenever the
+  // backend and transport allow it.
+  int graphs = -1;
 };
 
 struct RunResult {
@@ -58,6 +62,7 @@ struct RunResult {
   int64_t polls = 0;             // termination polls performed
   int64_t kernel_launches = 0;
   bool overlapped = false;       // epochs ran with the overlapped halo exchange
+  int64_t graph_launches = 0;    // epochs replayed from a captured HIP graph
 };
 
 class Engine {
@@ -76,6 +81,7 @@ class Engine {
   int epoch_depth() const { return D_; }
   int tmax() const { return tmax_; }
   bool overlap() const { return overlap_; }
+  bool graphs() const { return use_graphs_; }
   int64_t generation() const { return gen_; }
   void set_generation(int64_t g) { gen_ = g; }
   Backend* backend() const { return be_; }
@@ -119,6 +125,8 @@ class Engine {
   void exchange_columns(void* buf);
   // d generations (d <= D_) with the row exchange overlapped (see engine.cpp).
   void epoch_overlapped(int64_t d);
+  void run_epoch(int64_t d);
+  void release_graphs();
 
   EngineConfig cfg_;
   Backend* be_;
@@ -135,6 +143,14 @@ class Engine {
   uint32_t* alive_dev_ = nullptr;
   void* colbuf_[4] = {nullptr, nullptr, nullptr, nullptr};  // send W, send E, recv W, recv E
   bool overlap_ = false;
+  bool use_graphs_ = false, capturing_ = false;
+  int64_t* gen_dev_ = nullptr;        // device: (epoch start - flags_base_) for graph replays
+  int64_t epoch_start_ = 0;
+  void* graph_[2] = {nullptr, nullptr};  // by buffer parity at epoch start
+  int graph_flip_[2] = {0, 0};
+  int64_t graph_kernels_[2] = {0, 0};
+  uint32_t* graph_flags_ = nullptr;   // flags buffer the graphs were captured with
+  int64_t graph_runs_ = 0;
   TileGeom gs_;                     // edge scratch tile: D owned rows + D halo rows each side
   void* edge_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [top|bottom][parity]
   int64_t gen_ = 0;

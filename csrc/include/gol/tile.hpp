@@ -67,6 +67,12 @@ struct BlockArgs {
   int64_t gen_base = 0;
   uint32_t* changed = nullptr;
   int64_t flags_base = 0;
+  // Graph-replayable flag addressing: when gen_dev is set, the flags of
+  // generation gen_base + 1 + L are changed[*gen_dev + gen_rel + L] (device
+  // value read at run time), so a captured epoch can be replayed at any
+  // generation; gen_base / flags_base are then ignored for addressing.
+  const int64_t* gen_dev = nullptr;
+  int64_t gen_rel = 0;
 };
 
 }  // namespace gol

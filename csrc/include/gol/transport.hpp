@@ -51,6 +51,9 @@ class Transport {
   // In-place element-wise MAX over ranks of n uint32 values.
   virtual void allreduce_max_u32(uint32_t* buf, size_t n, void* stream) = 0;
   virtual void barrier() = 0;
+  // exchange()/allreduce enqueue device work only (no host waits), so they
+  // can be captured into a HIP graph.
+  virtual bool capturable() const { return false; }
 };
 
 // Single rank: nothing to exchange with.
@@ -62,6 +65,7 @@ class SelfTransport final : public Transport {
   void exchange(const std::vector<P2POp>& ops, void* stream) override;
   void allreduce_max_u32(uint32_t*, size_t, void*) override {}
   void barrier() override {}
+  bool capturable() const override { return true; }
 };
 
 // Shared state of a group of in-process ranks.

@@ -66,7 +66,13 @@ void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t s
   p.own_w1 = int(ceil_div(g.cell0() + g.W, 32));
   const int64_t tail = (g.cell0() + g.W) % 32;
   p.last_mask = tail ? (0xFFFFFFFFu >> (32 - tail)) : 0xFFFFFFFFu;
-  p.changed = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
+  if (a.gen_dev) {
+    p.changed = a.changed;  // resolved on the device: changed + *gen_dev + gen_rel
+    p.gen_dev = a.changed ? a.gen_dev : nullptr;
+    p.gen_rel = a.gen_rel;
+  } else {
+    p.changed = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
+  }
   const int64_t rows = a.row_hi - a.row_lo;
   const int x = xlane_of(g.layout, w, tune);
   if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {

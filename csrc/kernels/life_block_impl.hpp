@@ -569,7 +569,8 @@ void life_block_kernel(const LifeBlockParams p) {
       for (int i = 0; i < W; ++i) any |= st.acc[L].w[i] & fmask[i];
       mask |= (__ballot(any != 0u) != 0ull ? 1u : 0u) << L;
     }
-    if (lane < T && ((mask >> lane) & 1u)) p.changed[lane] = 1u;
+    uint32_t* ch = p.gen_dev ? p.changed + (*p.gen_dev + p.gen_rel) : p.changed;
+    if (lane < T && ((mask >> lane) & 1u)) ch[lane] = 1u;
   }
 }
 
@@ -715,7 +716,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void l
       for (int i = 0; i < W; ++i) any |= acc[L].w[i] & ctx.fmask[i];
       mask |= (__ballot(any != 0u) != 0ull ? 1u : 0u) << L;
     }
-    if (lane < T && ((mask >> lane) & 1u)) p.changed[lane] = 1u;
+    uint32_t* ch = p.gen_dev ? p.changed + (*p.gen_dev + p.gen_rel) : p.changed;
+    if (lane < T && ((mask >> lane) & 1u)) ch[lane] = 1u;
   }
 }
 

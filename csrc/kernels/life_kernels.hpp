@@ -23,7 +23,9 @@ struct LifeBlockParams {
   int seg_rem;
   int own_w0, own_w1;
   uint32_t last_mask;
-  uint32_t* changed;  // changed[L] <-> generation gen_base + 1 + L
+  uint32_t* changed;  // changed[L] <-> generation gen_base + 1 + L (after resolving gen_dev)
+  const int64_t* gen_dev;  // if set: changed += *gen_dev + gen_rel at run time (graph replay)
+  int64_t gen_rel;
   // Split schedule (life_block_impl.hpp): segments tile the INPUT rows
   // [row_lo - T, row_hi + T); boundary level states go to `state`
   // (rows of state_pitch 32-bit words).
@@ -80,6 +82,7 @@ void launch_load_rows(uint8_t* buf, const TileGeom& g, const uint8_t* stage, int
                       int64_t r0, int64_t n, hipStream_t s);
 void launch_store_rows(const uint8_t* buf, const TileGeom& g, uint8_t* stage, int64_t ld,
                        int64_t r0, int64_t n, bool ascii, hipStream_t s);
+void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s);
 void launch_init_random(uint8_t* buf, const TileGeom& g, uint64_t seed, uint32_t thresh24,
                         int64_t grow0, int64_t gcol0, hipStream_t s);
 

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
                                                             uint8_t* __restrict__ out, int64_t pitch,
                                                             int64_t row_lo, int64_t row_hi, int64_t Wc,
                                                             int64_t own_c0, int64_t own_c1,
-                                                            uint32_t* changed) {
+                                                            uint32_t* changed, const int64_t* gen_dev) {
   constexpr int kLdsRows = kTileH + 2;
   constexpr int kRowsPerThread = kTileH / 4;
   __shared__ __attribute__((aligned(16))) uint8_t tile[kLdsRows * kLdsStride];
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
     }
   }
   // Idempotent plain store (an atomic per wave to one address serialises in L2).
-  if (changed && __ballot(diff != 0u) != 0ull && (tid & 63) == 0) *changed = 1u;
+  if (changed && __ballot(diff != 0u) != 0ull && (tid & 63) == 0) (gen_dev ? changed + *gen_dev : changed)[0] = 1u;
 }
 
 }  // namespace
@@ -170,13 +170,14 @@ void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream) 
               "life_step_lds: row range outside the tile");
   GOL_REQUIRE(g.pitch % 16 == 0, "life_step_lds: pitch must be 16-byte aligned");
   const int64_t rows = a.row_hi - a.row_lo;
-  uint32_t* changed = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
+  uint32_t* changed = a.changed ? a.changed + (a.gen_dev ? a.gen_rel : a.gen_base + 1 - a.flags_base) : nullptr;
+  const int64_t* gen_dev = a.changed ? a.gen_dev : nullptr;
   const int th = lds_rows == 32 ? 32 : 64;
   GOL_REQUIRE(ceil_div(rows, int64_t(th)) < (int64_t(1) << 31), "life_step_lds: too many rows");
   const dim3 grid(unsigned(ceil_div(g.Wc(), int64_t(kTileW))), unsigned(ceil_div(rows, int64_t(th))));
   auto k = th == 32 ? life_step_lds_kernel<32> : life_step_lds_kernel<64>;
   hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
-                     g.pitch, a.row_lo, a.row_hi, g.Wc(), g.cell0(), g.cell0() + g.W, changed);
+                     g.pitch, a.row_lo, a.row_hi, g.Wc(), g.cell0(), g.cell0() + g.W, changed, gen_dev);
 }
 
 }  // namespace hipk

@@ -158,7 +158,13 @@ __global__ void init_random_u8(uint8_t* buf, int64_t pitch, int64_t row0, int64_
   }
 }
 
+__global__ void i64_k(int64_t* p, int64_t v, int add) { *p = add ? *p + v : v; }
+
 }  // namespace
+
+void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s) {
+  hipLaunchKernelGGL(i64_k, dim3(1), dim3(1), 0, s, p, v, add ? 1 : 0);
+}
 
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s) {
   if (g.hw == 0) return;

@@ -137,7 +137,8 @@ void CpuBackend::run_block(const BlockArgs& a) {
     }, 8);
     if (a.changed) {
       bool ch = std::any_of(any.begin(), any.end(), [](uint8_t v) { return v != 0; });
-      if (ch) a.changed[a.gen_base + lev - a.flags_base] = 1u;
+      const int64_t idx = a.gen_dev ? *a.gen_dev + a.gen_rel + (lev - 1) : a.gen_base + lev - a.flags_base;
+      if (ch) a.changed[idx] = 1u;
     }
   }
   const auto& fin = lvl[T & 1];

@@ -142,6 +142,26 @@ class HipBackend final : public Backend {
   }
   void event_wait(void* ev) override { HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(ev))); }
   void event_destroy(void* ev) override { hipEventDestroy(static_cast<hipEvent_t>(ev)); }
+  bool supports_graphs() const override { return tune_.split == 0; }  // split allocates scratch lazily
+  void capture_begin() override {
+    HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+  }
+  void* capture_end() override {
+    hipGraph_t g = nullptr;
+    HIP_CHECK(hipStreamEndCapture(stream_, &g));
+    hipGraphExec_t exec = nullptr;
+    HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(g));
+    return exec;
+  }
+  void graph_launch(void* g) override { HIP_CHECK(hipGraphLaunch(static_cast<hipGraphExec_t>(g), stream_)); }
+  void graph_destroy(void* g) override {
+    if (g) hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
+  }
+  void i64_async(int64_t* dev, int64_t v, bool add) override {
+    hipk::launch_i64(dev, v, add, stream_);
+    HIP_CHECK(hipGetLastError());
+  }
   void* comm_stream() override {
     if (!comm_) HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
     return comm_;

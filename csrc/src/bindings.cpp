@@ -178,7 +178,8 @@ PYBIND11_MODULE(_gol, m) {
       .def_readwrite("epoch", &EngineConfig::epoch)
       .def_readwrite("poll_gens", &EngineConfig::poll_gens)
       .def_readwrite("overlap", &EngineConfig::overlap)
-      .def_readwrite("lagged_poll", &EngineConfig::lagged_poll);
+      .def_readwrite("lagged_poll", &EngineConfig::lagged_poll)
+      .def_readwrite("graphs", &EngineConfig::graphs);
 
   py::class_<RunResult>(m, "RunResult")
       .def_readonly("generations", &RunResult::generations)
@@ -191,6 +192,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_readonly("polls", &RunResult::polls)
       .def_readonly("kernel_launches", &RunResult::kernel_launches)
       .def_readonly("overlapped", &RunResult::overlapped)
+      .def_readonly("graph_launches", &RunResult::graph_launches)
       .def("as_dict", [](const RunResult& r) {
         py::dict d;
         d["generations"] = r.generations;
@@ -203,6 +205,7 @@ PYBIND11_MODULE(_gol, m) {
         d["polls"] = r.polls;
         d["kernel_launches"] = r.kernel_launches;
         d["overlapped"] = r.overlapped;
+        d["graph_launches"] = r.graph_launches;
         return d;
       });
 
@@ -219,6 +222,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("epoch_depth", &Engine::epoch_depth)
       .def_property_readonly("tmax", &Engine::tmax)
       .def("overlap", &Engine::overlap)
+      .def("graphs", &Engine::graphs)
       .def_property("generation", &Engine::generation, &Engine::set_generation)
       .def("current_buffer", [](const Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })
       .def("load_cells",

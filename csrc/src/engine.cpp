@@ -56,10 +56,22 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     for (auto& e : edge_)
       for (auto& b : e) b = be_->alloc(size_t(gs_.bytes()));
   }
+  use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
+                (cfg_.graphs > 0 || tr_->size() == 1);
+  if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
   gen_ = cfg_.start_gen;
 }
 
+void Engine::release_graphs() {
+  for (auto& g : graph_) {
+    if (g) be_->graph_destroy(g);
+    g = nullptr;
+  }
+}
+
 Engine::~Engine() {
+  release_graphs();
+  if (gen_dev_) be_->release(gen_dev_);
   for (auto& b : buf_)
     if (b) be_->release(b);
   for (auto& b : colbuf_)
@@ -228,6 +240,21 @@ void Engine::epoch_overlapped(int64_t d) {
   gen_ += d;
 }
 
+void Engine::run_epoch(int64_t d) {
+  if (overlap_) {
+    epoch_overlapped(d);
+    return;
+  }
+  halo_exchange();
+  int64_t a = 0;
+  while (d > 0) {
+    const int T = pick_T(d);
+    step_block(T, a + T, g_.R() - a - T);
+    a += T;
+    d -= T;
+  }
+}
+
 void Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
                     int64_t gen_base) {
   BlockArgs a;
@@ -238,8 +265,15 @@ void Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_l
   a.row_hi = row_hi;
   a.T = T;
   a.gen_base = gen_base;
-  a.changed =
-      (flags_ && gen_base + T < flags_base_ + flags_len_ && gen_base >= flags_base_) ? flags_ : nullptr;
+  if (capturing_) {
+    // Replayable: the flags offset comes from gen_dev_ at run time.
+    a.changed = flags_;
+    a.gen_dev = gen_dev_;
+    a.gen_rel = gen_base - epoch_start_ + 1;
+  } else {
+    a.changed =
+        (flags_ && gen_base + T < flags_base_ + flags_len_ && gen_base >= flags_base_) ? flags_ : nullptr;
+  }
   a.flags_base = flags_base_;
   be_->run_block(a);
   ++launches_;
@@ -309,6 +343,12 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   }
   flags_base_ = start;
   be_->memset_async(flags_, 0, size_t(flags_len_) * 4);
+  if (use_graphs_) {
+    if (graph_flags_ != flags_) release_graphs();  // kernel arguments point at the flags
+    graph_flags_ = flags_;
+    be_->i64_async(gen_dev_, 0, /*add=*/false);  // first epoch starts at flags_base_
+  }
+  const int64_t g0 = graph_runs_;
   const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_;
   tr_->barrier();
   be_->synchronize();
@@ -320,18 +360,34 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   Poll pending;
   bool have_pending = false;
   while (gen_ < limit) {
-    int64_t d = std::min<int64_t>(D_, limit - gen_);
-    if (overlap_) {
-      epoch_overlapped(d);
-    } else {
-      halo_exchange();
-      int64_t a = 0;
-      while (d > 0) {
-        int T = pick_T(d);
-        step_block(T, a + T, g_.R() - a - T);
-        a += T;
-        d -= T;
+    const int64_t d = std::min<int64_t>(D_, limit - gen_);
+    if (use_graphs_ && d == D_) {
+      // Full epochs replay a captured graph; the only per-epoch input is the
+      // device generation offset, advanced by the graph itself.
+      const int par = cur_;
+      if (!graph_[par]) {
+        const int64_t k0 = launches_;
+        capturing_ = true;
+        epoch_start_ = gen_;
+        be_->capture_begin();
+        run_epoch(d);
+        be_->i64_async(gen_dev_, D_, /*add=*/true);
+        graph_[par] = be_->capture_end();
+        capturing_ = false;
+        graph_flip_[par] = cur_ ^ par;
+        graph_kernels_[par] = launches_ - k0;
+        be_->graph_launch(graph_[par]);  // capture only recorded it
+      } else {
+        be_->graph_launch(graph_[par]);
+        cur_ ^= graph_flip_[par];
+        gen_ += D_;
+        ++exchanges_;
+        launches_ += graph_kernels_[par];
       }
+      ++graph_runs_;
+    } else {
+      if (use_graphs_) be_->i64_async(gen_dev_, d, /*add=*/true);  // keep the offset in step
+      run_epoch(d);
     }
     ++epoch;
     if (stop_early && (epoch % poll_epochs == 0 || gen_ == limit)) {
@@ -360,6 +416,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.polls = polls_ - p0;
   res.kernel_launches = launches_ - l0;
   res.overlapped = overlap_;
+  res.graph_launches = graph_runs_ - g0;
   res.generations = limit;
   if (found >= 0) {
     res.first_unchanged = found;

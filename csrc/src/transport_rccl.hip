@@ -69,6 +69,7 @@ class RcclTransport final : public Transport {
     NCCL_CHECK(ncclAllReduce(barrier_buf_, barrier_buf_, 1, ncclUint32, ncclMax, comm_, barrier_stream_));
     if (hipStreamSynchronize(barrier_stream_) != hipSuccess) fail("RCCL barrier failed");
   }
+  bool capturable() const override { return true; }  // grouped send/recv are stream-ordered
 
  private:
   int rank_, size_, dev_;

@@ -47,7 +47,7 @@ struct Options {
   bool random = false;
   uint64_t seed = 1;
   double density = 0.5;
-  int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0, overlap = -1;
+  int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0, overlap = -1, graphs = -1;
   bool show = false;
 };
 
@@ -67,6 +67,7 @@ struct Options {
                "  --decomp auto|PxQ           process grid (Px columns x Py rows)\n"
                "  --tmax T --epoch D --poll N temporal block, halo depth, poll interval\n"
                "  --overlap auto|on|off       overlap the row halo exchange with the interior\n"
+               "  --graphs auto|on|off        replay full epochs as captured HIP graphs\n"
                "  --threads N                 host threads for the cpu engine\n"
                "  --style serial|mpi|openmp|cuda   stdout format of the matching reference build\n"
                "  --metrics-json PATH         write run metrics as JSON\n"
@@ -103,6 +104,9 @@ Options parse(int argc, char** argv) {
     else if (a == "--overlap") {
       std::string v = next();
       o.overlap = v == "on" ? 1 : v == "off" ? 0 : -1;
+    } else if (a == "--graphs") {
+      std::string v = next();
+      o.graphs = v == "on" ? 1 : v == "off" ? 0 : -1;
     }
     else if (a == "--show") o.show = true;
     else if (a == "--random") {
@@ -193,6 +197,7 @@ int run(const Options& o) {
     cfg.epoch = o.epoch;
     cfg.poll_gens = o.poll;
     cfg.overlap = o.overlap;
+    cfg.graphs = o.graphs;
     int ndev = 1;
     if (engine == "hip") {
       GOL_REQUIRE(hip_available(), "--engine hip: no HIP device available");

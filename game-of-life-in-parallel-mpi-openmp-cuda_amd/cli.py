@@ -38,6 +38,8 @@ def parse_args(argv=None):
     p.add_argument("--poll", type=int, default=0)
     p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                    help="overlap the row halo exchange with interior compute")
+    p.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
+                   help="replay full epochs as captured HIP graphs")
     p.add_argument("--threads", type=int, default=0)
     p.add_argument("--style", default="serial", choices=["serial", "mpi", "openmp", "cuda"])
     p.add_argument("--metrics-json", default=None)
@@ -94,7 +96,7 @@ def main(argv=None) -> int:
 
     cfg = LifeConfig(a.width, a.height, gen_limit=a.gens, check_similarity=not a.no_similarity,
                      sim_freq=a.sim_freq, layout=a.layout, decomp=a.decomp, tmax=a.tmax,
-                     epoch=a.epoch, poll_gens=a.poll, overlap=a.overlap)
+                     epoch=a.epoch, poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs)
     src = a.input_file
     if a.resume:
         from .utils.checkpoint import load_checkpoint  # noqa: PLC0415

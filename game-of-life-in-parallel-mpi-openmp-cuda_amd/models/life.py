@@ -43,6 +43,7 @@ class LifeConfig:
     poll_gens: int = 0          # generations between termination polls (0 = 256)
     overlap: str = "auto"       # auto | on | off: overlap row halo exchange with the interior
     lagged_poll: bool = True    # check termination polls one window late (no queue drain)
+    graphs: str = "auto"        # auto | on | off: replay full epochs as captured HIP graphs
     start_gen: int = 0          # resume: generation number of the initial state
     sim_phase: int = 0          # resume: similarity counter at start_gen
 
@@ -68,6 +69,7 @@ class LifeConfig:
         c.poll_gens = int(self.poll_gens)
         c.overlap = {"auto": -1, "off": 0, "on": 1}[self.overlap]
         c.lagged_poll = bool(self.lagged_poll)
+        c.graphs = {"auto": -1, "off": 0, "on": 1}[self.graphs]
         c.start_gen = int(self.start_gen)
         c.sim_phase = int(self.sim_phase)
         return c
@@ -98,6 +100,7 @@ class RunReport:
     kernel_launches: int = 0
     cells: int = 0
     overlapped: bool = False
+    graph_launches: int = 0
 
     @property
     def cell_updates_per_s(self) -> float:
@@ -164,7 +167,8 @@ class Simulation:
                 "layout": self.config.resolved_layout(), "decomp": d.describe(),
                 "rank": self.rank, "ranks": d.nranks(), "tile_rows": g.H, "tile_cols": g.W,
                 "halo_rows": g.Dv, "halo_words": g.hw, "tmax": self._eng.tmax,
-                "epoch": self._eng.epoch_depth, "pitch": g.pitch, "overlap": self._eng.overlap()}
+                "epoch": self._eng.epoch_depth, "pitch": g.pitch, "overlap": self._eng.overlap(),
+                "graphs": self._eng.graphs()}
 
     # -- state -----------------------------------------------------------
     def load(self, grid: np.ndarray) -> None:
@@ -198,7 +202,8 @@ class Simulation:
         rep = RunReport(generations=r.generations, executed=r.executed, stop_reason=r.stop_reason,
                         loop_ms=r.loop_ms, first_unchanged=r.first_unchanged, extinct=r.extinct,
                         exchanges=r.exchanges, polls=r.polls, kernel_launches=r.kernel_launches,
-                        cells=self.config.width * self.config.height, overlapped=r.overlapped)
+                        cells=self.config.width * self.config.height, overlapped=r.overlapped,
+                        graph_launches=r.graph_launches)
         self.last_report = rep
         return rep
 

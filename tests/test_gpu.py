@@ -146,6 +146,31 @@ def test_split_schedule_tall_grid_flags(gpu, monkeypatch):
     assert (out == ref).all()
 
 
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_graph_replay_matches_plain_launches(gpu, layout):
+    """Full epochs replayed from captured HIP graphs (device-side generation
+    offset for the flags) == plain launches, incl. exact termination."""
+    for W, H, seed, density in CONVERGING:
+        g = random_grid(W, H, seed, density)
+        ref, rgens, _ = reference_run(g)
+        outs = {}
+        for mode in ("on", "off"):
+            sim = Simulation(LifeConfig(W, H, layout=layout, tmax=4, epoch=8, poll_gens=16, graphs=mode),
+                             engine="hip")
+            sim.load(g)
+            rep = sim.run()
+            assert rep.generations == rgens, (mode, seed)
+            assert (mode == "on") == (rep.graph_launches > 0) or rgens < 8
+            outs[mode] = sim.tile()
+        assert (outs["on"] == ref).all() and (outs["off"] == ref).all()
+    g = random_grid(1000 - 1000 % 32, 300, 5)
+    a = Simulation(LifeConfig(992, 300, gen_limit=500, graphs="on"), engine="hip")
+    a.load(g)
+    r = a.run()
+    assert r.graph_launches >= 7 and a.describe()["graphs"]
+    assert (a.tile() == life_step_torch(g, 500, device="cuda")).all()
+
+
 def test_hip_matches_cpu_backend_long_run(gpu):
     g = random_grid(1024, 512, 5)
     a = life_step(g, 300, engine="hip")
