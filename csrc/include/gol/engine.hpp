@@ -47,8 +47,10 @@ struct EngineConfig {
   bool lagged_poll = true;
   // Replay full epochs as captured HIP graphs (one per buffer parity):
   // -1 auto (single rank on a graph-capable backend), 0 off, 1 whenever the
-  // backend and transport allow it.
-  int graphs = -1;
+  // backend and transport allow it.  Off by default: on ROCm 7 / MI355X the
+  // replayed epochs measured 2-50% slower than stream launches
+  // (profiles/sweep_graphs.jsonl); the host is never the bottleneck here.
+  int graphs = 0;
 };
 
 struct RunResult {

@@ -42,7 +42,7 @@
 #include "life_kernels.hpp"
 
 #ifndef GOL_T16_WAVES
-#define GOL_T16_WAVES 3
+#define GOL_T16_WAVES 1
 #endif
 
 
@@ -138,6 +138,7 @@ __device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, 
 template <int W_, int XL_>
 struct BitsIO {
   static constexpr int W = W_, XL = XL_;
+  static constexpr bool kBits = true;
   struct Raw {
     uint32_t w[W];
   };
@@ -163,6 +164,7 @@ struct BitsIO {
 template <int W_, int XL_>
 struct U8IO {
   static constexpr int W = W_, XL = XL_;
+  static constexpr bool kBits = false;
   struct Raw {
     uint4 q[2 * W];
   };
@@ -446,12 +448,12 @@ __device__ __forceinline__ void skew_steady_and_drain(Levels<T, IO::W>& st, RowR
 // trapezoid its own rows determine (level L on [in0 + L, in1 - L)), stores
 // the level-T rows [in0 + T, in1 - T) and saves, per level, the two rows
 // next to each boundary for phase 2 (life_split_down_kernel).
-// Occupancy target: T = 16 needs ~171 VGPRs unconstrained; asking for three
-// waves per SIMD (<= 168) costs a few extra moves but 1.5x the resident
-// waves for latency hiding.
+// Optional occupancy target for the bit-layout T = 16 kernel (171 VGPRs
+// unconstrained = 2 waves/SIMD).  Forcing 3 waves/SIMD (-DGOL_T16_WAVES=3,
+// <= 168 VGPRs with small spills) measured 3-8% slower, so it is off.
 template <int T, class IO, bool SKEW, bool SPLIT>
 constexpr int min_waves_per_eu() {
-  return (T == 16 && IO::W == 1 && !SKEW) ? GOL_T16_WAVES : 1;
+  return (T == 16 && IO::W == 1 && IO::kBits && !SKEW) ? GOL_T16_WAVES : 1;
 }
 
 template <int T, class IO, bool SKEW, bool SPLIT = false>

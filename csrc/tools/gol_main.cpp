@@ -47,7 +47,7 @@ struct Options {
   bool random = false;
   uint64_t seed = 1;
   double density = 0.5;
-  int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0, overlap = -1, graphs = -1;
+  int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0, overlap = -1, graphs = 0;
   bool show = false;
 };
 

@@ -38,7 +38,7 @@ def parse_args(argv=None):
     p.add_argument("--poll", type=int, default=0)
     p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                    help="overlap the row halo exchange with interior compute")
-    p.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
+    p.add_argument("--graphs", default="off", choices=["auto", "on", "off"],
                    help="replay full epochs as captured HIP graphs")
     p.add_argument("--threads", type=int, default=0)
     p.add_argument("--style", default="serial", choices=["serial", "mpi", "openmp", "cuda"])

@@ -43,7 +43,7 @@ class LifeConfig:
     poll_gens: int = 0          # generations between termination polls (0 = 256)
     overlap: str = "auto"       # auto | on | off: overlap row halo exchange with the interior
     lagged_poll: bool = True    # check termination polls one window late (no queue drain)
-    graphs: str = "auto"        # auto | on | off: replay full epochs as captured HIP graphs
+    graphs: str = "off"         # auto | on | off: replay full epochs as captured HIP graphs
     start_gen: int = 0          # resume: generation number of the initial state
     sim_phase: int = 0          # resume: similarity counter at start_gen
 
