@@ -39,6 +39,8 @@ class Backend {
   virtual void* event_record() = 0;
   virtual void event_wait(void* ev) = 0;  // host blocks until the event completes
   virtual void event_destroy(void* ev) = 0;
+  // Non-blocking: has the event completed?  (Synchronous backends: always.)
+  virtual bool event_query(void* /*ev*/) { return true; }
   // Second queue for communication that overlaps compute (HIP: a separate
   // non-blocking stream; synchronous backends return nullptr and run
   // everything in program order).  stream_mark() records a point on `from`

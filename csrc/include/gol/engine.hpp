@@ -51,6 +51,9 @@ struct EngineConfig {
   // replayed epochs measured 2-50% slower than stream launches
   // (profiles/sweep_graphs.jsonl); the host is never the bottleneck here.
   int graphs = 0;
+  // Watchdog: fail (instead of hanging) when a termination poll waits on the
+  // device longer than this many seconds (0: GOL_WATCHDOG_S or 900 s).
+  double watchdog_s = 0;
 };
 
 struct RunResult {
@@ -65,6 +68,7 @@ struct RunResult {
   int64_t kernel_launches = 0;
   bool overlapped = false;       // epochs ran with the overlapped halo exchange
   int64_t graph_launches = 0;    // epochs replayed from a captured HIP graph
+  int64_t halo_bytes = 0;        // bytes this rank sent in halo exchanges
 };
 
 class Engine {
@@ -153,6 +157,8 @@ class Engine {
   int64_t graph_kernels_[2] = {0, 0};
   uint32_t* graph_flags_ = nullptr;   // flags buffer the graphs were captured with
   int64_t graph_runs_ = 0;
+  int64_t halo_bytes_ = 0;
+  double watchdog_s_ = 900;
   TileGeom gs_;                     // edge scratch tile: D owned rows + D halo rows each side
   void* edge_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [top|bottom][parity]
   int64_t gen_ = 0;

@@ -54,6 +54,9 @@ class Transport {
   // exchange()/allreduce enqueue device work only (no host waits), so they
   // can be captured into a HIP graph.
   virtual bool capturable() const { return false; }
+  // Throws if the communicator has failed asynchronously (RCCL async error);
+  // called by the engine while it waits on the device.
+  virtual void check_health() {}
 };
 
 // Single rank: nothing to exchange with.
@@ -105,6 +108,15 @@ class ThreadTransport final : public Transport {
   std::shared_ptr<ThreadHub> hub_;
   int rank_;
   Backend* backend_;
+  // Fault injection for tests: GOL_FAULT_DELAY_US = random
+  // delay (0..N us) before publishing and before consuming each message, to
+  // shake out ordering bugs; GOL_FAULT_GARBLE = corrupt the N-th message this
+  // rank receives (1-based; low bit of every 8th byte), which the golden comparison must
+  // catch.
+  int delay_us_ = 0;
+  int64_t garble_at_ = 0, received_ = 0;
+  uint64_t rng_ = 0;
+  void fault_delay();
 };
 
 // RCCL transport (one process per GPU).  `unique_id` is the 128-byte

@@ -13,8 +13,11 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "../kernels/life_kernels.hpp"
 #include "gol/backend.hpp"
+#include "gol/trace.hpp"
 
 #define HIP_CHECK(expr)                                                                     \
   do {                                                                                      \
@@ -142,6 +145,12 @@ class HipBackend final : public Backend {
   }
   void event_wait(void* ev) override { HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(ev))); }
   void event_destroy(void* ev) override { hipEventDestroy(static_cast<hipEvent_t>(ev)); }
+  bool event_query(void* ev) override {
+    const hipError_t e = hipEventQuery(static_cast<hipEvent_t>(ev));
+    if (e == hipErrorNotReady) return false;
+    HIP_CHECK(e);
+    return true;
+  }
   bool supports_graphs() const override { return tune_.split == 0; }  // split allocates scratch lazily
   void capture_begin() override {
     HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
@@ -279,6 +288,8 @@ bool hip_available() {
 
 std::unique_ptr<Backend> make_hip_backend(int device) {
   GOL_REQUIRE(hip_available(), "no HIP device available (HIP backend requested)");
+  // Engine trace ranges -> roctx (visible with rocprofv3 --marker-trace).
+  trace::set_hooks([](const char* m) { roctxRangePushA(m); }, [] { roctxRangePop(); });
   return std::make_unique<HipBackend>(device);
 }
 

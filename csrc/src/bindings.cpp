@@ -179,7 +179,8 @@ PYBIND11_MODULE(_gol, m) {
       .def_readwrite("poll_gens", &EngineConfig::poll_gens)
       .def_readwrite("overlap", &EngineConfig::overlap)
       .def_readwrite("lagged_poll", &EngineConfig::lagged_poll)
-      .def_readwrite("graphs", &EngineConfig::graphs);
+      .def_readwrite("graphs", &EngineConfig::graphs)
+      .def_readwrite("watchdog_s", &EngineConfig::watchdog_s);
 
   py::class_<RunResult>(m, "RunResult")
       .def_readonly("generations", &RunResult::generations)
@@ -193,6 +194,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_readonly("kernel_launches", &RunResult::kernel_launches)
       .def_readonly("overlapped", &RunResult::overlapped)
       .def_readonly("graph_launches", &RunResult::graph_launches)
+      .def_readonly("halo_bytes", &RunResult::halo_bytes)
       .def("as_dict", [](const RunResult& r) {
         py::dict d;
         d["generations"] = r.generations;
@@ -206,6 +208,7 @@ PYBIND11_MODULE(_gol, m) {
         d["kernel_launches"] = r.kernel_launches;
         d["overlapped"] = r.overlapped;
         d["graph_launches"] = r.graph_launches;
+        d["halo_bytes"] = r.halo_bytes;
         return d;
       });
 

@@ -2,7 +2,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
+
+#include "gol/trace.hpp"
 
 namespace gol {
 
@@ -56,6 +60,9 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     for (auto& e : edge_)
       for (auto& b : e) b = be_->alloc(size_t(gs_.bytes()));
   }
+  watchdog_s_ = cfg_.watchdog_s > 0 ? cfg_.watchdog_s : 900.0;
+  if (cfg_.watchdog_s <= 0)
+    if (const char* w = std::getenv("GOL_WATCHDOG_S")) watchdog_s_ = std::max(1.0, std::atof(w));
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
@@ -139,6 +146,7 @@ void Engine::exchange_columns(void* buf) {
       {false, nb[kWest], colbuf_[2], size_t(span * H)},
   };
   tr_->exchange(ops, be_->stream());
+  halo_bytes_ += 2 * span * H;
   be_->copy_2d_async(base + g_.offset(r0, 0), pitch, colbuf_[2], span, span, H);
   be_->copy_2d_async(base + g_.offset(r0, g_.cell0() + g_.W), pitch, colbuf_[3], span, span, H);
 }
@@ -148,6 +156,7 @@ void Engine::exchange_columns(void* buf) {
 // per-generation messages with a strided MPI_Type_vector column
 // (src/game_mpi.c:335-383).
 void Engine::halo_exchange() {
+  trace::Range tr("gol.halo_exchange");
   void* buf = buf_[cur_];
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
@@ -167,6 +176,7 @@ void Engine::halo_exchange() {
         {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
     };
     tr_->exchange(ops, be_->stream());
+    halo_bytes_ += 2 * int64_t(bytes);
   }
   ++exchanges_;
 }
@@ -187,6 +197,7 @@ void Engine::halo_exchange() {
 // Every computed row holds real cells, so the changed flags of all three
 // regions OR together exactly as in the plain schedule.
 void Engine::epoch_overlapped(int64_t d) {
+  trace::Range tr("gol.epoch_overlapped");
   auto nb = dec_.neighbors(rank_);
   const int64_t D = D_, H = g_.H, Dv = g_.Dv, pitch = g_.pitch;
   auto* main_in = static_cast<uint8_t*>(buf_[cur_]);
@@ -205,6 +216,7 @@ void Engine::epoch_overlapped(int64_t d) {
       {false, nb[kNorth], top, bytes},                  // north's bottom rows -> my top-edge halo
   };
   tr_->exchange(ops, comm ? comm : be_->stream());
+  halo_bytes_ += 2 * int64_t(bytes);
   void* rows_done = be_->stream_mark(comm);
   ++exchanges_;
 
@@ -308,6 +320,20 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
 
 bool Engine::poll_check(Poll& p, int64_t* first_unchanged) {
   if (p.to <= p.from) return false;
+  if (!be_->event_query(p.ev)) {
+    // Watchdog: poll instead of blocking, check the communicator, and fail
+    // with a message rather than hang forever on a dead peer or kernel.
+    trace::Range tr("gol.poll_wait");
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!be_->event_query(p.ev)) {
+      tr_->check_health();
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (s > watchdog_s_)
+        fail("watchdog: generation " + std::to_string(p.to) + " not reached after " + std::to_string(s) +
+             " s (GOL_WATCHDOG_S); a rank or kernel is stuck");
+      std::this_thread::sleep_for(std::chrono::microseconds(s < 0.01 ? 20 : 500));
+    }
+  }
   be_->event_wait(p.ev);
   be_->event_destroy(p.ev);
   p.ev = nullptr;
@@ -349,7 +375,8 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     be_->i64_async(gen_dev_, 0, /*add=*/false);  // first epoch starts at flags_base_
   }
   const int64_t g0 = graph_runs_;
-  const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_;
+  const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_;
+  trace::Range trace_run("gol.run");
   tr_->barrier();
   be_->synchronize();
   auto t0 = std::chrono::steady_clock::now();
@@ -417,6 +444,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.kernel_launches = launches_ - l0;
   res.overlapped = overlap_;
   res.graph_launches = graph_runs_ - g0;
+  res.halo_bytes = halo_bytes_ - hb0;
   res.generations = limit;
   if (found >= 0) {
     res.first_unchanged = found;

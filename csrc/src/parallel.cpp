@@ -1,5 +1,9 @@
 #include "gol/parallel.hpp"
 
+#include <atomic>
+
+#include "gol/trace.hpp"
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -82,5 +86,23 @@ ThreadPool& global_pool() {
   static ThreadPool pool(default_host_threads());
   return pool;
 }
+
+namespace trace {
+namespace {
+std::atomic<PushFn> g_push{nullptr};
+std::atomic<PopFn> g_pop{nullptr};
+}  // namespace
+
+void set_hooks(PushFn push, PopFn pop) {
+  g_push.store(push);
+  g_pop.store(pop);
+}
+void push(const char* name) {
+  if (PushFn f = g_push.load(std::memory_order_relaxed)) f(name);
+}
+void pop() {
+  if (PopFn f = g_pop.load(std::memory_order_relaxed)) f();
+}
+}  // namespace trace
 
 }  // namespace gol

@@ -1,7 +1,10 @@
 #include "gol/transport.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "gol/backend.hpp"
 #include "gol/common.hpp"
@@ -15,13 +18,26 @@ void SelfTransport::exchange(const std::vector<P2POp>& ops, void*) {
 ThreadHub::ThreadHub(int nranks) : red(), n_(nranks) { GOL_REQUIRE(nranks > 0, "hub size"); }
 
 ThreadTransport::ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, Backend* backend)
-    : hub_(std::move(hub)), rank_(rank), backend_(backend) {}
+    : hub_(std::move(hub)), rank_(rank), backend_(backend) {
+  if (const char* d = std::getenv("GOL_FAULT_DELAY_US")) delay_us_ = std::max(0, std::atoi(d));
+  if (const char* g = std::getenv("GOL_FAULT_GARBLE")) garble_at_ = std::atoll(g);
+  rng_ = 0x9E3779B97F4A7C15ull * uint64_t(rank + 1);
+}
+
+void ThreadTransport::fault_delay() {
+  if (delay_us_ <= 0) return;
+  rng_ ^= rng_ << 13;
+  rng_ ^= rng_ >> 7;
+  rng_ ^= rng_ << 17;
+  std::this_thread::sleep_for(std::chrono::microseconds(rng_ % uint64_t(delay_us_ + 1)));
+}
 
 // Rendezvous exchange: sends publish the sender's buffer, the receiver copies
 // straight out of it (device-to-device for HIP backends on one device) and
 // marks it consumed; the sender returns once all its messages are consumed.
 void ThreadTransport::exchange(const std::vector<P2POp>& ops, void*) {
   backend_->synchronize();  // sender data must be complete before publishing
+  fault_delay();
   std::vector<std::shared_ptr<ThreadHub::Msg>> sent;
   {
     std::lock_guard<std::mutex> lk(hub_->mu);
@@ -48,8 +64,16 @@ void ThreadTransport::exchange(const std::vector<P2POp>& ops, void*) {
     GOL_REQUIRE(m->bytes == op.bytes, "thread transport: message size mismatch (" +
                                           std::to_string(m->bytes) + " vs " +
                                           std::to_string(op.bytes) + ")");
+    fault_delay();
     backend_->copy_2d_async(op.buf, int64_t(op.bytes), m->buf, int64_t(op.bytes), int64_t(op.bytes), 1);
     backend_->synchronize();
+    if (garble_at_ > 0 && ++received_ == garble_at_ && op.bytes > 0) {
+      // flip the low bit of every 8th byte: cells (u8 layout) or bit-cells
+      std::vector<uint8_t> h(op.bytes);
+      backend_->copy_d2h(h.data(), op.buf, op.bytes);
+      for (size_t i = 0; i < h.size(); i += 8) h[i] ^= 0x01;
+      backend_->copy_h2d(op.buf, h.data(), op.bytes);
+    }
     {
       std::lock_guard<std::mutex> lk(hub_->mu);
       m->consumed = true;

@@ -70,6 +70,12 @@ class RcclTransport final : public Transport {
     if (hipStreamSynchronize(barrier_stream_) != hipSuccess) fail("RCCL barrier failed");
   }
   bool capturable() const override { return true; }  // grouped send/recv are stream-ordered
+  void check_health() override {
+    ncclResult_t r = ncclSuccess;
+    NCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
+    if (r != ncclSuccess && r != ncclInProgress)
+      fail(std::string("RCCL communicator failed asynchronously: ") + ncclGetErrorString(r));
+  }
 
  private:
   int rank_, size_, dev_;

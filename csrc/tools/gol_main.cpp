@@ -99,8 +99,8 @@ Options parse(int argc, char** argv) {
     else if (a == "--ranks") o.ranks = std::atoi(next().c_str());
     else if (a == "--threads") o.threads = std::atoi(next().c_str());
     else if (a == "--tmax") o.tmax = std::atoi(next().c_str());
-    else if (a == "--epoch") o.epoch = std::atoi(next().c_str());
-    else if (a == "--poll") o.poll = std::atoi(next().c_str());
+    else if (a == "--epoch" || a == "--halo-depth") o.epoch = std::atoi(next().c_str());
+    else if (a == "--poll" || a == "--poll-every") o.poll = std::atoi(next().c_str());
     else if (a == "--overlap") {
       std::string v = next();
       o.overlap = v == "on" ? 1 : v == "off" ? 0 : -1;

@@ -34,8 +34,10 @@ def parse_args(argv=None):
     p.add_argument("--decomp", default="auto")
     p.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"])
     p.add_argument("--tmax", type=int, default=0)
-    p.add_argument("--epoch", type=int, default=0)
-    p.add_argument("--poll", type=int, default=0)
+    p.add_argument("--epoch", "--halo-depth", dest="epoch", type=int, default=0,
+                   help="generations per halo exchange (deep halo depth)")
+    p.add_argument("--poll", "--poll-every", dest="poll", type=int, default=0,
+                   help="generations between termination polls")
     p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                    help="overlap the row halo exchange with interior compute")
     p.add_argument("--graphs", default="off", choices=["auto", "on", "off"],

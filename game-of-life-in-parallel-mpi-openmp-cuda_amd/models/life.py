@@ -101,6 +101,7 @@ class RunReport:
     cells: int = 0
     overlapped: bool = False
     graph_launches: int = 0
+    halo_bytes: int = 0
 
     @property
     def cell_updates_per_s(self) -> float:
@@ -203,7 +204,7 @@ class Simulation:
                         loop_ms=r.loop_ms, first_unchanged=r.first_unchanged, extinct=r.extinct,
                         exchanges=r.exchanges, polls=r.polls, kernel_launches=r.kernel_launches,
                         cells=self.config.width * self.config.height, overlapped=r.overlapped,
-                        graph_launches=r.graph_launches)
+                        graph_launches=r.graph_launches, halo_bytes=r.halo_bytes)
         self.last_report = rep
         return rep
 

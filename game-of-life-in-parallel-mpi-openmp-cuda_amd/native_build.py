@@ -108,7 +108,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         for f in futs:
             f.result()
     core = [str(objs[s]) for s in HOST_SRCS + HIP_SRCS]
-    rocm_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}", "-pthread"]
+    rocm_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM / 'lib'}",
+                 "-pthread"]
     outs = {
         "module": MODULE,
         "gol": BIN / "gol",
@@ -123,6 +124,37 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     return outs
 
 
+SELFTEST_MAIN = "tools/gol_selftest.cpp"
+SANITIZERS = {
+    "address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+    "thread": ["-fsanitize=thread"],
+    "none": [],
+}
+
+
+def build_selftest(kind: str = "address", verbose: bool = False, jobs: int | None = None) -> Path:
+    """Host-only self test (engine + CPU backend + thread transport + text
+    I/O vs the serial oracle) built with a sanitizer: bin/gol_selftest_<kind>.
+    No HIP code is involved, so ASan/UBSan/TSan apply to the whole binary."""
+    flags = SANITIZERS[kind]
+    obj_dir = REPO / "build" / f"san_{kind}"
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    BIN.mkdir(parents=True, exist_ok=True)
+    inc = [f"-I{CSRC / 'include'}", f"-I{CSRC}"]
+    srcs = HOST_SRCS + [SELFTEST_MAIN]
+    hdr = _headers_mtime()
+    objs = {s: obj_dir / (s.replace("/", "_") + ".o") for s in srcs}
+    cmds = [["g++", "-O1", "-g", "-std=c++17", "-pthread", *flags, *inc, "-c", str(CSRC / s), "-o", str(objs[s])]
+            for s in srcs if _needs(objs[s], CSRC / s, hdr)]
+    with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
+        for f in [ex.submit(_run, c, verbose) for c in cmds]:
+            f.result()
+    out = BIN / f"gol_selftest_{kind}"
+    if cmds or not out.exists():
+        _run(["g++", *flags, "-pthread", *[str(objs[s]) for s in srcs], "-o", str(out)], verbose)
+    return out
+
+
 def is_built() -> bool:
     if not MODULE.exists():
         return False
@@ -132,6 +164,10 @@ def is_built() -> bool:
 
 
 if __name__ == "__main__":
+    if "--selftest" in sys.argv:
+        kind = sys.argv[sys.argv.index("--selftest") + 1]
+        print(build_selftest(kind, verbose="-v" in sys.argv))
+        sys.exit(0)
     out = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
     for k, v in out.items():
         print(f"{k}: {v}")
