@@ -29,9 +29,9 @@ serial: build
 mpi: build
 	$(call AOUT,mpi,)
 async: build
-	$(call AOUT,mpi,)
+	$(call AOUT,async,)
 collective: build
-	$(call AOUT,mpi,)
+	$(call AOUT,collective,)
 openmp: build
 	$(call AOUT,openmp,)
 cuda: build

@@ -10,6 +10,7 @@
 // (src/game.c:238-241).  The compile-time knobs of the reference
 // (GEN_LIMIT, CHECK_SIMILARITY, SIMILARITY_FREQUENCY: README.md:65) are
 // runtime flags with the same defaults.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -38,8 +39,8 @@ struct Options {
   std::string layout = "auto";  // auto | bits | u8
   std::string decomp = "auto";
   std::string comm = "thread";  // thread | rccl (in-process ranks)
-  std::string output = "./game_output.out";
-  std::string style = "serial";  // serial | mpi | openmp | cuda
+  std::string output;  // default: the matching reference build's file (see default_output)
+  std::string style = "serial";  // serial | mpi | async | collective | openmp | cuda
   std::string metrics;
   int64_t gens = 1000;
   int sim_freq = 3;
@@ -60,7 +61,8 @@ struct Options {
                "  --sim-freq F                SIMILARITY_FREQUENCY (default 3)\n"
                "  --no-similarity             disable the similarity check\n"
                "  --random SEED[:DENSITY]     random initial grid instead of an input file\n"
-               "  --output PATH|none          output file (default ./game_output.out)\n"
+               "  --output PATH|none          output file (default: the reference build's name for\n"
+               "                              --style: ./game_output.out, ./mpi_output.out, ...)\n"
                "  --gpus N                    run on N GPUs in this process (one rank each)\n"
                "  --ranks N                   in-process ranks (subdomains; share devices)\n"
                "  --comm thread|rccl          in-process halo transport\n"
@@ -69,7 +71,8 @@ struct Options {
                "  --overlap auto|on|off       overlap the row halo exchange with the interior\n"
                "  --graphs auto|on|off        replay full epochs as captured HIP graphs\n"
                "  --threads N                 host threads for the cpu engine\n"
-               "  --style serial|mpi|openmp|cuda   stdout format of the matching reference build\n"
+               "  --style serial|mpi|async|collective|openmp|cuda\n"
+               "                              stdout format and output name of that reference build\n"
                "  --metrics-json PATH         write run metrics as JSON\n"
                "  --show                      print the final grid with VT100 escapes\n");
   std::exit(code);
@@ -126,6 +129,12 @@ Options parse(int argc, char** argv) {
   if (o.W <= 0) o.W = 30;
   if (o.H <= 0) o.H = 30;
   if (o.gpus > 0) o.ranks = o.gpus;
+  static const char* kStyles[] = {"serial", "mpi", "async", "collective", "openmp", "cuda"};
+  if (std::find(std::begin(kStyles), std::end(kStyles), o.style) == std::end(kStyles)) usage(2);
+  // Output file of the matching reference build: src/game.c:27,
+  // src/game_mpi.c:29, src/game_mpi_async.c:432, src/game_mpi_collective.c:429,
+  // src/game_openmp.c:445, src/game_cuda.cu:37.
+  if (o.output.empty()) o.output = "./" + std::string(o.style == "serial" ? "game" : o.style) + "_output.out";
   return o;
 }
 
@@ -290,12 +299,12 @@ int run(const Options& o) {
   }
 
   // stdout contract of the matching reference build.
-  if (o.style == "mpi" || o.style == "openmp") {
+  if (o.style == "mpi" || o.style == "async" || o.style == "collective" || o.style == "openmp") {
     std::printf("Reading file:\t%.2lf msecs\n", read_ms);
     std::printf("Generations:\t%d\n", int(res.generations));
     std::printf("Execution time:\t%.2lf msecs\n", res.loop_ms);
     std::printf("Writing file:\t%.2lf msecs\n", write_ms);
-    if (o.style == "mpi")
+    if (o.style != "openmp")  // every MPI process prints it (src/game_mpi.c:514)
       for (int r = 0; r < std::max(1, o.ranks); ++r) std::printf("Finished\n");
   } else if (o.style == "cuda") {
     std::printf("Generations:\t%d\n", int(res.generations));

@@ -30,7 +30,8 @@ def parse_args(argv=None):
     p.add_argument("--sim-freq", type=int, default=3, help="SIMILARITY_FREQUENCY")
     p.add_argument("--no-similarity", action="store_true")
     p.add_argument("--random", default=None, help="SEED[:DENSITY] random init instead of a file")
-    p.add_argument("--output", default="./game_output.out", help="output path or 'none'")
+    p.add_argument("--output", default=None,
+                   help="output path or 'none' (default: the reference build's name for --style)")
     p.add_argument("--decomp", default="auto")
     p.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"])
     p.add_argument("--tmax", type=int, default=0)
@@ -43,12 +44,14 @@ def parse_args(argv=None):
     p.add_argument("--graphs", default="off", choices=["auto", "on", "off"],
                    help="replay full epochs as captured HIP graphs")
     p.add_argument("--threads", type=int, default=0)
-    p.add_argument("--style", default="serial", choices=["serial", "mpi", "openmp", "cuda"])
+    p.add_argument("--style", default="serial", choices=["serial", "mpi", "async", "collective", "openmp", "cuda"])
     p.add_argument("--metrics-json", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--resume", default=None, help="checkpoint directory to resume from")
     a = p.parse_args(argv)
+    if a.output is None:  # src/game.c:27, src/game_mpi.c:29, ... src/game_cuda.cu:37
+        a.output = f"./{'game' if a.style == 'serial' else a.style}_output.out"
     if a.width <= 0:
         a.width = 30
     if a.height <= 0:
