@@ -8,10 +8,11 @@
 #   make cmake      CMake build into build/cmake
 #   make test       CPU test tier;  make test-gpu  MI355X tier
 #   make bench      1-GPU benchmark JSON line
+#   make selftest-asan / selftest-tsan   host runtime self test under ASan+UBSan / TSan
 PYTHON ?= python3
 JOBS ?= 8
 
-.PHONY: all build serial mpi async collective openmp cuda cmake test test-gpu bench clean
+.PHONY: all build serial mpi async collective openmp cuda cmake test test-gpu bench selftest-asan selftest-tsan clean
 
 all: build
 
@@ -48,6 +49,14 @@ test-gpu: build
 
 bench: build
 	$(PYTHON) bench.py
+
+selftest-asan:
+	$(PYTHON) game-of-life-in-parallel-mpi-openmp-cuda_amd/native_build.py --selftest address
+	./bin/gol_selftest_address
+
+selftest-tsan:
+	$(PYTHON) game-of-life-in-parallel-mpi-openmp-cuda_amd/native_build.py --selftest thread
+	TSAN_OPTIONS=halt_on_error=1 ./bin/gol_selftest_thread
 
 clean:
 	rm -rf build bin a.out game-of-life-in-parallel-mpi-openmp-cuda_amd/_gol.so

@@ -7,6 +7,7 @@
 //   python gol_amd/native_build.py --selftest address   -> bin/gol_selftest_address
 //   python gol_amd/native_build.py --selftest thread    -> bin/gol_selftest_thread
 //
+// T0 unit checks (decomposition math, text-format edge cases) come first.
 // Every configuration runs P ranks as threads (ThreadHub/ThreadTransport),
 // each with its own CPU backend, and compares the gathered grid and the
 // "Generations" value with cpu_reference_run.
@@ -21,6 +22,7 @@
 
 #include "gol/backend.hpp"
 #include "gol/cpu_ref.hpp"
+#include "gol/decomp.hpp"
 #include "gol/engine.hpp"
 #include "gol/io.hpp"
 #include "gol/transport.hpp"
@@ -117,6 +119,69 @@ bool text_roundtrip() {
   return ok;
 }
 
+// T0 unit checks: decomposition math and text-format edge cases.
+bool unit_checks() {
+  bool ok = true;
+  auto check = [&](bool c, const char* what) {
+    if (!c) std::printf("  unit check failed: %s\n", what);
+    ok = ok && c;
+  };
+  // split_range: balanced, contiguous, covering
+  for (int64_t n : {1, 7, 64, 1000, 32768})
+    for (int p : {1, 2, 3, 8}) {
+      int64_t next = 0;
+      for (int i = 0; i < p; ++i) {
+        const Extent e = split_range(n, p, i);
+        check(e.begin == next && e.size() >= n / p && e.size() <= n / p + 1, "split_range");
+        next = e.end;
+      }
+      check(next == n, "split_range covers");
+    }
+  // neighbours on a periodic Px x Py torus; north = previous rows (the
+  // reference inverts N/S, src/game_mpi.c:293-294)
+  for (int Px : {1, 2, 3, 4})
+    for (int Py : {1, 2, 3}) {
+      const Decomposition d(96 * Px, 10 * Py, Px, Py, 32);
+      for (int r = 0; r < d.nranks(); ++r) {
+        const auto nb = d.neighbors(r);
+        const int px = d.px_of(r), py = d.py_of(r);
+        check(nb[kNorth] == d.rank_of(px, py - 1) && nb[kSouth] == d.rank_of(px, py + 1), "N/S");
+        check(nb[kWest] == d.rank_of(px - 1, py) && nb[kEast] == d.rank_of(px + 1, py), "W/E");
+        check(nb[kNW] == d.rank_of(px - 1, py - 1) && nb[kSE] == d.rank_of(px + 1, py + 1), "corners");
+        check(d.rows(nb[kNorth]).end % d.H == d.rows(r).begin, "north tile ends where mine starts");
+        check(d.cols(r).begin % 32 == 0, "column splits word aligned");
+      }
+    }
+  // short input file: an error, not a hang (the reference loops forever,
+  // src/game.c:149-167)
+  const std::string dir = std::getenv("TMPDIR") ? std::getenv("TMPDIR") : "/tmp";
+  const std::string path = dir + "/gol_selftest_short_" + std::to_string(::getpid()) + ".txt";
+  if (FILE* f = std::fopen(path.c_str(), "w")) {
+    std::fputs("0101\n1010\n", f);
+    std::fclose(f);
+  }
+  bool threw = false;
+  std::vector<uint8_t> g;
+  try {
+    read_text_grid(path, 4, 3, g);
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  check(threw, "short file raises");
+  // CRLF line ends are accepted like '\n' (fgetc semantics skip both)
+  if (FILE* f = std::fopen(path.c_str(), "w")) {
+    std::fputs("0101\r\n1010\r\n0011\r\n", f);
+    std::fclose(f);
+  }
+  g.clear();
+  read_text_grid(path, 4, 3, g);
+  const std::vector<uint8_t> want = {0, 1, 0, 1, 1, 0, 1, 0, 0, 0, 1, 1};
+  check(g == want, "CRLF input");
+  std::remove(path.c_str());
+  std::printf("unit checks -> %s\n", ok ? "ok" : "FAILED");
+  return ok;
+}
+
 }  // namespace
 
 int main() {
@@ -129,7 +194,7 @@ int main() {
       {64, 32, "2x1", 2, Layout::Bits, 16, 16, 0, 1000, 11, 0.2},  // terminates early
       {33, 17, "1x1", 1, Layout::U8, 16, 0, -1, 1000, 4, 0.35},
   };
-  bool ok = true;
+  bool ok = unit_checks();
   for (const Case& k : cases) ok = run_case(k) && ok;
   ok = text_roundtrip() && ok;
   std::printf(ok ? "SELFTEST OK\n" : "SELFTEST FAILED\n");
