@@ -39,8 +39,8 @@ struct EngineConfig {
   int epoch = 0;                   // generations per halo exchange (0 = auto)
   int poll_gens = 0;               // generations between termination polls (0 = auto)
   // Overlap the north/south halo exchange with the interior of the epoch
-  // (edge strips recomputed in scratch tiles): -1 auto (Py > 1 and tiles
-  // tall enough), 0 off, 1 on when possible.
+  // (edge strips recomputed in scratch tiles): 1 on when possible (Py > 1,
+  // H > 2D); 0 / -1 (auto) off - measured slower than the plain exchange.
   int overlap = -1;
   // Check each termination poll one poll window later, so the host never
   // drains the device queue (stops are absorbing, so running past is exact).

@@ -51,9 +51,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     size_t n = size_t(g_.span_bytes(32 * int64_t(g_.hw)) * g_.H);
     for (auto& b : colbuf_) b = be_->alloc(n);
   }
-  // The overlapped schedule needs a non-empty interior (H > 2D) and pays
-  // about 2D extra rows of compute per epoch, so auto mode wants H >= 4D.
-  overlap_ = dec_.Py > 1 && cfg_.overlap != 0 && g_.H >= (cfg_.overlap > 0 ? 2 : 4) * int64_t(D_) + 1;
+  // The overlapped schedule needs a non-empty interior (H > 2D).  It is
+  // opt-in: its edge strips run as small, latency-bound launches (eight per
+  // epoch), which on the 32768 x 4096 per-rank tile cost 4x more than the
+  // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
+  overlap_ = dec_.Py > 1 && cfg_.overlap > 0 && g_.H >= 2 * int64_t(D_) + 1;
   if (overlap_) {
     gs_ = TileGeom::make(cfg_.layout, D_, g_.W, D_, g_.hw);
     GOL_REQUIRE(gs_.pitch == g_.pitch, "edge scratch pitch mismatch");
