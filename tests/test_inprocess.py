@@ -97,3 +97,33 @@ def test_overlap_is_opt_in(native):
     assert on.sims[0].native_engine.overlap()
     short = InProcessGroup(LifeConfig(64, 40, decomp="1x2", tmax=4, epoch=16, overlap="on"), 2, engine="cpu")
     assert not short.sims[0].native_engine.overlap()
+
+
+@pytest.mark.parametrize("overlap", ["off", "on"])
+def test_random_transport_delays_do_not_change_results(native, monkeypatch, overlap):
+    """Fault injection: random delays before every publish and
+    consume shake the message interleaving; results must stay exact."""
+    monkeypatch.setenv("GOL_FAULT_DELAY_US", "300")
+    W, H = 128, 120
+    g = random_grid(W, H, 8)
+    ref, _, _ = reference_run(g, 40)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=40, decomp="2x3", layout="u8", tmax=2, epoch=6,
+                                    overlap=overlap), 6, engine="cpu")
+    grp.load(g)
+    grp.run()
+    assert (grp.gather() == ref).all()
+
+
+def test_garbled_halo_is_detected(native, monkeypatch):
+    """Fault injection: a corrupted halo message must show up as
+    a mismatch against the serial reference - the golden comparison catches
+    communication faults."""
+    monkeypatch.setenv("GOL_FAULT_GARBLE", "3")
+    W, H = 96, 96
+    g = random_grid(W, H, 21)
+    ref, _, _ = reference_run(g, 30)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=30, decomp="1x2", layout="u8", tmax=2, epoch=4,
+                                    overlap="off"), 2, engine="cpu")
+    grp.load(g)
+    grp.run()
+    assert (grp.gather() != ref).any()
