@@ -832,6 +832,7 @@ void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const Lif
     case 2: launch_T<2, IO>(p, out_rows, tune, s); break;
     case 4: launch_T<4, IO>(p, out_rows, tune, s); break;
     case 8: launch_T<8, IO>(p, out_rows, tune, s); break;
+    case 12: launch_T<12, IO>(p, out_rows, tune, s); break;
     case 16: launch_T<16, IO>(p, out_rows, tune, s); break;
     default: fail("life_block: unsupported temporal block size " + std::to_string(T));
   }

@@ -11,7 +11,7 @@
 namespace gol {
 
 namespace {
-constexpr int kTSizes[] = {16, 8, 4, 2, 1};  // temporal block sizes built for every backend
+constexpr int kTSizes[] = {16, 12, 8, 4, 2, 1};  // temporal block sizes built for every backend
 
 int64_t min_tile_rows(const Decomposition& d) { return d.H / d.Py; }
 int64_t min_tile_cols(const Decomposition& d) { return (d.W / d.col_unit / d.Px) * d.col_unit; }
