@@ -1,6 +1,7 @@
 // life_block dispatcher: validates the launch and picks the compiled kernel
 // variant (layout x words-per-lane x cross-lane primitive).  The kernel
-// itself is in life_block_impl.hpp.
+// itself is in life_block_impl.hpp / life_group_impl.hpp (schedules in
+// life_block_launch.hpp).
 #include "life_kernels.hpp"
 
 #include <string>
@@ -36,9 +37,11 @@ const char* xlane_name(int x) {
 std::string life_block_variant(Layout layout, const LifeTuning& tune) {
   const int w = words_per_lane(layout, tune);
   if (layout == Layout::U8 && tune.u8_lds) return "u8 lds-tiled single-step";
+  const bool grouped = tune.group != 0 && tune.split == 0 && !tune.skew;
   return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=" + std::to_string(w) + " " +
          xlane_name(xlane_of(layout, w, tune)) + (tune.skew ? " skew" : "") +
-         (tune.split > 0 ? " split" : tune.split < 0 ? " split=auto" : "");
+         (tune.split > 0 ? " split" : tune.split < 0 ? " split=auto" : "") +
+         (grouped ? (tune.group < 0 ? std::string(" group=auto") : " group=" + std::to_string(tune.group)) : "");
 }
 
 int life_block_max_T(Layout layout, const LifeTuning& tune) {
@@ -52,6 +55,9 @@ void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t s
   GOL_REQUIRE(a.row_lo - a.T >= 0 && a.row_hi + a.T <= g.R() && a.row_lo < a.row_hi,
               "life_block: row range outside the tile");
   GOL_REQUIRE(g.Wp() < (int64_t(1) << 30), "life_block: row too wide");
+  // Row stores go through a buffer descriptor per row (num_records = pitch)
+  // and drop non-owned lanes at offset 2^30 (life_block_impl.hpp Writer).
+  GOL_REQUIRE(g.pitch < (int64_t(1) << 30), "life_block: row pitch must be < 1 GiB");
   const int w = words_per_lane(g.layout, tune);
   GOL_REQUIRE(g.Wp() >= w, "life_block: tile narrower than one lane's words");
   GOL_REQUIRE(g.pitch >= (g.layout == Layout::Bits ? 4 : 32) * g.Wp(), "life_block: pitch too small");

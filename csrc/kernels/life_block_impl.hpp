@@ -61,6 +61,12 @@ struct Vec {
   uint32_t w[W];
 };
 
+// Raw buffer descriptor (V#) for range-checked stores; flags = gfx950 data
+// format word of the descriptor (cdna_hip_programming.md T8).
+using BufRsrc = __amdgpu_buffer_rsrc_t;
+using U32x4 = uint32_t __attribute__((ext_vector_type(4)));
+constexpr int kBufFlags = 0x00020000;
+
 // Words of the neighbouring lanes: lane i gets lane i-1's last word (left)
 // and lane i+1's first word (right).  Edge lanes receive don't-care values;
 // they only feed the wave's halo words.
@@ -159,6 +165,10 @@ struct BitsIO {
   __device__ static __forceinline__ void store(uint8_t* row, int col, int i, uint32_t w) {
     reinterpret_cast<uint32_t*>(row)[col + i] = w;
   }
+  static constexpr int kWordBytes = 4;
+  __device__ static __forceinline__ void store_buf(BufRsrc row, int voff, uint32_t w) {
+    __builtin_amdgcn_raw_buffer_store_b32(w, row, voff, 0, 0);
+  }
 };
 
 template <int W_, int XL_>
@@ -204,6 +214,13 @@ struct U8IO {
     uint4* p = reinterpret_cast<uint4*>(row + 32 * int64_t(col + i));
     p[0] = make_uint4(spread(w, 0), spread(w, 1), spread(w, 2), spread(w, 3));
     p[1] = make_uint4(spread(w, 4), spread(w, 5), spread(w, 6), spread(w, 7));
+  }
+  static constexpr int kWordBytes = 32;
+  __device__ static __forceinline__ void store_buf(BufRsrc row, int voff, uint32_t w) {
+    const U32x4 a = {spread(w, 0), spread(w, 1), spread(w, 2), spread(w, 3)};
+    const U32x4 b = {spread(w, 4), spread(w, 5), spread(w, 6), spread(w, 7)};
+    __builtin_amdgcn_raw_buffer_store_b128(a, row, voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(b, row, voff + 16, 0, 0);
   }
 };
 
@@ -252,6 +269,10 @@ __device__ __forceinline__ Vec<W> level_full(Levels<T, W>& st, const Vec<W>& cur
     nxt.w[i] = rule(st.h0[L][s1].w[i], st.h1[L][s1].w[i], st.h0[L][s2].w[i], st.h1[L][s2].w[i], h0.w[i],
                     h1.w[i], ctr);
     st.acc[L].w[i] = bop3<tt::OR_XOR>(st.acc[L].w[i], nxt.w[i], ctr);
+    // Opaque def: in straight-line code (prologue / grouped epilogue) hipcc
+    // otherwise reassociates the flag ORs of many steps into one late tree
+    // and keeps every step's rows live for it (+75 VGPRs at T = 16).
+    asm("" : "+v"(st.acc[L].w[i]));
   }
   st.h0[L][S] = h0;
   st.h1[L][S] = h1;
@@ -359,18 +380,24 @@ struct BottomSaver {
 };
 
 // Output of one row: lanes store the words they own (not the wave halos).
+// Branch-free: every lane issues a buffer store through a descriptor over the
+// row (wave-uniform base, num_records = pitch), and lanes that own no word
+// pass an offset past num_records, which the hardware range check drops.  A
+// per-lane `if (own) store` puts an exec-masked block around every row store;
+// in the grouped kernel's straight-line epilogue those 32 blocks drove hipcc
+// to 400 registers.
 template <class IO>
 struct Writer {
   static constexpr int W = IO::W;
+  static constexpr int kDrop = 0x40000000;  // >= any row pitch: dropped
   uint8_t* out;
   int64_t pitch;
   int col;
   bool own[W];
   __device__ __forceinline__ void row(int64_t r, const Vec<W>& v) const {
-    uint8_t* p = out + r * pitch;
+    const BufRsrc rs = __builtin_amdgcn_make_buffer_rsrc(out + r * pitch, short(0), int(pitch), kBufFlags);
 #pragma unroll
-    for (int i = 0; i < W; ++i)
-      if (own[i]) IO::store(p, col, i, v.w[i]);
+    for (int i = 0; i < W; ++i) IO::store_buf(rs, own[i] ? (col + i) * IO::kWordBytes : kDrop, v.w[i]);
   }
 };
 
@@ -733,18 +760,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void l
 // and keeps the cheapest.  (Filling 1122 waves into 1024 SIMDs would put two
 // waves on a tenth of them and nearly double the kernel time; the model
 // prefers 1020 or 2040 waves there.)
-// Returns whether the skewed schedule applies (every segment >= T rows).
+// Returns whether the skewed schedule applies (every segment >= T rows);
+// *cost_out (optional) receives the model's score of the chosen plan.
 inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int simds, int occ, int min_seg,
-                 int target_waves, double overhead_rows = -1) {
+                 int target_waves, double overhead_rows = -1, double* cost_out = nullptr) {
   if (overhead_rows < 0) overhead_rows = 0.5 * T + 2;
   const int64_t smin = std::max<int64_t>({int64_t(min_seg), 2 * int64_t(T), 1});
   const int64_t max_nseg = std::max<int64_t>(1, out_rows / smin);
   int64_t best_n = 1;
+  double best = 1e300;
   if (target_waves > 0) {
     best_n = std::min<int64_t>(max_nseg, std::max<int64_t>(1, target_waves / std::max(1, p.ncolw)));
   } else {
     static constexpr double kT[] = {0, 1.2, 1.0, 0.97, 0.95};
-    double best = 1e300;
     for (int64_t n = 1; n <= max_nseg; ++n) {
       const int64_t waves = int64_t(p.ncolw) * n;
       const int64_t k = ceil_div(waves, int64_t(simds));
@@ -761,6 +789,7 @@ inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int simds, int occ
   p.nseg = int(best_n);
   p.seg_rows = int(out_rows / best_n);
   p.seg_rem = int(out_rows % best_n);
+  if (cost_out) *cost_out = target_waves > 0 ? 0.0 : best;
   return p.seg_rows >= T;
 }
 
@@ -777,65 +806,6 @@ template <int T, class IO, bool SKEW, bool SPLIT>
 int waves_per_simd() {
   static const int cached = occupancy_of(life_block_kernel<T, IO, SKEW, SPLIT>);
   return cached;
-}
-
-// Split schedule pays off when the classic schedule's redundant boundary
-// triangles (about T^2 level-rows per segment boundary) are a large share of
-// a segment's S*T level-rows.
-constexpr int kSplitMaxRowsPerT = 8;
-
-template <int T, class IO>
-void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
-  p.ncolw = int(ceil_div(p.Wp, 64 * IO::W - 2));
-  const int simds = 4 * std::max(1, tune.cus);
-  if constexpr (T >= 4) {
-    bool split = tune.split > 0;
-    if (tune.split < 0 && !tune.skew) {
-      LifeBlockParams q = p;
-      plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves);
-      split = q.seg_rows < kSplitMaxRowsPerT * T;
-    }
-    if (split && tune.scratch) {
-      const int64_t in_rows = out_rows + 2 * int64_t(T);
-      // Segments of >= 2T + 2 input rows: the last two steps (bottom state)
-      // then fall in the steady loop, never in the prologue.
-      plan(p, T, in_rows, simds, waves_per_simd<T, IO, false, true>(), std::max(tune.min_seg_rows, 2 * T + 2),
-           tune.target_waves, 0.0);
-      p.state_pitch = round_up(int64_t(p.Wp), int64_t(64));  // words per state row
-      const int64_t nb = p.nseg - 1;
-      // nb boundaries + 1 dummy slot, 2 sides, T-1 levels, 2 rows
-      p.state = static_cast<uint32_t*>(tune.scratch(size_t((nb + 1) * 2 * (T - 1) * 2 * p.state_pitch * 4)));
-      hipLaunchKernelGGL((life_block_kernel<T, IO, false, true>), dim3(unsigned(ceil_div(p.ncolw * p.nseg, 4))),
-                         dim3(256), 0, s, p);
-      if (nb > 0)
-        hipLaunchKernelGGL((life_split_down_kernel<T, IO>), dim3(unsigned(ceil_div(int64_t(p.ncolw) * nb, int64_t(4)))),
-                           dim3(256), 0, s, p);
-      return;
-    }
-  }
-  const int occ = tune.skew ? waves_per_simd<T, IO, true, false>() : waves_per_simd<T, IO, false, false>();
-  const bool skew = plan(p, T, out_rows, simds, occ, tune.min_seg_rows, tune.target_waves) && tune.skew;
-  const int waves = p.ncolw * p.nseg;
-  const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
-  if (skew)
-    hipLaunchKernelGGL((life_block_kernel<T, IO, true>), grid, block, 0, s, p);
-  else
-    hipLaunchKernelGGL((life_block_kernel<T, IO, false>), grid, block, 0, s, p);
-}
-
-// Host entry point of one compiled variant (instantiated once per
-// translation unit, life_block_*.hip).
-template <class IO>
-void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const LifeTuning& tune, hipStream_t s) {
-  switch (T) {
-    case 1: launch_T<1, IO>(p, out_rows, tune, s); break;
-    case 2: launch_T<2, IO>(p, out_rows, tune, s); break;
-    case 4: launch_T<4, IO>(p, out_rows, tune, s); break;
-    case 8: launch_T<8, IO>(p, out_rows, tune, s); break;
-    case 12: launch_T<12, IO>(p, out_rows, tune, s); break;
-    case 16: launch_T<16, IO>(p, out_rows, tune, s); break;
-    default: fail("life_block: unsupported temporal block size " + std::to_string(T));
-  }
 }
 
 }  // namespace lb

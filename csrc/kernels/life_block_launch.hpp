@@ -1,0 +1,99 @@
+// Host-side launch of one compiled life_block variant (one translation unit
+// per layout x words-per-lane x cross-lane primitive, life_block_*.hip):
+// chooses the schedule of a temporal block and its launch shape.
+//   grouped  life_group_kernel (life_group_impl.hpp): default for T >= 4 when
+//            the rows allow M segments of 2T rows per group (GOL_GROUP)
+//   classic  life_block_kernel: T < 4, short tiles, GOL_GROUP=0, GOL_SKEW=1
+//   split    life_block_kernel<SPLIT> + life_split_down_kernel: GOL_SPLIT=1
+#pragma once
+
+#include "life_group_impl.hpp"
+
+namespace gol {
+namespace hipk {
+namespace lb {
+
+// Split schedule pays off when the classic schedule's redundant boundary
+// triangles (about T^2 level-rows per segment boundary) are a large share of
+// a segment's S*T level-rows.
+constexpr int kSplitMaxRowsPerT = 8;
+
+template <int T, class IO>
+void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
+  p.ncolw = int(ceil_div(p.Wp, 64 * IO::W - 2));
+  const int simds = 4 * std::max(1, tune.cus);
+  if constexpr (T >= 4) {
+    if (tune.group != 0 && tune.split == 0 && !tune.skew) {
+      // M = 4 or 8 waves per workgroup; auto (-1) takes the cheapest of
+      // M = 4, M = 8 and the classic plan under the makespan model (classic
+      // charged its redundant triangle, T-1 rows, at the triangles' ILP).
+      LifeBlockParams g4 = p, g8 = p;
+      const double c4 = (tune.group == 4 || tune.group < 0)
+                            ? plan_group<T, 4>(g4, out_rows, simds, group_waves_per_simd<T, IO, 4>(),
+                                               tune.target_waves)
+                            : -1.0;
+      const double c8 = (tune.group == 8 || tune.group < 0)
+                            ? plan_group<T, 8>(g8, out_rows, simds, group_waves_per_simd<T, IO, 8>(),
+                                               tune.target_waves)
+                            : -1.0;
+      double cc = -1.0;
+      if (tune.group < 0) {
+        LifeBlockParams q = p;
+        plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves,
+             1.2 * (T - 1), &cc);
+      }
+      if (c4 > 0 && (c8 < 0 || c4 <= c8) && (cc < 0 || c4 <= cc)) return launch_group<T, IO, 4>(g4, s);
+      if (c8 > 0 && (cc < 0 || c8 <= cc)) return launch_group<T, IO, 8>(g8, s);
+    }
+    bool split = tune.split > 0;
+    if (tune.split < 0 && !tune.skew) {
+      LifeBlockParams q = p;
+      plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves);
+      split = q.seg_rows < kSplitMaxRowsPerT * T;
+    }
+    if (split && tune.scratch) {
+      const int64_t in_rows = out_rows + 2 * int64_t(T);
+      // Segments of >= 2T + 2 input rows: the last two steps (bottom state)
+      // then fall in the steady loop, never in the prologue.
+      plan(p, T, in_rows, simds, waves_per_simd<T, IO, false, true>(), std::max(tune.min_seg_rows, 2 * T + 2),
+           tune.target_waves, 0.0);
+      p.state_pitch = round_up(int64_t(p.Wp), int64_t(64));  // words per state row
+      const int64_t nb = p.nseg - 1;
+      // nb boundaries + 1 dummy slot, 2 sides, T-1 levels, 2 rows
+      p.state = static_cast<uint32_t*>(tune.scratch(size_t((nb + 1) * 2 * (T - 1) * 2 * p.state_pitch * 4)));
+      hipLaunchKernelGGL((life_block_kernel<T, IO, false, true>), dim3(unsigned(ceil_div(p.ncolw * p.nseg, 4))),
+                         dim3(256), 0, s, p);
+      if (nb > 0)
+        hipLaunchKernelGGL((life_split_down_kernel<T, IO>), dim3(unsigned(ceil_div(int64_t(p.ncolw) * nb, int64_t(4)))),
+                           dim3(256), 0, s, p);
+      return;
+    }
+  }
+  const int occ = tune.skew ? waves_per_simd<T, IO, true, false>() : waves_per_simd<T, IO, false, false>();
+  const bool skew = plan(p, T, out_rows, simds, occ, tune.min_seg_rows, tune.target_waves) && tune.skew;
+  const int waves = p.ncolw * p.nseg;
+  const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
+  if (skew)
+    hipLaunchKernelGGL((life_block_kernel<T, IO, true>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((life_block_kernel<T, IO, false>), grid, block, 0, s, p);
+}
+
+// Host entry point of one compiled variant (instantiated once per
+// translation unit, life_block_*.hip).
+template <class IO>
+void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const LifeTuning& tune, hipStream_t s) {
+  switch (T) {
+    case 1: launch_T<1, IO>(p, out_rows, tune, s); break;
+    case 2: launch_T<2, IO>(p, out_rows, tune, s); break;
+    case 4: launch_T<4, IO>(p, out_rows, tune, s); break;
+    case 8: launch_T<8, IO>(p, out_rows, tune, s); break;
+    case 12: launch_T<12, IO>(p, out_rows, tune, s); break;
+    case 16: launch_T<16, IO>(p, out_rows, tune, s); break;
+    default: fail("life_block: unsupported temporal block size " + std::to_string(T));
+  }
+}
+
+}  // namespace lb
+}  // namespace hipk
+}  // namespace gol

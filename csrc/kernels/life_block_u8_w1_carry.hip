@@ -1,5 +1,5 @@
 // life_block variant: U8IO<1, kXlaneCarry> (see life_block_impl.hpp).
-#include "life_block_impl.hpp"
+#include "life_block_launch.hpp"
 
 namespace gol {
 namespace hipk {

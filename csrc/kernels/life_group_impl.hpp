@@ -1,0 +1,259 @@
+// Grouped temporal-blocking schedule (default for T >= 4): the classic
+// life_block sweep of life_block_impl.hpp with the per-segment redundancy
+// removed inside a workgroup.
+//
+// The classic schedule starts every wave segment T rows above its output and
+// recomputes the triangle of level rows that the segment above also computes:
+// T(T-1) level-rows per boundary, 240 at T = 16, against 16 x 34 useful
+// level-rows per wave on the 8-GPU per-rank tile (32768 x 4096).  The split
+// schedule (life_split_down_kernel) moves the triangle into a second kernel,
+// which measured slower.  Here a workgroup of M waves owns M consecutive
+// segments of one column strip and shares its M-1 internal boundaries through
+// LDS:
+//   * wave m reads input rows from in0 = G0 + m q - T (G0 = first output row
+//     of the group).  Wave m >= 1 thus starts exactly at its boundary
+//     b_m = in0 (a trapezoid: its level-L rows begin at b_m + L) and saves,
+//     during its 2T prologue steps, its level-L rows b_m + L and b_m + L + 1
+//     (L = 1..T-1) in LDS;
+//   * after one workgroup barrier, every wave but the last finishes with the
+//     inverted triangle below its lower boundary b = in0 + q: 2T more steps
+//     (epilogue_tri) in which level e/2 is fed the lower wave's saved row
+//     instead of computing it, writing the level-T rows [b - T, b + T);
+//   * wave 0 starts and wave M-1 ends like classic waves, so only one boundary
+//     in M (the group boundaries) keeps the redundant triangle.
+// Inside a group every level row is computed exactly once.  Waves 0..M-2
+// produce q output rows each; the last wave, which also pays the redundant
+// triangle (about T-1 rows' worth), produces the rest of the group.
+//
+// The reference has no counterpart: its CUDA evolve (src/game_cuda.cu:128-148)
+// is one generation per launch, one thread per cell.
+#pragma once
+
+#include <cstdlib>
+
+#include "life_block_impl.hpp"
+
+namespace gol {
+namespace hipk {
+namespace lb {
+
+// LDS slot of one boundary: [L-1][j][word i][lane] (lane-contiguous: a wave's
+// access is 64 consecutive dwords, conflict-free).  Slot m holds wave m's
+// top rows; wave 0 writes slot 0, which nobody reads (a branch around the
+// stores splits the prologue into ~30 blocks and doubled the registers).
+template <int T, int W>
+struct LdsSaver {
+  uint32_t* slot;
+  int lane;
+  __device__ __forceinline__ void operator()(int L, int j, const Vec<W>& v) const {
+#pragma unroll
+    for (int i = 0; i < W; ++i) slot[(((L - 1) * 2 + j) * W + i) * 64 + lane] = v.w[i];
+  }
+};
+
+// Epilogue step E (0..2T-1) at sweep step k = kmain + E, window slot S: level
+// L0 = E/2 receives its row in0 + k - L0 = b + L0 + (E & 1), which is the
+// input row for L0 = 0 and the lower wave's saved row otherwise; levels
+// L0..T-1 advance and the level-T row b + E - T is written.
+template <int T, class IO, int E, int S>
+__device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>& rd, const uint32_t* below,
+                                             int lane, const Writer<IO>& wr, int k) {
+  if constexpr (E < 2 * T) {
+    constexpr int W = IO::W;
+    constexpr int L0 = E / 2;
+    Vec<W> cur;
+    if constexpr (L0 == 0) {
+      cur = rd.template take<S>(k);
+    } else {
+#pragma unroll
+      for (int i = 0; i < W; ++i) cur.w[i] = below[(((L0 - 1) * 2 + (E & 1)) * W + i) * 64 + lane];
+    }
+    wr.row(k - T, levels_full<T, IO, S, L0, T>(st, cur));
+    // Keep the scheduler inside one step: interleaving the whole epilogue
+    // (272 level bodies at T = 16) blows the register budget.
+    __builtin_amdgcn_sched_barrier(0);
+    epilogue_tri<T, IO, E + 1, (S + 1) % 3>(st, rd, below, lane, wr, k + 1);
+  }
+}
+
+#ifndef GOL_GROUP_T16_WAVES
+#define GOL_GROUP_T16_WAVES 2
+#endif
+
+// Occupancy floor of the grouped kernel.  Its LDS slots make hipcc assume
+// LDS-limited occupancy and spend up to 400 registers (VGPR + AGPR, one wave
+// per SIMD) unless the register budget is pinned: 2 waves/SIMD for T >= 12
+// (<= 256 registers; the classic kernel needs 171 at T = 16), 3 for T = 8.
+template <int T, class IO>
+constexpr int group_min_waves() {
+  return T >= 16 ? GOL_GROUP_T16_WAVES : T >= 12 ? 3 : 4;
+}
+
+template <int T, class IO, int M>
+__global__ __launch_bounds__(64 * M) __attribute__((amdgpu_waves_per_eu(group_min_waves<T, IO>())))
+void life_group_kernel(const LifeBlockParams p) {
+  constexpr int W = IO::W;
+  constexpr int kWaveOut = 64 * W - 2;
+  constexpr int kSlot = (T - 1) * 2 * W * 64;  // dwords per boundary
+  __shared__ uint32_t saved[M * kSlot];
+  const int lane = threadIdx.x & 63;
+  const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kcol = blockIdx.x / p.nseg;
+  const int grp = blockIdx.x - kcol * p.nseg;
+  const int64_t G0 = p.row_lo + int64_t(grp) * p.seg_rows + min(grp, p.seg_rem);
+  const int64_t G1 = G0 + p.seg_rows + (grp < p.seg_rem ? 1 : 0);
+  const int64_t in0 = G0 + int64_t(m) * p.grp_q - T;
+  const bool last = m == M - 1;
+  constexpr int kPro = 2 * T;
+  // Steps before the epilogue (waves 0..M-2; (q - 2T) % 3 == 0 by plan) or
+  // all steps (last wave, classic end: level-T rows up to G1 - 1).
+  const int kmain = last ? int(G1 + T - in0) : p.grp_q;
+
+  const int col = kcol * kWaveOut - 1 + W * lane;
+  const int64_t pitch = p.pitch;
+  RowReader<IO> rd;
+  Writer<IO> wr;
+  uint32_t fmask[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const int c = col + i;
+    const bool ok = c >= 0 && c < p.Wp;
+    const bool halo = (lane == 0 && i == 0) || (lane == 63 && i == W - 1);
+    rd.ok[i] = ok;
+    wr.own[i] = ok && !halo;
+    fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
+  }
+
+  Levels<T, W> st;
+#pragma unroll
+  for (int L = 0; L < T; ++L) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) st.h0[L][s].w[i] = st.h1[L][s].w[i] = st.cc[L][s].w[i] = 0u;
+      st.pipe[L].w[i] = st.acc[L].w[i] = 0u;
+    }
+  }
+
+  rd.base = p.in + in0 * pitch;  // input row of step k: in0 + k
+  rd.pitch = pitch;
+  rd.kmax = last ? kmain - 1 : kmain + 1;
+#pragma unroll
+  for (int i = 0; i < W; ++i) rd.off[i] = min(max(col + i, 0), p.Wp - 1);
+  rd.init();
+  wr.out = p.out + in0 * pitch;  // level-T row of step k: in0 + k - T
+  wr.pitch = pitch;
+  wr.col = col;
+
+  const LdsSaver<T, W> saver{saved + m * kSlot, lane};
+  prologue_tri<T, IO, 0>(st, rd, saver, NoBottom{});
+  __syncthreads();  // every wave's boundary rows are in LDS
+
+  int k = kPro;
+  constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
+  for (; k + 3 <= kmain; k += 3) {
+    wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
+    wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
+    wr.row(k + 2 - T, levels_full<T, IO, S2, 0, T>(st, rd.template take<S2>(k + 2)));
+  }
+  if (last) {
+    if (k < kmain) {
+      wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
+      if (k + 1 < kmain) wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
+    }
+  } else {
+    epilogue_tri<T, IO, 0, S0>(st, rd, saved + (m + 1) * kSlot, lane, wr, k);  // k == kmain
+  }
+
+  if (p.changed) {
+    uint32_t mask = 0;
+#pragma unroll
+    for (int L = 0; L < T; ++L) {
+      uint32_t any = 0;
+#pragma unroll
+      for (int i = 0; i < W; ++i) any |= st.acc[L].w[i] & fmask[i];
+      mask |= (__ballot(any != 0u) != 0ull ? 1u : 0u) << L;
+    }
+    uint32_t* ch = p.gen_dev ? p.changed + (*p.gen_dev + p.gen_rel) : p.changed;
+    if (lane < T && ((mask >> lane) & 1u)) ch[lane] = 1u;
+  }
+}
+
+// Plan: groups per strip (p.nseg), balanced group sizes (p.seg_rows,
+// p.seg_rem) and the per-wave row count q (p.grp_q) with q >= 2T and
+// (q - 2T) % 3 == 0, so that every non-last wave's main loop ends on the
+// window slot its epilogue starts with.  The score is plan()'s makespan
+// model: rounds x (longest wave + overhead) x resident waves x issue factor,
+// in rows of T level bodies.  Returns the cost, or -1 when the rows are too
+// few for M segments of 2T rows.
+template <int T, int M>
+double plan_group(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int target_waves) {
+  static constexpr double kT[] = {0, 1.2, 1.0, 0.97, 0.95};
+  constexpr double kOverhead = 0.4 * T;  // the two triangles (4T steps) run at lower ILP
+  const int64_t max_n = out_rows / (int64_t(M - 1) * 2 * T + 1);
+  int64_t best_n = 0;
+  int best_q = 0;
+  double best = 1e300;
+  for (int64_t n = 1; n <= max_n; ++n) {
+    const int64_t lo = out_rows / n, hi = lo + (out_rows % n ? 1 : 0);
+    // q near the balance point (Lg + T - 1) / M, on the right residue.
+    const int64_t ideal = std::max<int64_t>(2 * T, (hi + T - 1) / M);
+    int q = 0;
+    double span = 1e300;
+    for (int64_t c = ideal - 3; c <= ideal + 3; ++c) {
+      if (c < 2 * T || (c - 2 * T) % 3 != 0 || lo - int64_t(M - 1) * c < 0) continue;
+      const double s = std::max<double>(double(c), double(hi - int64_t(M - 1) * c) + (T - 1));
+      if (s < span) {
+        span = s;
+        q = int(c);
+      }
+    }
+    if (q == 0) continue;
+    const int64_t waves = int64_t(p.ncolw) * n * M;
+    const int64_t k = ceil_div(waves, int64_t(simds));
+    const int64_t rounds = ceil_div(k, int64_t(occ));
+    const int64_t kk = std::min<int64_t>(k, occ);
+    double cost = double(rounds) * (span + kOverhead) * double(kk) * kT[std::min<int64_t>(kk, 4)];
+    if (target_waves > 0)
+      cost = 1.0 + double(std::llabs(waves - int64_t(target_waves)));
+    else if (rounds > 4)
+      break;  // more groups only add rounds from here on
+    if (cost < best * 0.999) {
+      best = cost;
+      best_n = n;
+      best_q = q;
+    }
+  }
+  if (best_n == 0) return -1.0;
+  p.nseg = int(best_n);
+  p.seg_rows = int(out_rows / best_n);
+  p.seg_rem = int(out_rows % best_n);
+  p.grp_q = best_q;
+  return best;
+}
+
+template <class K>
+int occupancy_blocks(K kernel, int threads) {
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kernel, threads, 0) != hipSuccess || blocks <= 0)
+    blocks = 1;
+  return blocks;
+}
+
+// Resident waves per SIMD of the grouped kernel (a workgroup of M waves
+// spreads over the CU's 4 SIMDs).
+template <int T, class IO, int M>
+int group_waves_per_simd() {
+  static const int cached = std::max(1, occupancy_blocks(life_group_kernel<T, IO, M>, 64 * M) * M / 4);
+  return cached;
+}
+
+template <int T, class IO, int M>
+void launch_group(const LifeBlockParams& p, hipStream_t s) {
+  hipLaunchKernelGGL((life_group_kernel<T, IO, M>), dim3(unsigned(int64_t(p.ncolw) * p.nseg)), dim3(64 * M), 0, s,
+                     p);
+}
+
+}  // namespace lb
+}  // namespace hipk
+}  // namespace gol

@@ -82,6 +82,48 @@ def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
     assert (life_step(g, gens, engine="hip", layout="u8", tmax=tmax) == want).all()
 
 
+@pytest.mark.parametrize("group", ["0", "4", "8", "-1"])
+@pytest.mark.parametrize("tmax", [4, 8, 12, 16])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_grouped_schedule_vs_torch(gpu, monkeypatch, group, tmax, layout):
+    """Grouped schedule (csrc/kernels/life_group_impl.hpp: the M waves of a
+    workgroup share their segment boundaries through LDS, so only group
+    boundaries keep the redundant triangle) against the fp32 conv oracle:
+    several groups per strip, uneven group sizes, last-wave remainders, tail
+    words.  GOL_GROUP=0 is the classic schedule, -1 the model's choice."""
+    monkeypatch.setenv("GOL_GROUP", group)
+    for W, H in [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333)]:
+        g = random_grid(W, H, W + H + tmax)
+        gens = 2 * tmax + 3
+        want = life_step_torch(g, gens, device="cuda")
+        assert (life_step(g, gens, engine="hip", layout=layout, tmax=tmax) == want).all(), (W, H)
+
+
+@pytest.mark.parametrize("group", ["4", "8"])
+def test_grouped_schedule_many_groups_and_termination(gpu, monkeypatch, group):
+    """As many groups as the rows allow (GOL_TARGET_WAVES), and the exact
+    Generations count when the grid settles inside a grouped launch."""
+    monkeypatch.setenv("GOL_GROUP", group)
+    monkeypatch.setenv("GOL_TARGET_WAVES", "1000000")
+    g = random_grid(2048, 1500, 9)
+    for tmax in (8, 16):
+        want = life_step_torch(g, 3 * tmax + 1, device="cuda")
+        assert (life_step(g, 3 * tmax + 1, engine="hip", tmax=tmax) == want).all(), tmax
+    grid = np.zeros((1024, 512), dtype=np.uint8)
+    W, H, seed, density = CONVERGING[5]
+    grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)  # settles after a while
+    ref, rgens, _ = reference_run(grid)
+    for layout in ("bits", "u8"):
+        out, rep = simulate(grid, 1000, engine="hip", layout=layout, tmax=16)
+        assert rep.generations == rgens, layout
+        assert (out == ref).all(), layout
+
+
+def test_grouped_schedule_is_the_default(gpu):
+    sim = Simulation(LifeConfig(4096, 2048), engine="hip")
+    assert "group=4" in sim.describe()["backend"]
+
+
 @pytest.mark.parametrize("W,H", [(1, 1), (5, 3), (100, 70), (1023, 65), (1025, 200), (3000, 129)])
 @pytest.mark.parametrize("lds_rows", [32, 64])
 def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H, lds_rows):
