@@ -55,10 +55,15 @@ struct LdsSaver {
 // L0 = E/2 receives its row in0 + k - L0 = b + L0 + (E & 1), which is the
 // input row for L0 = 0 and the lower wave's saved row otherwise; levels
 // L0..T-1 advance and the level-T row b + E - T is written.
+// The last wave of a group shares steps E < nfull (plain input steps: the
+// 0-2 steps of its classic end that do not fill a 3-step loop iteration) and
+// stops there.  One code path for both kinds of wave: a separate remainder
+// branch beside the epilogue made hipcc allocate 199 instead of 123 VGPRs.
 template <int T, class IO, int E, int S>
 __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>& rd, const uint32_t* below,
-                                             int lane, const Writer<IO>& wr, int k) {
+                                             int lane, const Writer<IO>& wr, int k, int nfull) {
   if constexpr (E < 2 * T) {
+    if (E >= nfull) return;  // wave-uniform
     constexpr int W = IO::W;
     constexpr int L0 = E / 2;
     Vec<W> cur;
@@ -72,7 +77,7 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
     // Keep the scheduler inside one step: interleaving the whole epilogue
     // (272 level bodies at T = 16) blows the register budget.
     __builtin_amdgcn_sched_barrier(0);
-    epilogue_tri<T, IO, E + 1, (S + 1) % 3>(st, rd, below, lane, wr, k + 1);
+    epilogue_tri<T, IO, E + 1, (S + 1) % 3>(st, rd, below, lane, wr, k + 1, nfull);
   }
 }
 
@@ -105,9 +110,13 @@ void life_group_kernel(const LifeBlockParams p) {
   const int64_t in0 = G0 + int64_t(m) * p.grp_q - T;
   const bool last = m == M - 1;
   constexpr int kPro = 2 * T;
-  // Steps before the epilogue (waves 0..M-2; (q - 2T) % 3 == 0 by plan) or
-  // all steps (last wave, classic end: level-T rows up to G1 - 1).
-  const int kmain = last ? int(G1 + T - in0) : p.grp_q;
+  // Steps of the 3-step main loop end at kmain: q for waves 0..M-2 ((q - 2T)
+  // % 3 == 0 by plan); the last wave's classic end (level-T rows up to
+  // G1 - 1) takes kend steps, of which the last (kend - 2T) % 3 run as the
+  // epilogue's plain input steps.
+  const int kend = int(G1 + T - in0);
+  const int kmain = last ? kend - (kend - kPro) % 3 : p.grp_q;
+  const int nfull = last ? (kend - kPro) % 3 : 2 * T;
 
   const int col = kcol * kWaveOut - 1 + W * lane;
   const int64_t pitch = p.pitch;
@@ -137,7 +146,7 @@ void life_group_kernel(const LifeBlockParams p) {
 
   rd.base = p.in + in0 * pitch;  // input row of step k: in0 + k
   rd.pitch = pitch;
-  rd.kmax = last ? kmain - 1 : kmain + 1;
+  rd.kmax = last ? kend - 1 : kmain + 1;
 #pragma unroll
   for (int i = 0; i < W; ++i) rd.off[i] = min(max(col + i, 0), p.Wp - 1);
   rd.init();
@@ -156,14 +165,7 @@ void life_group_kernel(const LifeBlockParams p) {
     wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
     wr.row(k + 2 - T, levels_full<T, IO, S2, 0, T>(st, rd.template take<S2>(k + 2)));
   }
-  if (last) {
-    if (k < kmain) {
-      wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
-      if (k + 1 < kmain) wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
-    }
-  } else {
-    epilogue_tri<T, IO, 0, S0>(st, rd, saved + (m + 1) * kSlot, lane, wr, k);  // k == kmain
-  }
+  epilogue_tri<T, IO, 0, S0>(st, rd, saved + (m + 1) * kSlot, lane, wr, k, nfull);  // k == kmain
 
   if (p.changed) {
     uint32_t mask = 0;

@@ -63,7 +63,7 @@ class HipBackend final : public Backend {
     if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
     tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
     tune_.split = env_int("GOL_SPLIT", 0);  // measured slower so far (profiles/)
-    tune_.group = env_int("GOL_GROUP", 4);  // grouped schedule (life_group_impl.hpp)
+    tune_.group = env_int("GOL_GROUP", 8);  // grouped schedule (life_group_impl.hpp)
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
         HIP_CHECK(hipStreamSynchronize(stream_));  // earlier kernels may still use it

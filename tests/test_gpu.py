@@ -121,7 +121,7 @@ def test_grouped_schedule_many_groups_and_termination(gpu, monkeypatch, group):
 
 def test_grouped_schedule_is_the_default(gpu):
     sim = Simulation(LifeConfig(4096, 2048), engine="hip")
-    assert "group=4" in sim.describe()["backend"]
+    assert "group=8" in sim.describe()["backend"]
 
 
 @pytest.mark.parametrize("W,H", [(1, 1), (5, 3), (100, 70), (1023, 65), (1025, 200), (3000, 129)])
