@@ -33,6 +33,13 @@
 
 #include "life_block_impl.hpp"
 
+// Epilogue steps per scheduling region (sched_barrier between regions); 1
+// keeps the T = 16 kernel at 123 VGPRs (4 waves/SIMD), 2-4 let hipcc overlap
+// neighbouring steps at 130 VGPRs (3 waves/SIMD).
+#ifndef GOL_EPI_SCHED
+#define GOL_EPI_SCHED 1
+#endif
+
 namespace gol {
 namespace hipk {
 namespace lb {
@@ -76,7 +83,7 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
     wr.row(k - T, levels_full<T, IO, S, L0, T>(st, cur));
     // Keep the scheduler inside one step: interleaving the whole epilogue
     // (272 level bodies at T = 16) blows the register budget.
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (E % GOL_EPI_SCHED == GOL_EPI_SCHED - 1) __builtin_amdgcn_sched_barrier(0);
     epilogue_tri<T, IO, E + 1, (S + 1) % 3>(st, rd, below, lane, wr, k + 1, nfull);
   }
 }

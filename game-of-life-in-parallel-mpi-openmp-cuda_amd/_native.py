@@ -12,6 +12,7 @@ the engine.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import threading
 
@@ -44,6 +45,12 @@ def native():
                 raise ImportError(
                     "gol_amd native extension is missing or stale; run `python -m gol_amd.native_build`")
             native_build.build()
+        alt = os.environ.get("GOL_NATIVE_SO")  # experiment builds (scripts/build_alt.py)
+        if alt:
+            spec = importlib.util.spec_from_file_location(__package__ + "._gol", alt)
+            _mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_mod)
+            return _mod
         _mod = importlib.import_module(__package__ + "._gol")
         return _mod
 

@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Experiment builds: the default bit-layout kernel TU (life_block_bits_w1_dpp)
+recompiled with extra -D flags and linked into alt_so/<name>/_gol.so beside the
+regular objects.  bench.py loads one with GOL_NATIVE_SO=alt_so/<name>/_gol.so,
+so several kernel builds can be A/B-timed in one GPU call on one device.
+
+    python scripts/build_alt.py epi4 -DGOL_EPI_SCHED=4 -DGOL_GROUP_T16_WAVES=3
+"""
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+from gol_amd import native_build as nb  # noqa: E402
+
+
+def main() -> int:
+    name, flags = sys.argv[1], sys.argv[2:]
+    nb.build()
+    tu = "kernels/life_block_bits_w1_dpp.hip"
+    obj = nb.BUILD / f"alt_{name}.o"
+    cmd = nb._compile_cmd(nb.CSRC / tu, obj)
+    i = cmd.index("-c")
+    cmd[i:i] = flags
+    nb._run(cmd, True)
+    objs = [str(obj) if s == tu else str(nb.BUILD / (s.replace("/", "_") + ".o"))
+            for s in nb.HOST_SRCS + nb.HIP_SRCS + nb.BIND_SRCS]
+    out = REPO / "alt_so" / name / "_gol.so"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    libs = [f"-L{nb.ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx",
+            f"-Wl,-rpath,{nb.ROCM / 'lib'}", "-pthread"]
+    nb._run([nb._hipcc(), "-shared", "-fPIC", *objs, "-o", str(out), *libs], False)
+    print(out)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
