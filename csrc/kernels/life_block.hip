@@ -41,7 +41,8 @@ std::string life_block_variant(Layout layout, const LifeTuning& tune) {
   return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=" + std::to_string(w) + " " +
          xlane_name(xlane_of(layout, w, tune)) + (tune.skew ? " skew" : "") +
          (tune.split > 0 ? " split" : tune.split < 0 ? " split=auto" : "") +
-         (grouped ? (tune.group < 0 ? std::string(" group=auto") : " group=" + std::to_string(tune.group)) : "");
+         (grouped ? (tune.group < 0 ? std::string(" group=auto") : " group=" + std::to_string(tune.group)) : "") +
+         (grouped && tune.short_seg == 0 ? " short=off" : grouped && tune.short_seg == 2 ? " short=forced" : "");
 }
 
 int life_block_max_T(Layout layout, const LifeTuning& tune) {

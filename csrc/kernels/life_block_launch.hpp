@@ -3,11 +3,13 @@
 // chooses the schedule of a temporal block and its launch shape.
 //   grouped  life_group_kernel (life_group_impl.hpp): default for T >= 4 when
 //            the rows allow M segments of 2T rows per group (GOL_GROUP)
+//   short    life_short_kernel (life_short_impl.hpp): grouped, segments of
+//            Q < 2T rows, when the makespan model prefers it (GOL_SHORT)
 //   classic  life_block_kernel: T < 4, short tiles, GOL_GROUP=0, GOL_SKEW=1
 //   split    life_block_kernel<SPLIT> + life_split_down_kernel: GOL_SPLIT=1
 #pragma once
 
-#include "life_group_impl.hpp"
+#include "life_short_impl.hpp"
 
 namespace gol {
 namespace hipk {
@@ -42,8 +44,20 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
         plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves,
              1.2 * (T - 1), &cc);
       }
-      if (c4 > 0 && (c8 < 0 || c4 <= c8) && (cc < 0 || c4 <= cc)) return launch_group<T, IO, 4>(g4, s);
-      if (c8 > 0 && (cc < 0 || c8 <= cc)) return launch_group<T, IO, 8>(g8, s);
+      // Segments shorter than 2T (compiled for the default T = 16 bit / byte
+      // kernels): lets small tiles fill 4 waves per SIMD.
+      const auto better = [](double a, double b) { return a > 0 && (b < 0 || a <= b); };
+      if constexpr (T == 16 && IO::W == 1 && IO::XL == kXlaneDpp) {
+        LifeBlockParams s8 = p;
+        const double cs = tune.short_seg && (tune.group == 8 || tune.group < 0)
+                              ? plan_short<T, 8>(s8, out_rows, simds, short_waves_per_simd<T, IO, 8>(),
+                                                 tune.target_waves)
+                              : -1.0;
+        if (cs > 0 && (tune.short_seg == 2 || (better(cs, c4) && better(cs, c8) && better(cs, cc))))
+          return launch_short<T, IO, 8>(s8, s);
+      }
+      if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
+      if (better(c8, cc)) return launch_group<T, IO, 8>(g8, s);
     }
     bool split = tune.split > 0;
     if (tune.split < 0 && !tune.skew) {
