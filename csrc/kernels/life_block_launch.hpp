@@ -44,10 +44,11 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
         plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves,
              1.2 * (T - 1), &cc);
       }
-      // Segments shorter than 2T (compiled for the default T = 16 bit / byte
-      // kernels): lets small tiles fill 4 waves per SIMD.
+      // Segments shorter than 2T (compiled for the default T = 16 bit-layout
+      // kernel; the byte layout spills at 4 waves/SIMD): lets small tiles
+      // fill 4 waves per SIMD.
       const auto better = [](double a, double b) { return a > 0 && (b < 0 || a <= b); };
-      if constexpr (T == 16 && IO::W == 1 && IO::XL == kXlaneDpp) {
+      if constexpr (T == 16 && IO::kBits && IO::W == 1 && IO::XL == kXlaneDpp) {
         LifeBlockParams s8 = p;
         const double cs = tune.short_seg && (tune.group == 8 || tune.group < 0)
                               ? plan_short<T, 8>(s8, out_rows, simds, short_waves_per_simd<T, IO, 8>(),

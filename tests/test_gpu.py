@@ -119,7 +119,7 @@ def test_grouped_schedule_many_groups_and_termination(gpu, monkeypatch, group):
         assert (out == ref).all(), layout
 
 
-@pytest.mark.parametrize("layout", ["bits", "u8"])
+@pytest.mark.parametrize("layout", ["bits", "u8"])  # u8: falls back to the grouped kernel
 @pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
 def test_short_segment_schedule_vs_torch(gpu, monkeypatch, layout, W, H):
     """Short-segment groups (csrc/kernels/life_short_impl.hpp: segments of
