@@ -55,8 +55,12 @@ struct Below {
       // The lower wave saves level L at its steps 2L, 2L + 1; this wave needs
       // it at step Q + 2L.  Waves of a workgroup are co-resident and the lower
       // wave never waits on this one, so the spin ends.
-      while (__hip_atomic_load(ready + L, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      // Bounded (~0.1 s): a broken hand-off gives wrong cells, which the
+      // tests catch, instead of a hung GPU.
+      for (int spin = 0; spin < (1 << 22); ++spin) {
+        if (__hip_atomic_load(ready + L, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
         __builtin_amdgcn_s_sleep(1);
+      }
     }
     Vec<W> v;
 #pragma unroll
