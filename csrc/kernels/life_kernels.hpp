@@ -51,7 +51,7 @@ struct LifeTuning {
   int lds_rows = 32;        // rows per LDS tile (32 or 64)
   int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
-  int short_seg = 1;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
+  int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).
   std::function<void*(size_t)> scratch;
 };

@@ -64,7 +64,9 @@ class HipBackend final : public Backend {
     tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
     tune_.split = env_int("GOL_SPLIT", 0);  // measured slower so far (profiles/)
     tune_.group = env_int("GOL_GROUP", 8);  // grouped schedule (life_group_impl.hpp)
-    tune_.short_seg = env_int("GOL_SHORT", 1);  // short-segment groups (life_short_impl.hpp)
+    // Short-segment groups (life_short_impl.hpp): exact, but 10-20 % slower
+    // than the grouped kernel on the per-rank tile (profiles/sweep_short_segments.jsonl).
+    tune_.short_seg = env_int("GOL_SHORT", 0);
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
         HIP_CHECK(hipStreamSynchronize(stream_));  // earlier kernels may still use it
