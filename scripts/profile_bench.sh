@@ -10,4 +10,5 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_C
 echo "pmc1 ok"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY --output-format csv -d gpurun_out/prof/pmc2 -o run -- python3 bench.py $ARGS > gpurun_out/prof/bench_pmc2.json 2> gpurun_out/prof/bench_pmc2.err
 echo "pmc2 ok"
+timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES --output-format csv -d gpurun_out/prof/pmc3 -o run -- python3 bench.py $ARGS > gpurun_out/prof/bench_pmc3.json 2> gpurun_out/prof/bench_pmc3.err || echo "pmc3 (icache) unavailable"
 find gpurun_out/prof -name "*.csv" | head -50

@@ -9,7 +9,8 @@ import sys
 
 def short(name: str) -> str:
     n = name.replace("gol::hipk::", "").replace("(anonymous namespace)::", "").replace("lb::", "")
-    return n.split("(")[0][:90] if "life_block_kernel" not in n else n[:110]
+    keep = any(k in n for k in ("life_block_kernel", "life_group_kernel", "life_short_kernel"))
+    return n[:110] if keep else n.split("(")[0][:90]
 
 
 def main(d: str) -> None:
@@ -29,12 +30,13 @@ def main(d: str) -> None:
             continue
         agg = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
-            if not any(k in r["Kernel_Name"] for k in ("life_block_kernel", "life_step_lds")):
+            if not any(k in r["Kernel_Name"] for k in ("life_block_kernel", "life_group_kernel", "life_short_kernel",
+                                                       "life_step_lds")):
                 continue
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
         if not agg:
             continue
-        print(f"## PMC set `{sub}` (summed over all life_block_kernel dispatches)\n")
+        print(f"## PMC set `{sub}` (summed over all temporal-block kernel dispatches)\n")
         print("| counter | value |")
         print("|---|---:|")
         for k, v in sorted(agg.items()):
@@ -48,6 +50,9 @@ def main(d: str) -> None:
         if "SQ_WAIT_INST_ANY" in agg and "SQ_WAVE_CYCLES" in agg:
             derived.append(("wave cycles waiting on any instruction (fraction)",
                             agg["SQ_WAIT_INST_ANY"] / agg["SQ_WAVE_CYCLES"]))
+        if "SQC_ICACHE_HITS" in agg and "SQC_ICACHE_MISSES" in agg:
+            derived.append(("instruction cache hit rate",
+                            agg["SQC_ICACHE_HITS"] / max(1.0, agg["SQC_ICACHE_HITS"] + agg["SQC_ICACHE_MISSES"])))
         if "FETCH_SIZE" in agg:
             derived.append(("HBM fetch, GB (FETCH_SIZE is KB)", agg["FETCH_SIZE"] / 1e6))
         if derived:
