@@ -235,7 +235,7 @@ def test_graph_replay_matches_plain_launches(gpu, layout):
             outs[mode] = sim.tile()
         assert (outs["on"] == ref).all() and (outs["off"] == ref).all()
     g = random_grid(1000 - 1000 % 32, 300, 5)
-    a = Simulation(LifeConfig(992, 300, gen_limit=500, graphs="on"), engine="hip")
+    a = Simulation(LifeConfig(992, 300, gen_limit=500, epoch=64, graphs="on"), engine="hip")
     a.load(g)
     r = a.run()
     assert r.graph_launches >= 7 and a.describe()["graphs"]
