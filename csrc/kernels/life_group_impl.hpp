@@ -92,10 +92,10 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
 #define GOL_GROUP_T16_WAVES 2
 #endif
 
-// Occupancy floor of the grouped kernel.  Its LDS slots make hipcc assume
-// LDS-limited occupancy and spend up to 400 registers (VGPR + AGPR, one wave
-// per SIMD) unless the register budget is pinned: 2 waves/SIMD for T >= 12
-// (<= 256 registers; the classic kernel needs 171 at T = 16), 3 for T = 8.
+// Occupancy floor of the grouped kernel (a register cap, not a target: the
+// allocator lands at 123 VGPRs = 4 waves/SIMD for bits T = 16 and at 183 for
+// the byte layout).  Without a cap, an early version with a separate
+// remainder branch took ~400 registers (VGPR + AGPR, one wave per SIMD).
 template <int T, class IO>
 constexpr int group_min_waves() {
   return T >= 16 ? GOL_GROUP_T16_WAVES : T >= 12 ? 3 : 4;
