@@ -33,10 +33,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   tmax_ = std::min(tmax_, 16);
   // Epoch depth: a deeper halo means fewer latency-bound exchanges (or local
   // periodic fills: two ~5 us launches each) but ~D redundant rows per epoch.
-  // 8T (128) measured best with real exchanges on the 8-GPU per-rank tile and
-  // with the grouped kernel on one rank too (+4 % on 32768 x 4096 over 4T,
-  // profiles/sweep_small_tile_group.jsonl).
-  int D = cfg_.epoch > 0 ? cfg_.epoch : 8 * tmax_;
+  // With the grouped kernel the per-rank tile costs the same from 8T to 24T
+  // (profiles/sweep_epoch_group.jsonl; 4T is 4 % slower), so one rank uses 8T
+  // and several ranks 16T: half the RCCL exchanges (4 per 1000 generations),
+  // each one latency-bound.
+  int D = cfg_.epoch > 0 ? cfg_.epoch : (tr_->size() > 1 ? 16 : 8) * tmax_;
   if (dec_.Py > 1) D = int(std::min<int64_t>(D, min_tile_rows(dec_)));
   if (dec_.Px > 1) {
     int64_t cap = 32 * (min_tile_cols(dec_) / 32);
