@@ -58,6 +58,62 @@ struct LdsSaver {
   }
 };
 
+#ifndef GOL_PRIO_BUCKETS
+#define GOL_PRIO_BUCKETS 4
+#endif
+
+// Level bodies of epilogue steps 0..E-1 (step e advances levels e/2..T-1).
+template <int T>
+__host__ __device__ constexpr int epi_work_before(int E) {
+  int w = 0;
+  for (int e = 0; e < E; ++e) w += T - e / 2;
+  return w;
+}
+template <int T>
+__device__ __forceinline__ int epi_work(int nfull) {
+  return nfull >= 2 * T ? epi_work_before<T>(2 * T) : nfull * T;  // the last wave's plain steps
+}
+
+// Progress-ordered issue priority (GOL_PRIO_BUCKETS): the SIMD arbiter
+// favours the oldest of equal-priority waves, so co-resident waves with
+// equal work otherwise finish in a staircase and the last one runs alone
+// (15-20 % of a launch, scripts/wg_trace.py).  A wave drops one priority
+// level per 1/GOL_PRIO_BUCKETS of its post-barrier work, so waves that are behind
+// catch up.  Compiled out when off.
+struct Prio {
+  static constexpr int kLevels = GOL_PRIO_BUCKETS > 4 ? 4 : GOL_PRIO_BUCKETS;
+  int quarter;   // post-barrier work / levels, in level bodies
+  int done0 = 0;
+  int next = 0;  // work at which the priority drops next
+  int cur = kLevels - 1;
+  __device__ __forceinline__ explicit Prio(int wtot)
+      : quarter(max(1, wtot / max(kLevels, 1))), next(max(1, wtot / max(kLevels, 1))) {
+#if GOL_PRIO_BUCKETS
+    if (cur == 3) __builtin_amdgcn_s_setprio(3);
+    else if (cur == 2) __builtin_amdgcn_s_setprio(2);
+    else if (cur == 1) __builtin_amdgcn_s_setprio(1);
+#endif
+  }
+  __device__ __forceinline__ void at(int done) {
+#if GOL_PRIO_BUCKETS
+    if (cur > 0 && done >= next) {  // wave-uniform; one scalar compare per step
+      next += quarter;
+      --cur;
+      if (cur == 2) __builtin_amdgcn_s_setprio(2);
+      else if (cur == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#else
+    (void)done;
+#endif
+  }
+  __device__ __forceinline__ void reset() {
+#if GOL_PRIO_BUCKETS
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  }
+};
+
 // Epilogue step E (0..2T-1) at sweep step k = kmain + E, window slot S: level
 // L0 = E/2 receives its row in0 + k - L0 = b + L0 + (E & 1), which is the
 // input row for L0 = 0 and the lower wave's saved row otherwise; levels
@@ -68,9 +124,10 @@ struct LdsSaver {
 // branch beside the epilogue made hipcc allocate 199 instead of 123 VGPRs.
 template <int T, class IO, int E, int S>
 __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>& rd, const uint32_t* below,
-                                             int lane, const Writer<IO>& wr, int k, int nfull) {
+                                             int lane, const Writer<IO>& wr, int k, int nfull, Prio& prio) {
   if constexpr (E < 2 * T) {
     if (E >= nfull) return;  // wave-uniform
+    prio.at(prio.done0 + epi_work_before<T>(E));
     constexpr int W = IO::W;
     constexpr int L0 = E / 2;
     Vec<W> cur;
@@ -84,7 +141,7 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
     // Keep the scheduler inside one step: interleaving the whole epilogue
     // (272 level bodies at T = 16) blows the register budget.
     if constexpr (E % GOL_EPI_SCHED == GOL_EPI_SCHED - 1) __builtin_amdgcn_sched_barrier(0);
-    epilogue_tri<T, IO, E + 1, (S + 1) % 3>(st, rd, below, lane, wr, k + 1, nfull);
+    epilogue_tri<T, IO, E + 1, (S + 1) % 3>(st, rd, below, lane, wr, k + 1, nfull, prio);
   }
 }
 
@@ -98,7 +155,22 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
 // remainder branch took ~400 registers (VGPR + AGPR, one wave per SIMD).
 template <int T, class IO>
 constexpr int group_min_waves() {
+  if constexpr (IO::W >= 2) return T >= 12 ? 2 : T >= 8 ? 3 : 4;
   return T >= 16 ? GOL_GROUP_T16_WAVES : T >= 12 ? 3 : 4;
+}
+
+// One record per wave (LifeBlockParams::wg_trace): where it ran (HW_ID:
+// wave, SIMD, CU, SE fields; XCC_ID) and when it started and ended.
+__device__ __forceinline__ void wg_trace_record(uint64_t* tr, int M, int m, int lane, uint64_t t_start) {
+  const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+  const int64_t idx = int64_t(blockIdx.x) * M + m;
+  if (lane != 0 || idx >= kWgTraceWaves) return;
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID, 32 bits
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID, 16 bits
+  tr[4 * idx + 0] = (uint64_t(blockIdx.x) << 8) | uint64_t(m) | (uint64_t(1) << 63);
+  tr[4 * idx + 1] = (uint64_t(xcc) << 32) | hw;
+  tr[4 * idx + 2] = t_start;
+  tr[4 * idx + 3] = t_end;
 }
 
 template <int T, class IO, int M>
@@ -110,6 +182,7 @@ void life_group_kernel(const LifeBlockParams p) {
   __shared__ uint32_t saved[M * kSlot];
   const int lane = threadIdx.x & 63;
   const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t t_start = p.wg_trace ? __builtin_amdgcn_s_memrealtime() : 0;
   const int kcol = blockIdx.x / p.nseg;
   const int grp = blockIdx.x - kcol * p.nseg;
   const int64_t G0 = p.row_lo + int64_t(grp) * p.seg_rows + min(grp, p.seg_rem);
@@ -167,12 +240,18 @@ void life_group_kernel(const LifeBlockParams p) {
 
   int k = kPro;
   constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
+  // Post-barrier work in level bodies: main loop + epilogue triangle.
+  Prio prio((kmain - kPro) * T + epi_work<T>(nfull));
   for (; k + 3 <= kmain; k += 3) {
+    prio.at((k - kPro) * T);
     wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
     wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
     wr.row(k + 2 - T, levels_full<T, IO, S2, 0, T>(st, rd.template take<S2>(k + 2)));
   }
-  epilogue_tri<T, IO, 0, S0>(st, rd, saved + (m + 1) * kSlot, lane, wr, k, nfull);  // k == kmain
+
+  prio.done0 = (kmain - kPro) * T;
+  epilogue_tri<T, IO, 0, S0>(st, rd, saved + (m + 1) * kSlot, lane, wr, k, nfull, prio);  // k == kmain
+  prio.reset();
 
   if (p.changed) {
     uint32_t mask = 0;
@@ -186,6 +265,7 @@ void life_group_kernel(const LifeBlockParams p) {
     uint32_t* ch = p.gen_dev ? p.changed + (*p.gen_dev + p.gen_rel) : p.changed;
     if (lane < T && ((mask >> lane) & 1u)) ch[lane] = 1u;
   }
+  if (p.wg_trace) wg_trace_record(p.wg_trace, M, m, lane, t_start);
 }
 
 // Plan: groups per strip (p.nseg), balanced group sizes (p.seg_rows,

@@ -35,7 +35,13 @@ struct LifeBlockParams {
   // seg_rows/seg_rem = balanced OUTPUT rows per group, grp_q = output rows of
   // every wave of a group but the last.
   int grp_q;
+  // Diagnostics (GOL_WG_TRACE): if set, every wave of the grouped kernel
+  // writes {block<<8 | wave, XCC_ID<<32 | HW_ID, start, end} (s_memrealtime,
+  // 100 MHz) at wg_trace[4 * (block * M + wave)], below kWgTraceWaves waves.
+  uint64_t* wg_trace;
 };
+
+constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
 
 // Cross-lane primitive that moves the edge words between lanes.
 enum Xlane : int { kXlaneDpp = 0, kXlaneBpermute = 1, kXlaneCarry = 2 };
@@ -52,6 +58,7 @@ struct LifeTuning {
   int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
   int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
+  uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).
   std::function<void*(size_t)> scratch;
 };

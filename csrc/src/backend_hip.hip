@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -67,6 +68,14 @@ class HipBackend final : public Backend {
     // Short-segment groups (life_short_impl.hpp): exact, but 10-20 % slower
     // than the grouped kernel on the per-rank tile (profiles/sweep_short_segments.jsonl).
     tune_.short_seg = env_int("GOL_SHORT", 0);
+    if (const char* t = std::getenv("GOL_WG_TRACE")) {
+      const std::string v(t);
+      const size_t c = v.find(':');
+      if (c != std::string::npos) {
+        trace_at_ = std::atoi(v.substr(0, c).c_str());
+        trace_path_ = v.substr(c + 1);
+      }
+    }
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
         HIP_CHECK(hipStreamSynchronize(stream_));  // earlier kernels may still use it
@@ -192,8 +201,41 @@ class HipBackend final : public Backend {
   }
 
   void run_block(const BlockArgs& a) override {
+    if (trace_at_ >= 0 && launches_ == trace_at_) return run_block_traced(a);
+    ++launches_;
     hipk::launch_life_block(a, tune_, stream_);
     HIP_CHECK(hipGetLastError());
+  }
+  // GOL_WG_TRACE=<launch index>:<csv path>: one life_block launch records
+  // where and when each of its waves ran (grouped kernel, LifeBlockParams::
+  // wg_trace); scripts/wg_trace.py turns the CSV into a per-CU makespan view.
+  void run_block_traced(const BlockArgs& a) {
+    ++launches_;
+    const size_t bytes = size_t(hipk::kWgTraceWaves) * 4 * sizeof(uint64_t);
+    uint64_t* d = nullptr;
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    HIP_CHECK(hipMalloc(&d, bytes));
+    HIP_CHECK(hipMemsetAsync(d, 0, bytes, stream_));
+    tune_.wg_trace = d;
+    hipk::launch_life_block(a, tune_, stream_);
+    tune_.wg_trace = nullptr;
+    HIP_CHECK(hipGetLastError());
+    std::vector<uint64_t> h(size_t(hipk::kWgTraceWaves) * 4);
+    HIP_CHECK(hipMemcpyAsync(h.data(), d, bytes, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    HIP_CHECK(hipFree(d));
+    std::FILE* f = std::fopen(trace_path_.c_str(), "w");
+    GOL_REQUIRE(f != nullptr, "GOL_WG_TRACE: cannot open " + trace_path_);
+    std::fprintf(f, "block,wave,xcc_id,hw_id,t_start,t_end,T,rows\n");
+    for (int64_t i = 0; i < hipk::kWgTraceWaves; ++i) {
+      const uint64_t* r = &h[size_t(4 * i)];
+      if (!(r[0] >> 63)) continue;
+      std::fprintf(f, "%llu,%llu,%llu,%llu,%llu,%llu,%d,%lld\n", (unsigned long long)((r[0] & ~(1ull << 63)) >> 8),
+                   (unsigned long long)(r[0] & 255), (unsigned long long)(r[1] >> 32),
+                   (unsigned long long)(r[1] & 0xFFFFFFFFull), (unsigned long long)r[2], (unsigned long long)r[3],
+                   a.T, (long long)(a.row_hi - a.row_lo));
+    }
+    std::fclose(f);
   }
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override {
     if (cols) hipk::launch_fill_cols(static_cast<uint8_t*>(buf), g, stream_);
@@ -276,6 +318,9 @@ class HipBackend final : public Backend {
   hipStream_t comm_ = nullptr;
   void* scratch_ = nullptr;  // split-schedule boundary states
   size_t scratch_bytes_ = 0;
+  int64_t launches_ = 0;
+  int64_t trace_at_ = -1;
+  std::string trace_path_;
   std::array<hipEvent_t, 16> marks_{};
   size_t mark_next_ = 0;
   void* stage_ = nullptr;

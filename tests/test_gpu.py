@@ -49,7 +49,7 @@ def test_every_temporal_block_size(gpu, tmax, layout):
 
 @pytest.mark.parametrize("wpl,xlane,skew", [(1, 0, 0), (1, 1, 0), (1, 2, 0), (2, 0, 0), (2, 2, 0), (1, 0, 1),
                                             (1, 2, 1), (2, 0, 1)])
-@pytest.mark.parametrize("tmax", [1, 4, 8, 16])
+@pytest.mark.parametrize("tmax", [1, 4, 8, 12, 16])
 def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
     """Every compiled life_block variant (words/lane x DPP|bpermute|carry x
     schedule) against the fp32 conv oracle, including the changed-flag
