@@ -45,6 +45,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000, help="timed generations")
     ap.add_argument("--warmup", type=int, default=100, help="untimed generations")
+    ap.add_argument("--prewarm", type=int, default=8192,
+                    help="extra untimed generations before the warmup: the GPU clock needs ~10 ms of load to ramp "
+                         "(100 warmup gens = 1.3 ms left the first timed run 6%% slow, profiles/sweep_warmup.jsonl)")
     ap.add_argument("--size", type=int, default=32768, help="grid side (cells)")
     ap.add_argument("--height", type=int, default=0, help="grid height if not square (experiments only)")
     ap.add_argument("--layout", default="bits", choices=["bits", "u8"])
@@ -85,7 +88,7 @@ def main() -> int:
 
     S = a.size
     Hg = a.height or S
-    total = a.warmup + a.steps * a.repeats
+    total = a.prewarm + a.warmup + a.steps * a.repeats
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
                      poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs)
     sim = Simulation(cfg, transport=transport, backend=backend)
@@ -99,8 +102,8 @@ def main() -> int:
             torch.cuda.synchronize()
         backend.synchronize()
 
-    if a.warmup > 0:
-        eng.run_until(sim.generation + a.warmup)
+    if a.prewarm + a.warmup > 0:
+        eng.run_until(sim.generation + a.prewarm + a.warmup)
     best = None
     executed = a.steps
     for _ in range(a.repeats):
@@ -143,6 +146,7 @@ def main() -> int:
                 "tmax": desc["tmax"],
                 "epoch": desc["epoch"],
                 "generations_timed": gens,
+                "prewarm_generations": a.prewarm,
                 "loop_ms_engine": r.loop_ms,
                 "exchanges": r.exchanges,
                 "polls": r.polls,

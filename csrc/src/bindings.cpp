@@ -11,6 +11,7 @@
 
 #include <cstring>
 #include <thread>
+#include <tuple>
 
 #include "gol/backend.hpp"
 #include "gol/cpu_ref.hpp"
@@ -135,7 +136,23 @@ PYBIND11_MODULE(_gol, m) {
       .def("rank", &Transport::rank)
       .def("size", &Transport::size)
       .def("name", &Transport::name)
-      .def("barrier", &Transport::barrier, py::call_guard<py::gil_scoped_release>());
+      .def("barrier", &Transport::barrier, py::call_guard<py::gil_scoped_release>())
+      // Raw access for plumbing tests: ops = [(send, peer, address, bytes)],
+      // addresses in the transport's address space (device memory for rccl).
+      .def("exchange",
+           [](Transport& t, const std::vector<std::tuple<bool, int, std::uintptr_t, size_t>>& ops,
+              std::uintptr_t stream) {
+             std::vector<P2POp> v;
+             for (const auto& [send, peer, addr, bytes] : ops)
+               v.push_back({send, peer, reinterpret_cast<void*>(addr), bytes});
+             py::gil_scoped_release rel;
+             t.exchange(v, reinterpret_cast<void*>(stream));
+           })
+      .def("allreduce_max_u32",
+           [](Transport& t, std::uintptr_t addr, size_t n, std::uintptr_t stream) {
+             py::gil_scoped_release rel;
+             t.allreduce_max_u32(reinterpret_cast<uint32_t*>(addr), n, reinterpret_cast<void*>(stream));
+           });
   m.def("self_transport", []() { return std::shared_ptr<Transport>(new SelfTransport()); });
   py::class_<ThreadHub, std::shared_ptr<ThreadHub>>(m, "ThreadHub").def(py::init<int>());
   m.def("thread_transport",

@@ -319,6 +319,21 @@ def test_rccl_single_rank_self_exchange(gpu):
     tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0)
     assert tr.size() == 1 and tr.name() == "rccl"
     tr.barrier()
+    # The engine's row-phase op order (send N, recv S, send S, recv N) with
+    # every neighbour = self: pairs match in issue order, as between two ranks.
+    n = 256 * 4160  # 256 halo rows of a 32768-cell bit tile's pitch
+    top = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    bot = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    halo_s = torch.zeros_like(top)
+    halo_n = torch.zeros_like(top)
+    s = torch.cuda.current_stream().cuda_stream
+    tr.exchange([(True, 0, top.data_ptr(), n), (False, 0, halo_s.data_ptr(), n),
+                 (True, 0, bot.data_ptr(), n), (False, 0, halo_n.data_ptr(), n)], s)
+    flags = torch.tensor([3, 0, 7], dtype=torch.int32, device="cuda")
+    tr.allreduce_max_u32(flags.data_ptr(), 3, s)
+    torch.cuda.synchronize()
+    assert torch.equal(halo_s, top) and torch.equal(halo_n, bot)
+    assert flags.tolist() == [3, 0, 7]
 
 
 def test_torch_tensor_views_of_engine_buffers(gpu):

@@ -127,3 +127,38 @@ def test_garbled_halo_is_detected(native, monkeypatch):
     grp.load(g)
     grp.run()
     assert (grp.gather() != ref).any()
+
+
+def test_thread_transport_pair_matching_two_ranks(native):
+    """The row-phase op order of Engine::halo_exchange (engine.cpp) with
+    Py = 2, where north and south are the same peer: messages between a pair
+    must match in issue order (send N <-> recv S, send S <-> recv N), the
+    contract RCCL's grouped send/recv also follows."""
+    import threading
+
+    import numpy as np
+
+    C = native
+    hub = C.ThreadHub(2)
+    bes = [C.cpu_backend(1) for _ in range(2)]
+    trs = [C.thread_transport(hub, r, bes[r]) for r in range(2)]
+    n = 4096
+    rng = np.random.default_rng(0)
+    top = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(2)]
+    bot = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(2)]
+    halo_s = [np.zeros(n, np.uint8) for _ in range(2)]
+    halo_n = [np.zeros(n, np.uint8) for _ in range(2)]
+
+    def run(r):
+        p = 1 - r
+        trs[r].exchange([(True, p, top[r].ctypes.data, n), (False, p, halo_s[r].ctypes.data, n),
+                         (True, p, bot[r].ctypes.data, n), (False, p, halo_n[r].ctypes.data, n)], 0)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(30)
+    for r in range(2):
+        assert (halo_s[r] == top[1 - r]).all()  # south neighbour's top rows -> my bottom halo
+        assert (halo_n[r] == bot[1 - r]).all()  # north neighbour's bottom rows -> my top halo
