@@ -44,7 +44,14 @@ def native():
             if os.environ.get("GOL_NO_AUTOBUILD") == "1":
                 raise ImportError(
                     "gol_amd native extension is missing or stale; run `python -m gol_amd.native_build`")
-            native_build.build()
+            # torchrun starts one process per GPU: build once, the others wait
+            # on the lock and find the fresh artefacts.
+            import fcntl  # noqa: PLC0415
+
+            with open(native_build.MODULE.parent / ".build.lock", "w") as lk:
+                fcntl.flock(lk, fcntl.LOCK_EX)
+                if not native_build.is_built():
+                    native_build.build()
         alt = os.environ.get("GOL_NATIVE_SO")  # experiment builds (scripts/build_alt.py)
         if alt:
             spec = importlib.util.spec_from_file_location(__package__ + "._gol", alt)
