@@ -4,7 +4,10 @@ vendored) and run on the same input file as `bin/gol`; the output file must
 be byte-identical and the "Generations:" line equal.  The serial reference
 indexes [y][x] and is only correct for square grids (README.md:61), so the
 grids are square."""
+import gzip
+import json
 import subprocess
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -68,3 +71,42 @@ def test_output_bytes_match_reference_game_c_on_gpu(reference_serial, gol_bin, t
     f = tmp_path / "in.txt"
     io.generate(str(f), N, N, seed=seed, density=density)
     _compare(reference_serial, gol_bin, tmp_path, N, f, "--engine", "hip")
+
+
+# Recorded outputs of the same reference build on the same GRIDS inputs
+# (tests/make_game_c_fixtures.py), for boxes without the reference mount.
+FIXTURES = Path(__file__).resolve().parent / "fixtures" / "game_c"
+
+
+def _fixture(N, seed, density):
+    key = f"{N}_{seed}_{density}"
+    gens = json.loads((FIXTURES / "generations.json").read_text())[key]
+    return gens, gzip.decompress((FIXTURES / f"{key}.out.gz").read_bytes())
+
+
+def _compare_fixture(gol_bin, tmp_path, N, seed, density, engine):
+    f = tmp_path / "in.txt"
+    io.generate(str(f), N, N, seed=seed, density=density)
+    our_out, our_bytes = _run_ours(gol_bin, tmp_path, N, f, "--engine", engine)
+    gens, want = _fixture(N, seed, density)
+    assert generations_line(our_out) == gens
+    assert our_bytes == want
+
+
+@pytest.mark.parametrize("N,seed,density", GRIDS)
+def test_output_bytes_match_recorded_game_c(gol_bin, tmp_path, N, seed, density):
+    _compare_fixture(gol_bin, tmp_path, N, seed, density, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,seed,density", GRIDS)
+def test_output_bytes_match_recorded_game_c_on_gpu(gol_bin, tmp_path, N, seed, density):
+    _compare_fixture(gol_bin, tmp_path, N, seed, density, "hip")
+
+
+@pytest.mark.parametrize("N,seed,density", GRIDS)
+def test_recorded_game_c_fixtures_are_current(reference_serial, tmp_path, N, seed, density):
+    f = tmp_path / "in.txt"
+    io.generate(str(f), N, N, seed=seed, density=density)
+    ref_out, ref_bytes = run_reference_serial(reference_serial, tmp_path, N, N, f)
+    assert _fixture(N, seed, density) == (generations_line(ref_out), ref_bytes)
