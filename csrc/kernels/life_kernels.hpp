@@ -88,6 +88,8 @@ void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream);
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);
 void launch_fill_rows(uint8_t* buf, const TileGeom& g, hipStream_t s);
+// Fused cols+rows periodic fill (bit layout); false if the geometry needs the two-launch path.
+bool launch_fill_all(uint8_t* buf, const TileGeom& g, hipStream_t s);
 void launch_alive(const uint8_t* buf, const TileGeom& g, uint32_t* any_flag,
                   unsigned long long* count, hipStream_t s);
 // Owned rows [r0, r0+n) from a device staging array of 0/1-or-ASCII bytes.

@@ -238,8 +238,11 @@ class HipBackend final : public Backend {
     std::fclose(f);
   }
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override {
-    if (cols) hipk::launch_fill_cols(static_cast<uint8_t*>(buf), g, stream_);
-    if (rows) hipk::launch_fill_rows(static_cast<uint8_t*>(buf), g, stream_);
+    auto* p = static_cast<uint8_t*>(buf);
+    if (!(cols && rows && hipk::launch_fill_all(p, g, stream_))) {
+      if (cols) hipk::launch_fill_cols(p, g, stream_);
+      if (rows) hipk::launch_fill_rows(p, g, stream_);
+    }
     HIP_CHECK(hipGetLastError());
   }
   void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {
