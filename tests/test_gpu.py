@@ -347,3 +347,30 @@ def test_torch_tensor_views_of_engine_buffers(gpu):
     v[0] = 7
     torch.cuda.synchronize()
     assert int(x[0].item()) == 7
+
+
+@pytest.mark.parametrize("W,H,epoch", [(64, 5, 32), (96, 70, 64), (2048, 40, 128), (32, 1, 16)])
+def test_fused_periodic_fill_matches_cpu_buffer(gpu, W, H, epoch):
+    """Single-rank halo_exchange is one fused launch (fill_all_bits): the whole
+    padded buffer (column halos, halo rows and corners, multi-wrap when Dv > H)
+    must equal the CPU backend's two-pass fill."""
+    import torch
+
+    from gol_amd.parallel.dist import tensor_view
+
+    g = random_grid(W, H, W * 3 + H)
+    bufs = []
+    for engine in ("hip", "cpu"):
+        sim = Simulation(LifeConfig(W, H, gen_limit=64, layout="bits", epoch=epoch), engine=engine)
+        sim.load(g)
+        eng = sim.native_engine
+        eng.halo_exchange()
+        sim.backend.synchronize()
+        geo = eng.geom
+        raw = tensor_view(eng.current_buffer(), geo.R() * geo.pitch, engine == "hip").cpu().numpy().copy()
+        used = 4 * (2 * geo.hw + W // 32)  # bytes per row that hold cells (pitch padding excluded)
+        bufs.append((raw.reshape(geo.R(), geo.pitch)[:, :used], geo.Dv, geo.hw))
+        torch.cuda.synchronize()
+    (a, dva, hwa), (b, dvb, hwb) = bufs
+    assert (dva, hwa) == (dvb, hwb) and dva > 0 and hwa > 0
+    assert np.array_equal(a, b)
