@@ -65,6 +65,9 @@ class Backend {
 
   // Kernels.
   virtual void run_block(const BlockArgs& a) = 0;
+  // Throws if a kernel enqueued so far reported an error through the
+  // backend's device-visible error word (call after the work completed).
+  virtual void check_device_errors() {}
   // Largest temporal block size (generations per run_block) the backend runs
   // at full occupancy for this layout; the engine's default tmax.
   virtual int preferred_tmax(Layout) const { return 16; }

@@ -81,6 +81,7 @@ void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t s
     p.changed = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
   }
   p.wg_trace = tune.wg_trace;
+  p.err = tune.err;
   const int64_t rows = a.row_hi - a.row_lo;
   const int x = xlane_of(g.layout, w, tune);
   if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {

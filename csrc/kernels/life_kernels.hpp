@@ -39,6 +39,10 @@ struct LifeBlockParams {
   // writes {block<<8 | wave, XCC_ID<<32 | HW_ID, start, end} (s_memrealtime,
   // 100 MHz) at wg_trace[4 * (block * M + wave)], below kWgTraceWaves waves.
   uint64_t* wg_trace;
+  // Device-visible error word (host-mapped, Backend::check_device_errors):
+  // a kernel that has to give up (life_short_kernel's bounded LDS hand-off
+  // wait) sets it instead of continuing silently with invalid rows.
+  uint32_t* err;
 };
 
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
@@ -59,6 +63,7 @@ struct LifeTuning {
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
   int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
   uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
+  uint32_t* err = nullptr;       // LifeBlockParams::err
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).
   std::function<void*(size_t)> scratch;
 };

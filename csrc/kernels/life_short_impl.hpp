@@ -54,18 +54,25 @@ struct Below {
   const uint32_t* slot;
   uint32_t* ready;
   int lane;
+  uint32_t* err;
   template <int L, int J>
   __device__ __forceinline__ Vec<W> row() const {
     if constexpr (J == 0) {
       // The lower wave saves level L at its steps 2L, 2L + 1; this wave needs
       // it at step Q + 2L.  Waves of a workgroup are co-resident and the lower
       // wave never waits on this one, so the spin ends.
-      // Bounded (~0.1 s): a broken hand-off gives wrong cells, which the
-      // tests catch, instead of a hung GPU.
+      // Bounded (~0.1 s) instead of a hung GPU; giving up raises the launch's
+      // error word, which the host turns into an error at its next poll
+      // (Backend::check_device_errors), so the invalid rows never go unnoticed.
+      bool arrived = false;
       for (int spin = 0; spin < (1 << 22); ++spin) {
-        if (__hip_atomic_load(ready + L, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
+        if (__hip_atomic_load(ready + L, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) {
+          arrived = true;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
+      if (!arrived && err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     Vec<W> v;
 #pragma unroll
@@ -175,7 +182,7 @@ void life_short_kernel(const LifeBlockParams p) {
   const LdsFlagSaver<T, W> saver{saved + m * kSlot, ready + m * T, lane};
 
   if (!last) {
-    const Below<T, W> below{saved + (m + 1) * kSlot, ready + (m + 1) * T, lane};
+    const Below<T, W> below{saved + (m + 1) * kSlot, ready + (m + 1) * T, lane, p.err};
     para_steps<T, IO, Q, 0>(st, rd, saver, below, wr);
   } else {
     prologue_tri<T, IO, 0>(st, rd, saver, NoBottom{});

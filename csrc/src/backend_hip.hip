@@ -76,6 +76,11 @@ class HipBackend final : public Backend {
         trace_path_ = v.substr(c + 1);
       }
     }
+    // Kernel error word: fine-grained pinned host memory the kernels write
+    // through its device alias and the host reads without a copy.
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(uint32_t), hipHostMallocMapped));
+    *err_host_ = 0;
+    HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&tune_.err), err_host_, 0));
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
         HIP_CHECK(hipStreamSynchronize(stream_));  // earlier kernels may still use it
@@ -92,6 +97,7 @@ class HipBackend final : public Backend {
     if (comm_) hipStreamSynchronize(comm_);
     if (stage_) hipFree(stage_);
     if (scratch_) hipFree(scratch_);
+    if (err_host_) hipHostFree(err_host_);
     for (auto& e : marks_)
       if (e) hipEventDestroy(e);
     if (comm_) hipStreamDestroy(comm_);
@@ -237,6 +243,14 @@ class HipBackend final : public Backend {
     }
     std::fclose(f);
   }
+  void check_device_errors() override {
+    const uint32_t e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
+    if (e != 0) {
+      *err_host_ = 0;
+      fail("life_short kernel: a wave gave up waiting for its neighbour's LDS rows (device error word " +
+           std::to_string(e) + "); the rows of that launch are invalid");
+    }
+  }
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override {
     auto* p = static_cast<uint8_t*>(buf);
     if (!(cols && rows && hipk::launch_fill_all(p, g, stream_))) {
@@ -328,6 +342,7 @@ class HipBackend final : public Backend {
   size_t mark_next_ = 0;
   void* stage_ = nullptr;
   int64_t stage_bytes_ = 0;
+  uint32_t* err_host_ = nullptr;
 };
 
 }  // namespace

@@ -350,6 +350,7 @@ bool Engine::poll_check(Poll& p, int64_t* first_unchanged) {
   be_->event_wait(p.ev);
   be_->event_destroy(p.ev);
   p.ev = nullptr;
+  be_->check_device_errors();
   const uint32_t* h = flags_host_ + (p.from + 1 - flags_base_);
   for (int64_t i = 0; i < p.to - p.from; ++i)
     if (h[i] == 0) {
@@ -448,6 +449,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   }
   if (have_pending) poll_check(pending, &found);
   be_->synchronize();
+  be_->check_device_errors();
   tr_->barrier();
   auto t1 = std::chrono::steady_clock::now();
   res.loop_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -470,11 +472,14 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
       res.generations = found - 1;
       res.stop_reason = "extinction";
     } else if (cfg_.check_similarity) {
-      // Similarity checks happen at generations t > start with
-      // (t - start + sim_phase) % F == 0 (counter reset only on a failed check,
-      // src/game.c:181-189).
+      // Similarity checks happen at generations t > start_gen with
+      // (t - start_gen + sim_phase) % F == 0 (counter reset only on a failed
+      // check, src/game.c:181-189).  The phase is anchored at the configured
+      // start generation, not at this call's first generation: an earlier
+      // advance()/run_until() on the same engine does not shift it
+      // (utils/termination.py:reported_generations).
       const int64_t F = cfg_.sim_freq;
-      int64_t k = found - start + cfg_.sim_phase;
+      int64_t k = found - cfg_.start_gen + cfg_.sim_phase;
       int64_t tsim = found + ((F - (k % F)) % F);
       if (tsim <= limit) {
         res.generations = tsim - 1;

@@ -74,24 +74,38 @@ void read_text_tile(const std::string& path, int64_t W, int64_t H, Extent rows, 
   const int64_t exact = H * (W + 1);
 
   if (size == exact || size == exact - 1) {
-    // Exact layout: parallel pread of each row's subarray (MPI-IO view math).
+    // Exact layout: parallel pread of each row's subarray (MPI-IO view math,
+    // src/game_mpi_async.c:180-199).  Whether the file HAS that layout is a
+    // property of the whole file, so every rank checks the same bytes - the
+    // line break of every row, whatever its own column range - and all ranks
+    // of a decomposed run take the same path (a rank-local check let the
+    // last-column ranks fall back to the fgetc parse while the others read
+    // fixed offsets, and the tiles disagreed).
+    const int64_t nl_rows = size == exact ? H : H - 1;  // the last '\n' may be missing
     std::atomic<bool> bad{false};
-    global_pool().parallel_for(nr, [&](int64_t b, int64_t e) {
-      std::vector<uint8_t> line(size_t(nc + 1));
-      for (int64_t i = b; i < e && !bad.load(); ++i) {
-        const int64_t r = rows.begin + i;
-        const int64_t off = r * (W + 1) + cols.begin;
-        bool want_nl = cols.end == W && off + nc < size;
-        pread_all(f.fd, line.data(), size_t(nc + (want_nl ? 1 : 0)), off, path);
-        if (want_nl && line[size_t(nc)] != '\n') {
-          bad = true;
-          break;
-        }
-        uint8_t* dst = &out[size_t(i * nc)];
-        for (int64_t x = 0; x < nc; ++x) dst[x] = cell_of(line[size_t(x)]);
+    global_pool().parallel_for(nl_rows, [&](int64_t b, int64_t e) {
+      for (int64_t r = b; r < e && !bad.load(std::memory_order_relaxed); ++r) {
+        uint8_t ch = 0;
+        pread_all(f.fd, &ch, 1, r * (W + 1) + W, path);
+        if (ch != '\n') bad = true;
       }
-    }, 64);
-    if (!bad.load()) return;
+    }, 4096);
+    if (!bad.load()) {
+      // Every row is W cell bytes + '\n': read fixed offsets like the
+      // reference's MPI-IO builds, '1' alive and any other byte dead.  (A
+      // stray line break among a row's cells would leave the serial fgetc
+      // loop short of W*H cells, where the reference spins forever - quirk
+      // Q8 - so the fixed-offset reading is the defined behaviour for it.)
+      global_pool().parallel_for(nr, [&](int64_t b, int64_t e) {
+        std::vector<uint8_t> line(static_cast<size_t>(nc));
+        for (int64_t i = b; i < e; ++i) {
+          pread_all(f.fd, line.data(), size_t(nc), (rows.begin + i) * (W + 1) + cols.begin, path);
+          uint8_t* dst = &out[size_t(i * nc)];
+          for (int64_t x = 0; x < nc; ++x) dst[x] = cell_of(line[size_t(x)]);
+        }
+      }, 64);
+      return;
+    }
   }
   // Sequential fallback with the reference's fgetc semantics (skip '\n'; we
   // also skip '\r' so CRLF files work): cells are the first W*H other bytes.

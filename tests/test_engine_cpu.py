@@ -102,6 +102,27 @@ def test_advance_exact_and_generation_counter(native):
     assert sim.alive_count() == int(life_step_numpy(g, 23).sum())
 
 
+@pytest.mark.parametrize("first", [("run_until", 1), ("run_until", 2), ("advance", 1), ("advance", 5)])
+@pytest.mark.parametrize("layout", ["u8", "bits"])
+def test_run_after_partial_run_keeps_similarity_phase(native, first, layout):
+    """the similarity phase is anchored at start_gen, so run() after
+    an earlier advance()/run_until() on the same engine reports the same
+    Generations as one uninterrupted reference loop (48x40, seed 20 -> 875)."""
+    g = random_grid(64, 40, 15, 0.3) if layout == "bits" else random_grid(48, 40, 20)
+    ref, rgens, _ = reference_run(g)
+    assert rgens < 1000
+    sim = Simulation(LifeConfig(g.shape[1], g.shape[0], layout=layout), engine="cpu")
+    sim.load(g)
+    kind, n = first
+    if kind == "run_until":
+        sim.native_engine.run_until(n)
+    else:
+        sim.advance(n)
+    rep = sim.run()
+    assert rep.generations == rgens
+    assert (sim.tile() == ref).all()
+
+
 def test_random_init_is_layout_and_decomposition_independent(native):
     a = Simulation(LifeConfig(96, 40, layout="bits"), engine="cpu")
     b = Simulation(LifeConfig(96, 40, layout="u8"), engine="cpu")

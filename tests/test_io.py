@@ -57,6 +57,38 @@ def test_fgetc_semantics_and_crlf(tmp_path, native):
     assert (io.read_grid(str(q), 4, 3) == g).all()
 
 
+@pytest.mark.parametrize("body", [
+    "1" * 10 + "0" * 15 + "\n\n",          # 25 cells + 2 newlines = 27 B = exact size of 8x3
+    "10110011\n0110\n1001\n01100110\n",    # exact size, misplaced line breaks
+    "10110011\n01101001\n01100110",        # exact size - 1, no trailing newline
+    "10110011\n01101001\n01100110\n",      # exact layout
+])
+def test_column_tiles_take_the_same_path_as_the_full_read(tmp_path, native, body):
+    """Every column rank of a decomposed read sees the same layout decision,
+    so the tiles assemble to the full-width read."""
+    p = tmp_path / "g.txt"
+    p.write_bytes(body.encode())
+    W, H = 8, 3
+    full = io.read_grid(str(p), W, H)
+    for cols in [(0, 4), (4, 8), (0, 3), (3, 8), (2, 6)]:
+        for rows in [(0, H), (1, 3), (0, 1)]:
+            t = io.read_tile(str(p), W, H, rows, cols)
+            assert (t == full[rows[0]:rows[1], cols[0]:cols[1]]).all(), (cols, rows)
+
+
+def test_line_break_inside_an_exact_row_reads_fixed_offsets(tmp_path, native):
+    # Exact size and every row's '\n' in place, but a '\r' among the cells:
+    # the reference's serial fgetc loop would come up one cell short and spin
+    # (quirk Q8); its MPI-IO builds read fixed offsets, which every tile does
+    # here too - the stray byte is a dead cell and all ranks agree.
+    p = tmp_path / "g.txt"
+    p.write_bytes(b"0110\n1\r01\n0011\n")
+    full = io.read_grid(str(p), 4, 3)
+    assert full.tolist() == [[0, 1, 1, 0], [1, 0, 0, 1], [0, 0, 1, 1]]
+    for cols in [(0, 2), (2, 4), (1, 3)]:
+        assert (io.read_tile(str(p), 4, 3, (0, 3), cols) == full[:, cols[0]:cols[1]]).all()
+
+
 def test_tile_writes_assemble_the_file(tmp_path, native):
     W, H = 70, 45
     g = random_grid(W, H, 5)
