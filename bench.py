@@ -6,13 +6,20 @@ scaling at 1/2/4/8 GPUs" - cell-updates/s = W * H * Generations / loop time,
 exactly as the reference times its generation loop (src/game.c:175-199,
 src/game_mpi.c:385-424, src/game_cuda.cu:219-279).
 
-One *step* = one generation of the full 32768^2 grid (B3/S23 on a torus,
-with the reference's termination checks - per-generation change flags fused
-into the kernel and polled every 256 generations - and the halo exchanges
-the decomposition needs).  Strong scaling: the grid is fixed, N GPUs split it
-into 1 x N row strips, one process per GPU, halos over RCCL/xGMI.
+One *step* = one run of the reference's benchmark unit: GEN_LIMIT = 1000
+generations of the full 32768^2 grid (--gens-per-step), B3/S23 on a torus
+with the reference's termination checks on (per-generation change flags
+fused into the kernel, polled every 256 generations and resolved exactly at
+the end of the step) and every halo exchange the decomposition needs.  Each
+step continues the same grid (a random 32768^2 soup never reaches a fixed
+point within the run; if it did, the step would stop there exactly as the
+reference does and `generations_timed` would say so).  `--steps K` times
+exactly K such runs after `--warmup W` untimed ones, bracketed by a barrier +
+device synchronisation on both sides; the slowest rank's time counts.
+Strong scaling: the grid is fixed, N GPUs split it into 1 x N row strips,
+one process per GPU, halos and flag reductions over RCCL/xGMI.
 
-    python bench.py                                   # 1 GPU, 1000 gens
+    python bench.py                                   # 1 GPU
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
 
@@ -43,8 +50,10 @@ def log(*a):
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000, help="timed generations")
-    ap.add_argument("--warmup", type=int, default=100, help="untimed generations")
+    ap.add_argument("--steps", type=int, default=20, help="timed steps (one step = --gens-per-step generations)")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed steps before the timed ones")
+    ap.add_argument("--gens-per-step", type=int, default=1000,
+                    help="generations per step: GEN_LIMIT of the reference's benchmark run (src/game.c:6)")
     ap.add_argument("--prewarm", type=int, default=8192,
                     help="extra untimed generations before the warmup: the GPU clock needs ~10 ms of load to ramp "
                          "(100 warmup gens = 1.3 ms left the first timed run 6%% slow, profiles/sweep_warmup.jsonl)")
@@ -88,9 +97,10 @@ def main() -> int:
 
     S = a.size
     Hg = a.height or S
-    total = a.prewarm + a.warmup + a.steps * a.repeats
+    gps = max(1, a.gens_per_step)
+    total = a.prewarm + (a.warmup + a.steps * a.repeats) * gps
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
-                     poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs)
+                     poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs, timing_barriers=False)
     sim = Simulation(cfg, transport=transport, backend=backend)
     eng = sim.native_engine
     sim.init_random(a.seed, 0.5)
@@ -102,23 +112,30 @@ def main() -> int:
             torch.cuda.synchronize()
         backend.synchronize()
 
-    if a.prewarm + a.warmup > 0:
-        eng.run_until(sim.generation + a.prewarm + a.warmup)
+    def step():
+        """One reference benchmark run: gps generations with termination checks."""
+        return eng.run_until(sim.generation + gps)
+
+    if a.prewarm > 0:
+        eng.run_until(sim.generation + a.prewarm)
+    for _ in range(a.warmup):
+        step()
     best = None
-    executed = a.steps
     for _ in range(a.repeats):
         sync()
         t0 = time.perf_counter()
-        r = eng.run_until(sim.generation + a.steps)
+        g0 = sim.generation
+        rs = [step() for _ in range(a.steps)]
         sync()
         dt = time.perf_counter() - t0
         dt = allreduce_max_float(dt)
-        executed = r.executed
+        executed = sim.generation - g0
         if best is None or dt < best[0]:
-            best = (dt, r)
-    dt, r = best
+            best = (dt, executed, rs)
+    dt, executed, rs = best
     gens = max(1, executed)
     value = float(S) * float(Hg) * gens / dt
+    stops = sorted({r.stop_reason for r in rs})
     desc = sim.describe()
     if rank == 0:
         rec = {
@@ -128,7 +145,7 @@ def main() -> int:
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": dt * 1e3 / gens,
+            "ms_per_step": dt * 1e3 / max(1, a.steps),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": value / BASELINE_VALUE,
@@ -145,14 +162,18 @@ def main() -> int:
                 "engine": backend.name(),
                 "tmax": desc["tmax"],
                 "epoch": desc["epoch"],
+                "gens_per_step": gps,
                 "generations_timed": gens,
+                "step_stop_reasons": stops,
                 "prewarm_generations": a.prewarm,
-                "loop_ms_engine": r.loop_ms,
-                "exchanges": r.exchanges,
-                "polls": r.polls,
-                "kernel_launches": r.kernel_launches,
-                "overlapped_halo_exchange": r.overlapped,
-                "graph_epochs": r.graph_launches,
+                "warmup_generations": a.warmup * gps,
+                "loop_ms_engine_per_step": sum(r.loop_ms for r in rs) / max(1, len(rs)),
+                "exchanges_per_step": rs[-1].exchanges if rs else 0,
+                "polls_per_step": rs[-1].polls if rs else 0,
+                "kernel_launches_per_step": rs[-1].kernel_launches if rs else 0,
+                "halo_bytes_per_step": rs[-1].halo_bytes if rs else 0,
+                "overlapped_halo_exchange": bool(rs and rs[-1].overlapped),
+                "graph_epochs": sum(r.graph_launches for r in rs),
                 "baseline": "8.9e8 cell-updates/s (best reference run in BASELINE.md: MPI, 4 ranks, 2048^2, CPU)",
             },
         }

@@ -54,6 +54,11 @@ struct EngineConfig {
   // Watchdog: fail (instead of hanging) when a termination poll waits on the
   // device longer than this many seconds (0: GOL_WATCHDOG_S or 900 s).
   double watchdog_s = 0;
+  // Bracket each run's generation loop with a transport barrier (plus a
+  // device sync) so loop_ms covers every rank's loop - the reference times
+  // rank 0 only, with no barrier (src/game_mpi.c:385-424).  A caller that
+  // brackets the run itself (bench.py) turns them off.
+  bool timing_barriers = true;
 };
 
 struct RunResult {

@@ -391,7 +391,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   const int64_t g0 = graph_runs_;
   const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_;
   trace::Range trace_run("gol.run");
-  tr_->barrier();
+  if (cfg_.timing_barriers) tr_->barrier();
   be_->synchronize();
   auto t0 = std::chrono::steady_clock::now();
 
@@ -450,7 +450,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   if (have_pending) poll_check(pending, &found);
   be_->synchronize();
   be_->check_device_errors();
-  tr_->barrier();
+  if (cfg_.timing_barriers) tr_->barrier();
   auto t1 = std::chrono::steady_clock::now();
   res.loop_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   res.executed = gen_ - start;

@@ -46,6 +46,7 @@ class LifeConfig:
     graphs: str = "off"         # auto | on | off: replay full epochs as captured HIP graphs
     start_gen: int = 0          # resume: generation number of the initial state
     sim_phase: int = 0          # resume: similarity counter at start_gen
+    timing_barriers: bool = True  # barrier + sync around each run's loop (off: the caller brackets it)
 
     def resolved_layout(self) -> str:
         if self.layout == "auto":
@@ -72,6 +73,7 @@ class LifeConfig:
         c.graphs = {"auto": -1, "off": 0, "on": 1}[self.graphs]
         c.start_gen = int(self.start_gen)
         c.sim_phase = int(self.sim_phase)
+        c.timing_barriers = bool(self.timing_barriers)
         return c
 
 

@@ -66,12 +66,19 @@ def test_torchrun_terminating_run(native, tmp_path):
 
 def test_bench_cpu_dry_run_two_ranks(native, tmp_path):
     r = _torchrun(2, [str(REPO / "bench.py"), "--gpus", "2", "--engine", "cpu", "--comm", "torch",
-                      "--size", "256", "--steps", "40", "--warmup", "8"], tmp_path)
+                      "--size", "256", "--steps", "3", "--warmup", "1", "--gens-per-step", "100",
+                      "--prewarm", "16"], tmp_path)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     import json
 
     rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 2 and rec["steps"] == 40 and rec["value"] > 0
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1 and rec["value"] > 0
     assert rec["higher_is_better"] is True and rec["scaling"] == "strong"
+    cfg = rec["config"]
+    # one step = one --gens-per-step run; exactly steps x that many timed
+    assert cfg["gens_per_step"] == 100 and cfg["generations_timed"] == 300
+    assert cfg["step_stop_reasons"] == ["limit"]
+    assert cfg["exchanges_per_step"] >= 1 and cfg["polls_per_step"] >= 1
+    assert abs(rec["value"] - 256 * 256 * 300 / (rec["ms_per_step"] * 3e-3)) < 1e-6 * rec["value"]
