@@ -46,7 +46,8 @@ def main() -> int:
             rec["wall_s"] = round(time.time() - t0, 2)
             f.write(json.dumps(rec) + "\n")
             f.flush()
-            print(f"{rec['value']:.4e}  {rec['ms_per_step']*1e3:8.2f} us/gen  {line}", flush=True)
+            gps = rec.get("config", {}).get("gens_per_step", 1)
+            print(f"{rec['value']:.4e}  {rec['ms_per_step'] * 1e3 / gps:8.3f} us/gen  {line}", flush=True)
     return 0
 
 
