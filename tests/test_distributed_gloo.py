@@ -34,7 +34,7 @@ def _torchrun(nproc: int, args: list[str], cwd: Path, timeout: int = 300) -> sub
 
 
 @pytest.mark.parametrize("nproc,decomp,layout", [(2, "1x2", "bits"), (2, "2x1", "u8"), (4, "2x2", "bits"),
-                                                 (3, "1x3", "u8")])
+                                                 (3, "1x3", "u8"), (8, "1x8", "bits"), (8, "2x4", "u8")])
 def test_torchrun_cli_matches_serial(native, tmp_path, nproc, decomp, layout):
     W, H = 128, 96
     g = random_grid(W, H, 31)
