@@ -76,6 +76,13 @@ struct RunResult {
   int64_t halo_bytes = 0;        // bytes this rank sent in halo exchanges
 };
 
+// The reference's "Generations:" value of a run over (start_gen, limit] whose
+// first unchanged generation is g_f = first_unchanged (-1: none), given
+// whether the grid at g_f is empty; *reason (optional) receives limit |
+// extinction | similarity | fixed_point.  Mirrored by utils/termination.py.
+int64_t reported_generations(int64_t first_unchanged, bool extinct, int64_t limit, int64_t start_gen,
+                             bool check_similarity, int sim_freq, int sim_phase, std::string* reason = nullptr);
+
 class Engine {
  public:
   Engine(const EngineConfig& cfg, Backend* backend, Transport* transport);

@@ -1,0 +1,112 @@
+#include "gol/checkpoint.hpp"
+
+#include <sys/stat.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+#include "gol/common.hpp"
+#include "gol/io.hpp"
+
+namespace gol {
+namespace {
+
+void mkdirs(const std::string& dir) {
+  std::string cur;
+  for (size_t i = 0; i <= dir.size(); ++i) {
+    if (i == dir.size() || dir[i] == '/') {
+      if (!cur.empty() && ::mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST)
+        fail("cannot create checkpoint directory '" + cur + "': " + std::strerror(errno));
+    }
+    if (i < dir.size()) cur += dir[i];
+  }
+}
+
+// Value text of "key": <value> in a flat JSON object (numbers, booleans,
+// strings); empty if the key is absent.
+std::string json_field(const std::string& js, const std::string& key) {
+  const std::string k = "\"" + key + "\"";
+  size_t p = js.find(k);
+  if (p == std::string::npos) return {};
+  p = js.find(':', p + k.size());
+  if (p == std::string::npos) return {};
+  ++p;
+  while (p < js.size() && (js[p] == ' ' || js[p] == '\n' || js[p] == '\t' || js[p] == '\r')) ++p;
+  if (p < js.size() && js[p] == '"') {
+    const size_t e = js.find('"', p + 1);
+    return e == std::string::npos ? std::string() : js.substr(p + 1, e - p - 1);
+  }
+  size_t e = p;
+  while (e < js.size() && js[e] != ',' && js[e] != '}' && js[e] != '\n') ++e;
+  std::string v = js.substr(p, e - p);
+  while (!v.empty() && (v.back() == ' ' || v.back() == '\r')) v.pop_back();
+  return v;
+}
+
+int64_t need_int(const std::string& js, const std::string& key, const std::string& dir) {
+  const std::string v = json_field(js, key);
+  char* end = nullptr;
+  const long long x = std::strtoll(v.c_str(), &end, 10);
+  if (v.empty() || end == v.c_str() || *end != '\0')
+    fail("checkpoint '" + dir + "': meta.json has no integer '" + key + "'");
+  return int64_t(x);
+}
+
+}  // namespace
+
+std::string checkpoint_grid_path(const std::string& dir) { return dir + "/grid.txt"; }
+
+void checkpoint_begin(const std::string& dir, int64_t W, int64_t H) {
+  mkdirs(dir);
+  create_text_file(checkpoint_grid_path(dir), W, H);
+}
+
+void checkpoint_commit(const std::string& dir, const CheckpointMeta& m) {
+  std::ostringstream o;
+  o << "{\n \"format\": \"" << kCheckpointFormat << "\",\n \"width\": " << m.W << ",\n \"height\": " << m.H
+    << ",\n \"generation\": " << m.generation << ",\n \"sim_phase\": " << m.sim_phase
+    << ",\n \"gen_limit\": " << m.gen_limit << ",\n \"check_similarity\": "
+    << (m.check_similarity ? "true" : "false") << ",\n \"sim_freq\": " << m.sim_freq << ",\n \"layout\": \""
+    << m.layout << "\"\n}";
+  const std::string tmp = dir + "/meta.json.tmp", fin = dir + "/meta.json";
+  {
+    std::ofstream f(tmp, std::ios::trunc);
+    if (!f) fail("cannot write checkpoint metadata '" + tmp + "'");
+    f << o.str();
+    if (!f.flush()) fail("cannot write checkpoint metadata '" + tmp + "'");
+  }
+  if (std::rename(tmp.c_str(), fin.c_str()) != 0)
+    fail("cannot publish checkpoint metadata '" + fin + "': " + std::strerror(errno));
+}
+
+CheckpointMeta checkpoint_load(const std::string& dir) {
+  std::ifstream f(dir + "/meta.json");
+  if (!f) fail("checkpoint '" + dir + "': no meta.json (incomplete or not a checkpoint)");
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const std::string js = ss.str();
+  const std::string fmt = json_field(js, "format");
+  if (fmt != kCheckpointFormat)
+    fail("checkpoint '" + dir + "': format '" + fmt + "', expected '" + kCheckpointFormat + "'");
+  CheckpointMeta m;
+  m.W = need_int(js, "width", dir);
+  m.H = need_int(js, "height", dir);
+  m.generation = need_int(js, "generation", dir);
+  m.sim_phase = int(need_int(js, "sim_phase", dir));
+  m.gen_limit = need_int(js, "gen_limit", dir);
+  m.sim_freq = int(need_int(js, "sim_freq", dir));
+  const std::string cs = json_field(js, "check_similarity");
+  GOL_REQUIRE(cs == "true" || cs == "false", "checkpoint '" + dir + "': bad check_similarity");
+  m.check_similarity = cs == "true";
+  const std::string lay = json_field(js, "layout");
+  if (!lay.empty()) m.layout = lay;
+  GOL_REQUIRE(m.W > 0 && m.H > 0 && m.sim_freq > 0 && m.generation >= 0,
+              "checkpoint '" + dir + "': inconsistent metadata");
+  return m;
+}
+
+}  // namespace gol

@@ -360,6 +360,37 @@ bool Engine::poll_check(Poll& p, int64_t* first_unchanged) {
   return false;
 }
 
+int64_t reported_generations(int64_t first_unchanged, bool extinct, int64_t limit, int64_t start_gen,
+                             bool check_similarity, int sim_freq, int sim_phase, std::string* reason) {
+  std::string why = "limit";
+  int64_t gens = limit;
+  if (first_unchanged >= 0 && first_unchanged <= limit) {
+    why = "fixed_point";
+    if (extinct) {
+      // G_{g_f - 1} is the first empty grid: the loop's emptiness test stops
+      // at the next iteration and reports g_f - 1 (src/game.c:177).
+      gens = first_unchanged - 1;
+      why = "extinction";
+    } else if (check_similarity) {
+      // Similarity checks happen at generations t > start_gen with
+      // (t - start_gen + sim_phase) % F == 0 (counter reset only on a failed
+      // check, src/game.c:181-189); the first one at or after g_f fires and
+      // reports t - 1 (the break skips generation++).  The phase is anchored
+      // at the configured start generation, so an earlier advance() or
+      // run_until() on the same engine does not shift it.
+      const int64_t F = sim_freq;
+      const int64_t k = first_unchanged - start_gen + sim_phase;
+      const int64_t tsim = first_unchanged + ((F - (k % F)) % F);
+      if (tsim <= limit) {
+        gens = tsim - 1;
+        why = "similarity";
+      }
+    }
+  }
+  if (reason) *reason = why;
+  return gens;
+}
+
 RunResult Engine::run() { return run_impl(cfg_.gen_limit, /*stop_early=*/true); }
 
 RunResult Engine::run_until(int64_t limit) {
@@ -467,29 +498,9 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     if (tr_->size() > 1) tr_->allreduce_max_u32(alive_dev_, 1, be_->stream());
     uint32_t alive = 0;
     be_->copy_d2h(&alive, alive_dev_, 4);
-    if (!alive) {
-      res.extinct = true;
-      res.generations = found - 1;
-      res.stop_reason = "extinction";
-    } else if (cfg_.check_similarity) {
-      // Similarity checks happen at generations t > start_gen with
-      // (t - start_gen + sim_phase) % F == 0 (counter reset only on a failed
-      // check, src/game.c:181-189).  The phase is anchored at the configured
-      // start generation, not at this call's first generation: an earlier
-      // advance()/run_until() on the same engine does not shift it
-      // (utils/termination.py:reported_generations).
-      const int64_t F = cfg_.sim_freq;
-      int64_t k = found - cfg_.start_gen + cfg_.sim_phase;
-      int64_t tsim = found + ((F - (k % F)) % F);
-      if (tsim <= limit) {
-        res.generations = tsim - 1;
-        res.stop_reason = "similarity";
-      } else {
-        res.stop_reason = "fixed_point";
-      }
-    } else {
-      res.stop_reason = "fixed_point";
-    }
+    res.extinct = !alive;
+    res.generations = reported_generations(found, res.extinct, limit, cfg_.start_gen, cfg_.check_similarity,
+                                           cfg_.sim_freq, cfg_.sim_phase, &res.stop_reason);
   }
   return res;
 }

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "gol/backend.hpp"
+#include "gol/checkpoint.hpp"
 #include "gol/cpu_ref.hpp"
 #include "gol/engine.hpp"
 #include "gol/io.hpp"
@@ -50,6 +51,12 @@ struct Options {
   double density = 0.5;
   int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0, overlap = -1, graphs = 0;
   bool show = false;
+  int64_t checkpoint_every = 0;     // generations between checkpoints (0: none)
+  int64_t start_gen = 0;            // resume: generation of the loaded grid
+  int sim_phase = 0;                // resume: similarity counter at start_gen
+  std::string checkpoint_dir;       // where they go
+  std::string resume;               // checkpoint directory to resume from
+  bool gens_set = false, sim_set = false;
 };
 
 [[noreturn]] void usage(int code) {
@@ -74,6 +81,10 @@ struct Options {
                "  --style serial|mpi|async|collective|openmp|cuda\n"
                "                              stdout format and output name of that reference build\n"
                "  --metrics-json PATH         write run metrics as JSON\n"
+               "  --checkpoint-every K        write a checkpoint every K generations ...\n"
+               "  --checkpoint-dir DIR        ... into DIR (grid.txt + meta.json)\n"
+               "  --resume DIR                continue from a checkpoint: same final grid and\n"
+               "                              Generations line as the uninterrupted run\n"
                "  --show                      print the final grid with VT100 escapes\n");
   std::exit(code);
 }
@@ -92,9 +103,12 @@ Options parse(int argc, char** argv) {
     else if (a == "--layout") o.layout = next();
     else if (a == "--decomp") o.decomp = next();
     else if (a == "--comm") o.comm = next();
-    else if (a == "--gens") o.gens = std::atoll(next().c_str());
-    else if (a == "--sim-freq") o.sim_freq = std::atoi(next().c_str());
-    else if (a == "--no-similarity") o.similarity = false;
+    else if (a == "--gens") o.gens = std::atoll(next().c_str()), o.gens_set = true;
+    else if (a == "--sim-freq") o.sim_freq = std::atoi(next().c_str()), o.sim_set = true;
+    else if (a == "--no-similarity") o.similarity = false, o.sim_set = true;
+    else if (a == "--checkpoint-every") o.checkpoint_every = std::atoll(next().c_str());
+    else if (a == "--checkpoint-dir") o.checkpoint_dir = next();
+    else if (a == "--resume") o.resume = next();
     else if (a == "--output") o.output = next();
     else if (a == "--style") o.style = next();
     else if (a == "--metrics-json") o.metrics = next();
@@ -126,6 +140,25 @@ Options parse(int argc, char** argv) {
   if (pos.size() > 0) o.W = std::atoll(pos[0].c_str());
   if (pos.size() > 1) o.H = std::atoll(pos[1].c_str());
   if (pos.size() > 2) o.input = pos[2];
+  if (!o.resume.empty()) {
+    // The checkpoint fixes the grid and the counters; --gens / --sim-freq /
+    // --no-similarity given on the command line still win.
+    const CheckpointMeta m = checkpoint_load(o.resume);
+    if ((o.W > 0 && o.W != m.W) || (o.H > 0 && o.H != m.H))
+      throw Error("--resume: checkpoint is " + std::to_string(m.W) + "x" + std::to_string(m.H) +
+                  ", not the requested " + std::to_string(o.W) + "x" + std::to_string(o.H));
+    o.W = m.W;
+    o.H = m.H;
+    o.input = checkpoint_grid_path(o.resume);
+    if (!o.gens_set) o.gens = m.gen_limit;
+    if (!o.sim_set) {
+      o.similarity = m.check_similarity;
+      o.sim_freq = m.sim_freq;
+    }
+    o.start_gen = m.generation;
+    o.sim_phase = m.sim_phase;
+    if (o.layout == "auto" && (m.layout == "bits" || m.layout == "u8")) o.layout = m.layout;
+  }
   if (o.W <= 0) o.W = 30;
   if (o.H <= 0) o.H = 30;
   if (o.gpus > 0) o.ranks = o.gpus;
@@ -169,6 +202,8 @@ int run(const Options& o) {
   std::vector<uint8_t> final_grid;
   const bool want_grid = o.output != "none" || o.show;
 
+  if (engine == "ref" && (!o.resume.empty() || o.checkpoint_every > 0))
+    throw Error("--engine ref is the plain serial loop from generation 0: no checkpoint / resume");
   if (engine == "ref") {
     // Exact serial semantics (src/game.c), every generation evaluated eagerly.
     auto t0 = std::chrono::steady_clock::now();
@@ -207,6 +242,8 @@ int run(const Options& o) {
     cfg.poll_gens = o.poll;
     cfg.overlap = o.overlap;
     cfg.graphs = o.graphs;
+    cfg.start_gen = o.start_gen;
+    cfg.sim_phase = o.sim_phase;
     int ndev = 1;
     if (engine == "hip") {
       GOL_REQUIRE(hip_available(), "--engine hip: no HIP device available");
@@ -260,10 +297,53 @@ int run(const Options& o) {
       }
     });
     read_ms = ms_since(t0);
+    // Generation loop, in chunks of --checkpoint-every generations when
+    // checkpointing (each chunk ends with every rank's tile on disk).
     std::vector<RunResult> results(P);
-    par([&](int r) { results[r] = engines[r]->run(); });
-    res = results[0];
-    for (auto& rr : results) res.loop_ms = std::max(res.loop_ms, rr.loop_ms);
+    RunResult total;
+    const int64_t limit = o.gens;
+    for (;;) {
+      const int64_t gen = engines[0]->generation();
+      const int64_t target = o.checkpoint_every > 0 ? std::min(limit, gen + o.checkpoint_every) : limit;
+      par([&](int r) { results[r] = engines[r]->run_until(target); });
+      double ms = 0;
+      for (auto& rr : results) ms = std::max(ms, rr.loop_ms);
+      total.loop_ms += ms;
+      total.executed += results[0].executed;
+      total.exchanges += results[0].exchanges;
+      total.polls += results[0].polls;
+      total.kernel_launches += results[0].kernel_launches;
+      const RunResult& last = results[0];
+      if (last.first_unchanged >= 0 || engines[0]->generation() >= limit) {
+        total.first_unchanged = last.first_unchanged;
+        total.extinct = last.extinct;
+        total.generations = reported_generations(last.first_unchanged, last.extinct, limit, o.start_gen,
+                                                 o.similarity, o.sim_freq, o.sim_phase, &total.stop_reason);
+        break;
+      }
+      if (!o.checkpoint_dir.empty()) {
+        const int64_t g = engines[0]->generation();
+        checkpoint_begin(o.checkpoint_dir, o.W, o.H);
+        par([&](int r) {
+          Engine& e = *engines[r];
+          std::vector<uint8_t> tile(size_t(e.rows().size() * e.cols().size()));
+          e.store_cells(tile.data(), e.cols().size(), false);
+          write_text_tile(checkpoint_grid_path(o.checkpoint_dir), o.W, o.H, e.rows(), e.cols(), tile.data(),
+                          e.cols().size());
+        });
+        CheckpointMeta m;
+        m.W = o.W;
+        m.H = o.H;
+        m.generation = g;
+        m.sim_phase = sim_phase_at(g, o.start_gen, o.sim_phase, o.sim_freq);
+        m.gen_limit = limit;
+        m.check_similarity = o.similarity;
+        m.sim_freq = o.sim_freq;
+        m.layout = layout_name(layout);
+        checkpoint_commit(o.checkpoint_dir, m);
+      }
+    }
+    res = total;
 
     if (want_grid) {
       auto t1 = std::chrono::steady_clock::now();

@@ -30,7 +30,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("GOL_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/transport.cpp",
-             "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp"]
+             "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp"]
 LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "u8_w1_dpp",
                  "u8_w1_carry"]
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",

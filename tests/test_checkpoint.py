@@ -85,3 +85,65 @@ def test_checkpoint_grid_is_a_valid_reference_input(native, tmp_path):
     d = save_checkpoint(sim, str(tmp_path / "ck"))
     text = (d / "grid.txt").read_text()
     assert text == io.format_text(np.asarray(sim.tile()))
+
+
+def _bin(gol_bin, args, cwd):
+    r = subprocess.run([str(gol_bin), *map(str, args)], cwd=cwd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+@pytest.mark.parametrize("W,H,seed,density", CONVERGING[:4])
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_native_cli_checkpoint_resume_is_exact(gol_bin, tmp_path, W, H, seed, density, ranks):
+    """bin/gol --checkpoint-every / --resume (C++): a run stopped at its last
+    checkpoint and resumed ends with the uninterrupted run's grid and
+    Generations line, at a checkpoint generation off the similarity period."""
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    assert rgens < 1000
+    inp = tmp_path / "in.txt"
+    io.write_grid(str(inp), g)
+    ck = tmp_path / "ck"
+    every = max(1, rgens // 2 - 1)
+    full = _bin(gol_bin, [W, H, inp, "--engine", "cpu", "--ranks", ranks, "--checkpoint-every", every,
+                          "--checkpoint-dir", ck, "--output", tmp_path / "full.out"], tmp_path)
+    assert _gens(full) == rgens
+    assert (io.read_grid(str(tmp_path / "full.out"), W, H) == ref).all()
+    meta = json.loads((ck / "meta.json").read_text())
+    assert meta["generation"] % every == 0 and 0 < meta["generation"] < rgens + 3
+    res = _bin(gol_bin, ["--resume", ck, "--engine", "cpu", "--ranks", ranks, "--output", tmp_path / "res.out"],
+               tmp_path)
+    assert _gens(res) == rgens
+    assert (io.read_grid(str(tmp_path / "res.out"), W, H) == ref).all()
+
+
+def test_native_and_python_checkpoints_interoperate(gol_bin, native, tmp_path):
+    W, H, seed, density = CONVERGING[0]
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    # Python writes at generation 7, the C++ CLI resumes it.
+    sim = Simulation(LifeConfig(W, H), engine="cpu")
+    sim.load(g)
+    sim.advance(7)
+    save_checkpoint(sim, str(tmp_path / "py"))
+    out = _bin(gol_bin, ["--resume", tmp_path / "py", "--engine", "cpu", "--output", tmp_path / "a.out"], tmp_path)
+    assert _gens(out) == rgens and (io.read_grid(str(tmp_path / "a.out"), W, H) == ref).all()
+    # The C++ CLI writes one, Python resumes it.
+    _bin(gol_bin, [W, H, "--random", f"{seed}:{density}", "--engine", "cpu", "--gens", 11, "--checkpoint-every", 5,
+                   "--checkpoint-dir", tmp_path / "cc", "--output", "none"], tmp_path)
+    cfg, grid = load_checkpoint(str(tmp_path / "cc"), gen_limit=1000)
+    assert cfg.start_gen == 10
+    sim2 = Simulation(cfg, engine="cpu")
+    sim2.load(io.read_grid(str(grid), W, H))
+    rep = sim2.run()
+    assert rep.generations == rgens and (sim2.tile() == ref).all()
+
+
+def test_native_resume_rejects_a_missing_or_foreign_checkpoint(gol_bin, tmp_path):
+    r = subprocess.run([str(gol_bin), "--resume", str(tmp_path / "nope")], capture_output=True, text=True)
+    assert r.returncode != 0 and "meta.json" in r.stderr
+    (tmp_path / "bad").mkdir()
+    (tmp_path / "bad" / "meta.json").write_text('{"format": "something-else"}')
+    r = subprocess.run([str(gol_bin), "--resume", str(tmp_path / "bad")], capture_output=True, text=True)
+    assert r.returncode != 0 and "format" in r.stderr
