@@ -3,7 +3,7 @@
 set -euo pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-ARGS=${BENCH_ARGS:-"--steps 1000 --warmup 100"}
+ARGS=${BENCH_ARGS:-"--steps 20 --warmup 2"}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py $ARGS > gpurun_out/prof/bench_trace.json 2> gpurun_out/prof/bench_trace.err
 echo "trace ok"
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/prof/pmc1 -o run -- python3 bench.py $ARGS > gpurun_out/prof/bench_pmc1.json 2> gpurun_out/prof/bench_pmc1.err
