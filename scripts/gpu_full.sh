@@ -13,5 +13,5 @@ timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.er
 cat gpurun_out/bench.json
 BENCH_ARGS="--steps 500 --warmup 50" bash scripts/profile_bench.sh
 mv gpurun_out/prof gpurun_out/prof_full
-BENCH_ARGS="--steps 1000 --warmup 100 --size 32768 --height 4096" bash scripts/profile_bench.sh
+BENCH_ARGS="--steps 20 --warmup 2 --size 32768 --height 4096" bash scripts/profile_bench.sh
 mv gpurun_out/prof gpurun_out/prof_tile

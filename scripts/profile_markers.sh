@@ -9,7 +9,7 @@ for cfg in "full:--size 32768" "tile:--size 32768 --height 4096"; do
   name=${cfg%%:*}
   args=${cfg#*:}
   timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv \
-    -d gpurun_out/mk/$name -o run -- python3 bench.py --steps 1000 --warmup 100 $args \
+    -d gpurun_out/mk/$name -o run -- python3 bench.py --steps 20 --warmup 2 $args \
     > gpurun_out/mk/$name.json 2> gpurun_out/mk/$name.err
   echo "$name ok"
 done
