@@ -3,7 +3,7 @@
 # it and install ./a.out as a thin wrapper that selects the matching style.
 #
 #   make            build the native module and CLI tools (gfx950)
-#   make serial     ./a.out W H file  ->  bin/gol --style serial (CPU oracle engine is --engine ref)
+#   make serial | game   ./a.out W H file  ->  bin/gol --style serial (CPU oracle engine is --engine ref)
 #   make mpi | async | collective | openmp | cuda   (same engine, that variant's stdout lines)
 #   make cmake      CMake build into build/cmake
 #   make test       CPU test tier;  make test-gpu  MI355X tier
@@ -12,7 +12,7 @@
 PYTHON ?= python3
 JOBS ?= 8
 
-.PHONY: all build serial mpi async collective openmp cuda cmake test test-gpu bench selftest-asan selftest-tsan clean
+.PHONY: all build game serial mpi async collective openmp cuda cmake test test-gpu bench selftest-asan selftest-tsan clean
 
 all: build
 
@@ -27,6 +27,7 @@ endef
 
 serial: build
 	$(call AOUT,serial,)
+game: serial  # the reference's target name for the serial build (Makefile:12-13)
 mpi: build
 	$(call AOUT,mpi,)
 async: build
