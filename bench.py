@@ -160,6 +160,7 @@ def main() -> int:
                 "grid": f"{S}x{Hg}",
                 "layout": a.layout,
                 "engine": backend.name(),
+                "kernel": desc["kernel"],
                 "tmax": desc["tmax"],
                 "epoch": desc["epoch"],
                 "gens_per_step": gps,

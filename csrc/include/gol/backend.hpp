@@ -63,14 +63,31 @@ class Backend {
   virtual void* stream_mark(void* /*from*/) { return nullptr; }
   virtual void stream_wait(void* /*on*/, void* /*mark*/) {}
 
-  // Kernels.
-  virtual void run_block(const BlockArgs& a) = 0;
+  // Kernels.  run_block returns the drift of the stored frame in cells
+  // (BlockArgs::allow_drift): the output's column x holds the cell the input
+  // frame had at x - drift.
+  virtual int run_block(const BlockArgs& a) = 0;
+  // Whether run_block may drift the frame for this layout when allowed
+  // (the engine then sizes the left halo for the one-sided light cone).
+  virtual bool drifts(Layout) const { return false; }
+  // Owned rows of src rotated left by `shift` cells (0 < shift < W) into dst:
+  // dst cell x = src cell (x + shift) mod W.  Halos of dst are not written.
+  virtual void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) = 0;
   // Throws if a kernel enqueued so far reported an error through the
   // backend's device-visible error word (call after the work completed).
   virtual void check_device_errors() {}
   // Largest temporal block size (generations per run_block) the backend runs
   // at full occupancy for this layout; the engine's default tmax.
   virtual int preferred_tmax(Layout) const { return 16; }
+  // Kernel family for a rows x cols tile: the temporal block size (tmax_req
+  // > 0: the caller's) and whether blocks may drift the frame (drifts()).
+  struct KernelChoice {
+    int tmax = 16;
+    bool drift = false;
+  };
+  virtual KernelChoice choose_kernel(Layout l, int64_t /*rows*/, int64_t /*cols*/, int tmax_req) const {
+    return {tmax_req > 0 ? tmax_req : preferred_tmax(l), drifts(l)};
+  }
   // Periodic self-fill of halo regions of a single tile (any tile size):
   // columns (left/right halo words of owned rows) and/or rows (full padded
   // rows of the top/bottom halo, which also fills the corners).
@@ -91,7 +108,10 @@ class Backend {
                            int64_t grow0, int64_t gcol0) = 0;
 };
 
-std::unique_ptr<Backend> make_cpu_backend(int threads);
+// drift: emulate the drifting frame of the HIP adder window (each block's
+// output shifted right by T cells), so the engine's drift bookkeeping is
+// testable on the CPU; GOL_CPU_DRIFT=1 turns it on for default backends.
+std::unique_ptr<Backend> make_cpu_backend(int threads, int drift = -1);
 // Defined in backend_hip.hip; throws if no device or the kernels are missing.
 std::unique_ptr<Backend> make_hip_backend(int device);
 bool hip_available();

@@ -104,6 +104,14 @@ class Engine {
   void set_generation(int64_t g) { gen_ = g; }
   Backend* backend() const { return be_; }
   void* current_buffer() const { return buf_[cur_]; }
+  // Storage-frame drift (cells, mod W) left by drifting kernels
+  // (Backend::drifts): stored column x holds true column x - drift.
+  int64_t drift() const { return drift_; }
+  // Whether temporal blocks may run the drifting (adder-window) kernel.
+  bool drifting() const { return drift_ok_; }
+  // Rotates the drift out of the current buffer (owned rows); every
+  // read-out (store_cells) does this first.
+  void normalize();
 
   // State I/O.  `cells` is this rank's owned tile (rows() x cols()).
   void load_cells(const uint8_t* cells, int64_t ld);
@@ -137,9 +145,10 @@ class Engine {
   Poll poll_issue(int64_t from, int64_t to);
   bool poll_check(Poll& p, int64_t* first_unchanged);
   int pick_T(int64_t remaining) const;
-  // One temporal block in <in> -> <out> for generations (gen_base, gen_base+T].
-  void launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
-              int64_t gen_base);
+  // One temporal block in <in> -> <out> for generations (gen_base, gen_base+T];
+  // returns the frame drift of the launch (cells).
+  int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base);
+  void add_drift(int64_t cells);
   void exchange_columns(void* buf);
   // d generations (d <= D_) with the row exchange overlapped (see engine.cpp).
   void epoch_overlapped(int64_t d);
@@ -175,6 +184,9 @@ class Engine {
   void* edge_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [top|bottom][parity]
   int64_t gen_ = 0;
   int64_t exchanges_ = 0, polls_ = 0, launches_ = 0;
+  bool drift_ok_ = false;   // whole-width tile of 32-cell words on a drifting backend
+  int64_t drift_ = 0;
+  int64_t graph_drift_[2] = {0, 0};
 };
 
 }  // namespace gol

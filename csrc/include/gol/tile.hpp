@@ -73,6 +73,11 @@ struct BlockArgs {
   // generation; gen_base / flags_base are then ignored for addressing.
   const int64_t* gen_dev = nullptr;
   int64_t gen_rel = 0;
+  // The backend may run a kernel that stores generation t+1's cell x-1 at
+  // column x (one-sided window, no cross-lane ops): the stored frame then
+  // drifts right by T cells, which run_block reports.  Only valid when the
+  // tile is the whole torus width (the drift is a relabeling of columns).
+  bool allow_drift = false;
 };
 
 }  // namespace gol

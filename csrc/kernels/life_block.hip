@@ -23,13 +23,15 @@ namespace {
 
 // Cross-lane primitive actually compiled for (layout, words per lane).
 int xlane_of(Layout layout, int w, const LifeTuning& tune) {
+  if ((tune.xlane == kXlaneAdd || tune.xlane == kXlaneAuto) && w == 1) return tune.xlane;
   if (tune.xlane == kXlaneCarry) return kXlaneCarry;
   if (tune.xlane == kXlaneBpermute && layout == Layout::Bits && w == 1) return kXlaneBpermute;
   return kXlaneDpp;
 }
 
 const char* xlane_name(int x) {
-  return x == kXlaneCarry ? "carry" : x == kXlaneBpermute ? "bpermute" : "dpp";
+  return x == kXlaneAuto ? "auto(add|dpp)" : x == kXlaneAdd ? "add" : x == kXlaneCarry ? "carry"
+         : x == kXlaneBpermute ? "bpermute" : "dpp";
 }
 
 }  // namespace
@@ -51,7 +53,7 @@ int life_block_max_T(Layout layout, const LifeTuning& tune) {
   return words_per_lane(layout, tune) >= 2 ? 8 : 16;
 }
 
-void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream) {
+int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream) {
   const TileGeom& g = a.g;
   GOL_REQUIRE(a.row_lo - a.T >= 0 && a.row_hi + a.T <= g.R() && a.row_lo < a.row_hi,
               "life_block: row range outside the tile");
@@ -83,10 +85,21 @@ void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t s
   p.wg_trace = tune.wg_trace;
   p.err = tune.err;
   const int64_t rows = a.row_hi - a.row_lo;
-  const int x = xlane_of(g.layout, w, tune);
+  int x = xlane_of(g.layout, w, tune);
   if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {
     launch_life_step_lds(a, tune.lds_rows, stream);
-  } else if (g.layout == Layout::U8) {
+    return 0;
+  }
+  // The adder window drifts the storage frame by T cells (see kXlaneAdd); the
+  // engine allows that only for whole-width tiles of 32-cell words, and the
+  // left halo must hold the 2T cells its one-sided light cone consumes.
+  if (x == kXlaneAuto) x = kXlaneAdd;  // the engine decided through allow_drift
+  if (x == kXlaneAdd && !(a.allow_drift && 32 * g.hw >= 2 * a.T)) x = kXlaneDpp;
+  if (x == kXlaneAdd) {
+    (g.layout == Layout::U8 ? launch_u8_w1_add : launch_bits_w1_add)(p, rows, a.T, tune, stream);
+    return a.T;
+  }
+  if (g.layout == Layout::U8) {
     (x == kXlaneCarry ? launch_u8_w1_carry : launch_u8_w1_dpp)(p, rows, a.T, tune, stream);
   } else if (w == 2) {
     (x == kXlaneCarry ? launch_bits_w2_carry : launch_bits_w2_dpp)(p, rows, a.T, tune, stream);
@@ -94,6 +107,7 @@ void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t s
     (x == kXlaneCarry ? launch_bits_w1_carry
                       : x == kXlaneBpermute ? launch_bits_w1_bperm : launch_bits_w1_dpp)(p, rows, a.T, tune, stream);
   }
+  return 0;
 }
 
 }  // namespace hipk

@@ -102,9 +102,56 @@ __device__ __forceinline__ uint32_t left_in_carry(uint32_t first, uint32_t last)
   return l;
 }
 
-// Horizontal 3-sums (h1:h0) = left + centre + right for every word.
+// Words produced per wave, and which lane words are the wave's halo: the
+// symmetric windows need one halo word per side; the one-sided adder window
+// (kXlaneAdd) reads nothing to its right, so only lane 0 is a halo.
 template <int XL, int W>
-__device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1) {
+constexpr int wave_out_words() {
+  return XL == kXlaneAdd ? 64 * W - 1 : 64 * W - 2;
+}
+template <int XL, int W>
+__device__ __forceinline__ bool wave_halo(int lane, int i) {
+  return (lane == 0 && i == 0) || (XL != kXlaneAdd && lane == 63 && i == W - 1);
+}
+
+// One-sided window for the adder mode: l1 = cells x-1, l2 = cells x-2 at bit
+// x.  v_add_co_u32 doubles a word (shift left by one) and leaves every lane's
+// top bit in an SGPR-pair lane mask; s_lshl_b64 moves each mask bit one lane
+// up; v_addc_co_u32 adds it back in as bit 0.  All VALU ops here issue at the
+// full v_bitop3 rate (csrc/tools/ubench_dpp_mix.hip), unlike DPP/v_alignbit.
+__device__ __forceinline__ void adder_window(uint32_t c, uint32_t& l1, uint32_t& l2) {
+  // One block so the pair of lane masks never outlives the window (no SGPR
+  // pressure across levels); s_nop 0 where gfx950 wants a wait state between
+  // a carry-writing VALU op and a read of its VGPR result.
+  uint32_t t1;
+  uint64_t m1, m2;
+  asm("v_add_co_u32_e64 %[t1], %[m1], %[c], %[c]\n\t"    // c << 1; carry = bit 31
+      "s_lshl_b64 %[m1], %[m1], 1\n\t"                    // lane j <- lane j-1
+      "v_add_co_u32_e64 %[l2], %[m2], %[t1], %[t1]\n\t"   // carry = bit 30
+      "v_addc_co_u32_e64 %[l1], %[m1], %[t1], 0, %[m1]\n\t"
+      "s_lshl_b64 %[m2], %[m2], 1\n\t"
+      "v_addc_co_u32_e64 %[l2], %[m2], %[l1], %[l1], %[m2]\n\t"
+      "s_nop 0"
+      : [l1] "=&v"(l1), [l2] "=&v"(l2), [t1] "=&v"(t1), [m1] "=&s"(m1), [m2] "=&s"(m2)
+      : [c] "v"(c)
+      : "scc");
+}
+
+// Horizontal 3-sums (h1:h0) = left + centre + right for every word, and the
+// word of the cells the rule treats as centre (the input word itself, or for
+// the one-sided adder window the word shifted by one cell, ctr = x-1).
+template <int XL, int W>
+__device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1, Vec<W>& ctr) {
+  if constexpr (XL == kXlaneAdd) {
+    static_assert(W == 1, "adder window: one word per lane");
+    uint32_t l1, l2;
+    adder_window(c.w[0], l1, l2);
+    h0.w[0] = bop3<tt::XOR3>(l2, l1, c.w[0]);
+    h1.w[0] = bop3<tt::MAJ>(l2, l1, c.w[0]);
+    ctr.w[0] = l1;
+    return;
+  }
+  ctr = c;
   uint32_t lw = 0, rw;
   if constexpr (XL == kXlaneCarry) {
     rw = __builtin_amdgcn_mov_dpp(c.w[0], 0x130, 0xF, 0xF, true);  // wave_shl:1
@@ -261,8 +308,8 @@ struct Levels {
 template <int T, class IO, int S, int L, int W = IO::W>
 __device__ __forceinline__ Vec<W> level_full(Levels<T, W>& st, const Vec<W>& cur) {
   constexpr int s1 = (S + 1) % 3, s2 = (S + 2) % 3;
-  Vec<W> h0, h1, nxt;
-  hsum<IO::XL>(cur, h0, h1);
+  Vec<W> h0, h1, nxt, c;
+  hsum<IO::XL>(cur, h0, h1, c);
 #pragma unroll
   for (int i = 0; i < W; ++i) {
     const uint32_t ctr = st.cc[L][s2].w[i];
@@ -276,18 +323,18 @@ __device__ __forceinline__ Vec<W> level_full(Levels<T, W>& st, const Vec<W>& cur
   }
   st.h0[L][S] = h0;
   st.h1[L][S] = h1;
-  st.cc[L][S] = cur;
+  st.cc[L][S] = c;
   return nxt;
 }
 
 // Window fill only (the level's output row would still be invalid).
 template <int T, class IO, int S, int L, int W = IO::W>
 __device__ __forceinline__ void level_store(Levels<T, W>& st, const Vec<W>& cur) {
-  Vec<W> h0, h1;
-  hsum<IO::XL>(cur, h0, h1);
+  Vec<W> h0, h1, c;
+  hsum<IO::XL>(cur, h0, h1, c);
   st.h0[L][S] = h0;
   st.h1[L][S] = h1;
-  st.cc[L][S] = cur;
+  st.cc[L][S] = c;
 }
 
 template <int T, class IO, int S, int L, int LEND, int W = IO::W>
@@ -487,7 +534,7 @@ template <int T, class IO, bool SKEW, bool SPLIT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<T, IO, SKEW, SPLIT>())))
 void life_block_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
-  constexpr int kWaveOut = 64 * W - 2;  // words produced per wave
+  constexpr int kWaveOut = wave_out_words<IO::XL, W>();  // words produced per wave
   const int lane = threadIdx.x & 63;
   // readfirstlane: the wave index is uniform, so everything derived from it
   // (segment bounds, loop trip counts) lives in SGPRs with scalar branches.
@@ -514,7 +561,7 @@ void life_block_kernel(const LifeBlockParams p) {
   for (int i = 0; i < W; ++i) {
     const int c = col + i;
     const bool ok = c >= 0 && c < p.Wp;
-    const bool halo = (lane == 0 && i == 0) || (lane == 63 && i == W - 1);
+    const bool halo = wave_halo<IO::XL, W>(lane, i);
     rd.ok[i] = ok;
     wr.own[i] = ok && !halo;
     fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
@@ -655,12 +702,13 @@ __device__ __forceinline__ void down_level(const DownCtx<T, IO>& ctx, const Writ
   // > 256 VGPRs at T = 16).  sched_barrier every 8 rows stops the max-ILP
   // scheduler from hoisting every row's DPP shifts to the top of the level.
   Rows<N + 2, W> nxt;  // level L+1 rows [b-L-3, b+L+3); inner N-2 computed
-  Vec<W> ha0, ha1, hb0, hb1, hc0, hc1;
-  hsum<IO::XL>(cur.r[0], ha0, ha1);
-  hsum<IO::XL>(cur.r[1], hb0, hb1);
+  static_assert(IO::XL != kXlaneAdd, "split schedule: symmetric windows only");
+  Vec<W> ha0, ha1, hb0, hb1, hc0, hc1, cdummy;
+  hsum<IO::XL>(cur.r[0], ha0, ha1, cdummy);
+  hsum<IO::XL>(cur.r[1], hb0, hb1, cdummy);
 #pragma unroll
   for (int q = 0; q < N - 2; ++q) {
-    hsum<IO::XL>(cur.r[q + 2], hc0, hc1);
+    hsum<IO::XL>(cur.r[q + 2], hc0, hc1, cdummy);
 #pragma unroll
     for (int i = 0; i < W; ++i) {
       const uint32_t ctr = cur.r[q + 1].w[i];
@@ -690,7 +738,7 @@ template <int T, class IO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void life_split_down_kernel(
     const LifeBlockParams p) {
   constexpr int W = IO::W;
-  constexpr int kWaveOut = 64 * W - 2;
+  constexpr int kWaveOut = wave_out_words<IO::XL, W>();
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nb = p.nseg - 1;
@@ -708,7 +756,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void l
   for (int i = 0; i < W; ++i) {
     const int c = col + i;
     const bool ok = c >= 0 && c < p.Wp;
-    const bool halo = (lane == 0 && i == 0) || (lane == 63 && i == W - 1);
+    const bool halo = wave_halo<IO::XL, W>(lane, i);
     ctx.ok[i] = ok;
     ctx.off[i] = min(max(c, 0), p.Wp - 1);
     wr.own[i] = ok && !halo;
@@ -762,8 +810,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void l
 // prefers 1020 or 2040 waves there.)
 // Returns whether the skewed schedule applies (every segment >= T rows);
 // *cost_out (optional) receives the model's score of the chosen plan.
+// Relative time per level body of a SIMD holding k resident waves (k = 1..4),
+// per kernel family.  DPP/alignbit windows (csrc/tools/ubench_level.hip):
+// ~1.2x slower with one wave, flat from two.  The adder window issues two
+// extra SALU shifts per body and only reaches its rate with four waves per
+// SIMD (bench: 32768 x 16384 tile at T = 12, 2.5 / 3 / 4 waves per SIMD =
+// 8.05 / 7.35 / 5.86 ms per 1000 generations), so its planner aims there.
+inline double issue_factor(int xl, int64_t k) {
+  static constexpr double kSym[] = {0, 1.2, 1.0, 0.97, 0.95};
+  static constexpr double kAdd[] = {0, 2.0, 1.45, 1.25, 1.0};
+  const int64_t i = std::min<int64_t>(std::max<int64_t>(k, 1), 4);
+  return xl == kXlaneAdd ? kAdd[i] : kSym[i];
+}
+
 inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int simds, int occ, int min_seg,
-                 int target_waves, double overhead_rows = -1, double* cost_out = nullptr) {
+                 int target_waves, double overhead_rows = -1, double* cost_out = nullptr, int xl = kXlaneDpp) {
   if (overhead_rows < 0) overhead_rows = 0.5 * T + 2;
   const int64_t smin = std::max<int64_t>({int64_t(min_seg), 2 * int64_t(T), 1});
   const int64_t max_nseg = std::max<int64_t>(1, out_rows / smin);
@@ -772,14 +833,13 @@ inline bool plan(LifeBlockParams& p, int T, int64_t out_rows, int simds, int occ
   if (target_waves > 0) {
     best_n = std::min<int64_t>(max_nseg, std::max<int64_t>(1, target_waves / std::max(1, p.ncolw)));
   } else {
-    static constexpr double kT[] = {0, 1.2, 1.0, 0.97, 0.95};
     for (int64_t n = 1; n <= max_nseg; ++n) {
       const int64_t waves = int64_t(p.ncolw) * n;
       const int64_t k = ceil_div(waves, int64_t(simds));
       const int64_t rounds = ceil_div(k, int64_t(occ));
       const int64_t kk = std::min<int64_t>(k, occ);
       const double seg = double(ceil_div(out_rows, n));
-      const double cost = double(rounds) * (seg + overhead_rows) * double(kk) * kT[std::min<int64_t>(kk, 4)];
+      const double cost = double(rounds) * (seg + overhead_rows) * double(kk) * issue_factor(xl, kk);
       if (cost < best * 0.999) {
         best = cost;
         best_n = n;

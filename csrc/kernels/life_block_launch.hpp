@@ -22,7 +22,7 @@ constexpr int kSplitMaxRowsPerT = 8;
 
 template <int T, class IO>
 void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
-  p.ncolw = int(ceil_div(p.Wp, 64 * IO::W - 2));
+  p.ncolw = int(ceil_div(p.Wp, wave_out_words<IO::XL, IO::W>()));
   const int simds = 4 * std::max(1, tune.cus);
   if constexpr (T >= 4) {
     if (tune.group != 0 && tune.split == 0 && !tune.skew) {
@@ -32,17 +32,17 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       LifeBlockParams g4 = p, g8 = p;
       const double c4 = (tune.group == 4 || tune.group < 0)
                             ? plan_group<T, 4>(g4, out_rows, simds, group_waves_per_simd<T, IO, 4>(),
-                                               tune.target_waves)
+                                               tune.target_waves, IO::XL)
                             : -1.0;
       const double c8 = (tune.group == 8 || tune.group < 0)
                             ? plan_group<T, 8>(g8, out_rows, simds, group_waves_per_simd<T, IO, 8>(),
-                                               tune.target_waves)
+                                               tune.target_waves, IO::XL)
                             : -1.0;
       double cc = -1.0;
       if (tune.group < 0) {
         LifeBlockParams q = p;
         plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves,
-             1.2 * (T - 1), &cc);
+             1.2 * (T - 1), &cc, IO::XL);
       }
       // Segments shorter than 2T (compiled for the default T = 16 bit-layout
       // kernel; the byte layout spills at 4 waves/SIMD): lets small tiles
@@ -60,13 +60,13 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
       if (better(c8, cc)) return launch_group<T, IO, 8>(g8, s);
     }
-    bool split = tune.split > 0;
-    if (tune.split < 0 && !tune.skew) {
+    bool split = tune.split > 0 && IO::XL != kXlaneAdd;
+    if (tune.split < 0 && !tune.skew && IO::XL != kXlaneAdd) {
       LifeBlockParams q = p;
       plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves);
       split = q.seg_rows < kSplitMaxRowsPerT * T;
     }
-    if (split && tune.scratch) {
+    if constexpr (IO::XL != kXlaneAdd) if (split && tune.scratch) {
       const int64_t in_rows = out_rows + 2 * int64_t(T);
       // Segments of >= 2T + 2 input rows: the last two steps (bottom state)
       // then fall in the steady loop, never in the prologue.
@@ -85,7 +85,8 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
     }
   }
   const int occ = tune.skew ? waves_per_simd<T, IO, true, false>() : waves_per_simd<T, IO, false, false>();
-  const bool skew = plan(p, T, out_rows, simds, occ, tune.min_seg_rows, tune.target_waves) && tune.skew;
+  const bool skew = plan(p, T, out_rows, simds, occ, tune.min_seg_rows, tune.target_waves, -1, nullptr, IO::XL) &&
+                    tune.skew;
   const int waves = p.ncolw * p.nseg;
   const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
   if (skew)

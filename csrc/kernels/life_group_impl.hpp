@@ -148,6 +148,12 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
 #ifndef GOL_GROUP_T16_WAVES
 #define GOL_GROUP_T16_WAVES 2
 #endif
+// The adder window's T = 16 grouped kernel lands at ~156 VGPRs (3 waves/SIMD)
+// unconstrained; its level body is 17% cheaper at 4 waves/SIMD than at 3
+// (csrc/tools/ubench_body.hip), so it is held to 128 VGPRs.
+#ifndef GOL_GROUP_T16_ADD_WAVES
+#define GOL_GROUP_T16_ADD_WAVES 4
+#endif
 
 // Occupancy floor of the grouped kernel (a register cap, not a target: the
 // allocator lands at 123 VGPRs = 4 waves/SIMD for bits T = 16 and at 183 for
@@ -156,6 +162,7 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
 template <int T, class IO>
 constexpr int group_min_waves() {
   if constexpr (IO::W >= 2) return T >= 12 ? 2 : T >= 8 ? 3 : 4;
+  if constexpr (IO::XL == kXlaneAdd) return T >= 16 ? GOL_GROUP_T16_ADD_WAVES : T >= 12 ? 3 : 4;
   return T >= 16 ? GOL_GROUP_T16_WAVES : T >= 12 ? 3 : 4;
 }
 
@@ -177,7 +184,7 @@ template <int T, class IO, int M>
 __global__ __launch_bounds__(64 * M) __attribute__((amdgpu_waves_per_eu(group_min_waves<T, IO>())))
 void life_group_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
-  constexpr int kWaveOut = 64 * W - 2;
+  constexpr int kWaveOut = wave_out_words<IO::XL, W>();
   constexpr int kSlot = (T - 1) * 2 * W * 64;  // dwords per boundary
   __shared__ uint32_t saved[M * kSlot];
   const int lane = threadIdx.x & 63;
@@ -207,7 +214,7 @@ void life_group_kernel(const LifeBlockParams p) {
   for (int i = 0; i < W; ++i) {
     const int c = col + i;
     const bool ok = c >= 0 && c < p.Wp;
-    const bool halo = (lane == 0 && i == 0) || (lane == 63 && i == W - 1);
+    const bool halo = wave_halo<IO::XL, W>(lane, i);
     rd.ok[i] = ok;
     wr.own[i] = ok && !halo;
     fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
@@ -276,8 +283,7 @@ void life_group_kernel(const LifeBlockParams p) {
 // in rows of T level bodies.  Returns the cost, or -1 when the rows are too
 // few for M segments of 2T rows.
 template <int T, int M>
-double plan_group(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int target_waves) {
-  static constexpr double kT[] = {0, 1.2, 1.0, 0.97, 0.95};
+double plan_group(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int target_waves, int xl = kXlaneDpp) {
   constexpr double kOverhead = 0.4 * T;  // the two triangles (4T steps) run at lower ILP
   const int64_t max_n = out_rows / (int64_t(M - 1) * 2 * T + 1);
   int64_t best_n = 0;
@@ -302,7 +308,7 @@ double plan_group(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int 
     const int64_t k = ceil_div(waves, int64_t(simds));
     const int64_t rounds = ceil_div(k, int64_t(occ));
     const int64_t kk = std::min<int64_t>(k, occ);
-    double cost = double(rounds) * (span + kOverhead) * double(kk) * kT[std::min<int64_t>(kk, 4)];
+    double cost = double(rounds) * (span + kOverhead) * double(kk) * issue_factor(xl, kk);
     if (target_waves > 0)
       cost = 1.0 + double(std::llabs(waves - int64_t(target_waves)));
     else if (rounds > 4)

@@ -48,7 +48,19 @@ struct LifeBlockParams {
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
 
 // Cross-lane primitive that moves the edge words between lanes.
-enum Xlane : int { kXlaneDpp = 0, kXlaneBpermute = 1, kXlaneCarry = 2 };
+//   kXlaneAdd: no cross-lane data op at all.  The horizontal window is
+//   one-sided (cells x-2, x-1, x): both shifts are add-with-carry
+//   (v_add_co / v_addc_co) whose per-lane carry masks move one lane up on the
+//   SALU (s_lshl_b64).  Each generation then stores cell x-1 at bit x, so the
+//   tile's storage frame drifts one cell to the right per generation; the
+//   engine tracks the drift and rotates it out before any read-out
+//   (Engine::normalize).  Measured (csrc/tools/ubench_dpp_mix.hip): any DPP,
+//   v_alignbit or v_cmp in a v_bitop3 stream drops the SIMD from ~2.4 to
+//   ~4.5 cycles per instruction; add-with-carry ops do not.
+//   kXlaneAuto (default): the adder window where the engine allows a drift
+//   (HipBackend::choose_kernel: whole-width tiles that fill four waves per
+//   SIMD at T = 12), the DPP window everywhere else.
+enum Xlane : int { kXlaneAuto = -1, kXlaneDpp = 0, kXlaneBpermute = 1, kXlaneCarry = 2, kXlaneAdd = 3 };
 
 struct LifeTuning {
   int cus = 256;            // compute units of the device
@@ -56,7 +68,7 @@ struct LifeTuning {
   int min_seg_rows = 16;    // lower bound on rows per wave segment
   bool skew = false;        // software-pipelined (skewed) level schedule
   int wpl_bits = 1;         // 32-cell words per lane, bit layout (1 or 2)
-  int xlane = kXlaneDpp;    // cross-lane primitive
+  int xlane = kXlaneAuto;   // cross-lane primitive
   bool u8_lds = false;      // byte layout: single-step LDS-tiled kernel (T = 1)
   int lds_rows = 32;        // rows per LDS tile (32 or 64)
   int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
@@ -68,7 +80,9 @@ struct LifeTuning {
   std::function<void*(size_t)> scratch;
 };
 
-void launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream);
+// Returns the storage-frame drift of the launch in cells (T for the adder
+// window, 0 otherwise; BlockArgs::allow_drift).
+int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream);
 // Description of the kernel variant the tuning selects for a layout.
 std::string life_block_variant(Layout layout, const LifeTuning& tune);
 // Largest T that keeps 2 waves/SIMD for the variant's words-per-lane.
@@ -86,6 +100,8 @@ GOL_LIFE_VARIANT(launch_bits_w1_carry);
 GOL_LIFE_VARIANT(launch_bits_w2_carry);
 GOL_LIFE_VARIANT(launch_u8_w1_dpp);
 GOL_LIFE_VARIANT(launch_u8_w1_carry);
+GOL_LIFE_VARIANT(launch_bits_w1_add);
+GOL_LIFE_VARIANT(launch_u8_w1_add);
 
 // Single-generation LDS-tiled byte-layout kernel (life_step_lds.hip).
 void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream);
@@ -105,6 +121,10 @@ void launch_store_rows(const uint8_t* buf, const TileGeom& g, uint8_t* stage, in
 void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s);
 void launch_init_random(uint8_t* buf, const TileGeom& g, uint64_t seed, uint32_t thresh24,
                         int64_t grow0, int64_t gcol0, hipStream_t s);
+// Owned rows of `src` rotated left by `shift` cells (0 < shift < W) into
+// `dst`: dst cell x = src cell (x + shift) mod W.  Undoes the adder window's
+// storage drift.
+void launch_rotate_cols(const uint8_t* src, uint8_t* dst, const TileGeom& g, int64_t shift, hipStream_t s);
 
 }  // namespace hipk
 }  // namespace gol

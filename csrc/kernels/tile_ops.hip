@@ -189,6 +189,36 @@ __global__ void init_random_u8(uint8_t* buf, int64_t pitch, int64_t row0, int64_
 
 __global__ void i64_k(int64_t* p, int64_t v, int add) { *p = add ? *p + v : v; }
 
+// Undo the adder window's storage drift (life_kernels.hpp kXlaneAdd): owned
+// word k of the output row is cells [32k, 32k+32) of the true frame, which
+// the drifted input holds at cells [32k + s, 32k + s + 32) (mod W).
+__global__ void rotate_cols_bits(const uint32_t* in, uint32_t* out, int64_t pitch_w, int64_t row0, int64_t H,
+                                 int hw, int64_t ow, int64_t s) {
+  const int64_t q0 = s / 32;
+  const int sh = int(s % 32);
+  const int64_t n = H * ow;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n; t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / ow, k = t - i * ow;
+    const uint32_t* row = in + (row0 + i) * pitch_w + hw;
+    int64_t q = k + q0;
+    if (q >= ow) q -= ow;
+    const uint32_t lo = row[q];
+    const uint32_t hi = row[q + 1 == ow ? 0 : q + 1];
+    out[(row0 + i) * pitch_w + hw + k] = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+  }
+}
+
+__global__ void rotate_cols_u8(const uint8_t* in, uint8_t* out, int64_t pitch, int64_t row0, int64_t H, int64_t c0,
+                               int64_t W, int64_t s) {
+  const int64_t n = H * W;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n; t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / W, x = t - i * W;
+    int64_t y = x + s;
+    if (y >= W) y -= W;
+    out[(row0 + i) * pitch + c0 + x] = in[(row0 + i) * pitch + c0 + y];
+  }
+}
+
 }  // namespace
 
 void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s) {
@@ -262,6 +292,20 @@ void launch_init_random(uint8_t* buf, const TileGeom& g, uint64_t seed, uint32_t
   } else {
     hipLaunchKernelGGL(init_random_u8, dim3(grid_for(g.H * g.W)), dim3(kBlock), 0, s, buf, g.pitch,
                        int64_t(g.row0()), g.cell0(), g.H, g.W, seed, th, grow0, gcol0);
+  }
+}
+
+void launch_rotate_cols(const uint8_t* src, uint8_t* dst, const TileGeom& g, int64_t shift, hipStream_t s) {
+  GOL_REQUIRE(src != dst, "rotate_cols: source and destination must differ");
+  shift = ((shift % g.W) + g.W) % g.W;
+  if (g.layout == Layout::Bits) {
+    GOL_REQUIRE(g.W % 32 == 0, "rotate_cols: bit layout needs width % 32 == 0");
+    hipLaunchKernelGGL(rotate_cols_bits, dim3(grid_for(g.H * (g.W / 32))), dim3(kBlock), 0, s,
+                       reinterpret_cast<const uint32_t*>(src), reinterpret_cast<uint32_t*>(dst), g.pitch / 4,
+                       int64_t(g.row0()), g.H, g.hw, g.W / 32, shift);
+  } else {
+    hipLaunchKernelGGL(rotate_cols_u8, dim3(grid_for(g.H * g.W)), dim3(kBlock), 0, s, src, dst, g.pitch,
+                       int64_t(g.row0()), g.H, g.cell0(), g.W, shift);
   }
 }
 

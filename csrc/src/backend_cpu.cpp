@@ -39,8 +39,10 @@ inline uint32_t owned_mask(const TileGeom& g, int64_t c) {
 
 class CpuBackend final : public Backend {
  public:
-  explicit CpuBackend(int threads) : pool_(threads > 0 ? threads : default_host_threads()) {}
-  std::string name() const override { return "cpu"; }
+  CpuBackend(int threads, bool drift) : pool_(threads > 0 ? threads : default_host_threads()), drift_(drift) {}
+  std::string name() const override { return drift_ ? "cpu [drift]" : "cpu"; }
+  bool drifts(Layout) const override { return drift_; }
+  void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override;
   bool is_device() const override { return false; }
 
   void* alloc(size_t bytes) override {
@@ -66,7 +68,7 @@ class CpuBackend final : public Backend {
   void event_wait(void*) override {}
   void event_destroy(void*) override {}
 
-  void run_block(const BlockArgs& a) override;
+  int run_block(const BlockArgs& a) override;
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override;
   void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {
     *flag = alive_count(buf, g) > 0 ? 1u : 0u;
@@ -91,9 +93,10 @@ class CpuBackend final : public Backend {
     return pack32(row + 32 * c);
   }
   ThreadPool pool_;
+  bool drift_ = false;
 };
 
-void CpuBackend::run_block(const BlockArgs& a) {
+int CpuBackend::run_block(const BlockArgs& a) {
   const TileGeom& g = a.g;
   const int T = a.T;
   const int64_t Wp = g.Wp();
@@ -141,7 +144,19 @@ void CpuBackend::run_block(const BlockArgs& a) {
       if (ch) a.changed[idx] = 1u;
     }
   }
-  const auto& fin = lvl[T & 1];
+  auto& fin = lvl[T & 1];
+  // Drift emulation: the HIP adder window stores generation t+1's cell x-1 at
+  // column x, so after T levels the row sits T cells to the right with zeros
+  // (junk on the GPU) entering at the left edge of the padded row.
+  const int drift = (drift_ && a.allow_drift && T < 32 && 32 * g.hw >= 2 * T) ? T : 0;
+  if (drift) {
+    pool_.parallel_for(a.row_hi - a.row_lo, [&](int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) {
+        uint32_t* w = &fin[size_t((a.row_lo + k - r0) * Wp)];
+        for (int64_t c = Wp - 1; c >= 0; --c) w[c] = (w[c] << drift) | (c > 0 ? w[c - 1] >> (32 - drift) : 0u);
+      }
+    });
+  }
   auto* out = static_cast<uint8_t*>(a.out);
   pool_.parallel_for(a.row_hi - a.row_lo, [&](int64_t b, int64_t e) {
     for (int64_t k = b; k < e; ++k) {
@@ -152,6 +167,36 @@ void CpuBackend::run_block(const BlockArgs& a) {
         std::memcpy(row, src, size_t(4 * Wp));
       else
         for (int64_t c = 0; c < Wp; ++c) unpack32(src[c], row + 32 * c);
+    }
+  });
+  return drift;
+}
+
+void CpuBackend::rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) {
+  auto* s = static_cast<const uint8_t*>(src);
+  auto* d = static_cast<uint8_t*>(dst);
+  const int64_t W = g.W;
+  shift = ((shift % W) + W) % W;
+  pool_.parallel_for(g.H, [&](int64_t b, int64_t e) {
+    std::vector<uint8_t> cells(static_cast<size_t>(W));
+    for (int64_t i = b; i < e; ++i) {
+      const uint8_t* row = s + (g.row0() + i) * g.pitch;
+      uint8_t* out = d + (g.row0() + i) * g.pitch;
+      for (int64_t x = 0; x < W; ++x) {
+        const int64_t c = g.cell0() + x;
+        cells[size_t(x)] = g.layout == Layout::Bits ? uint8_t((row[4 * (c / 32) + (c % 32) / 8] >> (c % 8)) & 1u)
+                                                     : uint8_t(row[c] != 0);
+      }
+      for (int64_t x = 0; x < W; ++x) {
+        const int64_t c = g.cell0() + x;
+        const uint8_t v = cells[size_t((x + shift) % W)];
+        if (g.layout == Layout::Bits) {
+          uint8_t& byte = out[4 * (c / 32) + (c % 32) / 8];
+          byte = uint8_t((byte & ~(1u << (c % 8))) | (unsigned(v) << (c % 8)));
+        } else {
+          out[c] = v;
+        }
+      }
     }
   });
 }
@@ -277,8 +322,12 @@ void CpuBackend::init_random(void* buf, const TileGeom& g, uint64_t seed, double
 
 }  // namespace
 
-std::unique_ptr<Backend> make_cpu_backend(int threads) {
-  return std::make_unique<CpuBackend>(threads);
+std::unique_ptr<Backend> make_cpu_backend(int threads, int drift) {
+  if (drift < 0) {
+    const char* e = std::getenv("GOL_CPU_DRIFT");
+    drift = e && *e && *e != '0' ? 1 : 0;
+  }
+  return std::make_unique<CpuBackend>(threads, drift != 0);
 }
 
 }  // namespace gol

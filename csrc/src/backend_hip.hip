@@ -60,7 +60,7 @@ class HipBackend final : public Backend {
     tune_.min_seg_rows = env_int("GOL_MIN_SEG_ROWS", 16);
     tune_.skew = env_int("GOL_SKEW", 0) != 0;
     tune_.wpl_bits = env_int("GOL_WPL", 1);
-    tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneDpp);
+    tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneAuto);
     if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
     tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
     tune_.split = env_int("GOL_SPLIT", 0);  // measured slower so far (profiles/)
@@ -206,16 +206,45 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipStreamWaitEvent(on ? static_cast<hipStream_t>(on) : stream_, static_cast<hipEvent_t>(mark), 0));
   }
 
-  void run_block(const BlockArgs& a) override {
+  int run_block(const BlockArgs& a) override {
     if (trace_at_ >= 0 && launches_ == trace_at_) return run_block_traced(a);
     ++launches_;
-    hipk::launch_life_block(a, tune_, stream_);
+    const int drift = hipk::launch_life_block(a, tune_, stream_);
+    HIP_CHECK(hipGetLastError());
+    return drift;
+  }
+  bool drifts(Layout l) const override {
+    return tune_.xlane == hipk::kXlaneAdd && (l == Layout::Bits ? tune_.wpl_bits < 2 : true);
+  }
+  // The adder window (kXlaneAdd) beats the DPP window only at four resident
+  // waves per SIMD; its grouped kernel fits that at T = 12 (120 VGPRs) with
+  // segments of at least 2T = 24 rows.  Measured (profiles/r02/adder_ab.jsonl),
+  // per 1000 generations on one MI355X: 32768^2 12.8 -> 11.3 ms, 32768 x 16384
+  // 6.9 -> 5.9 ms, 32768 x 8192 3.9 -> 3.4 ms; the 32768 x 4096 tile (8-GPU
+  // split) cannot fill four waves per SIMD and stays on the DPP window
+  // (2.40 ms vs 2.47 ms at T = 8).
+  KernelChoice choose_kernel(Layout l, int64_t rows, int64_t cols, int tmax_req) const override {
+    KernelChoice k{tmax_req > 0 ? tmax_req : preferred_tmax(l), false};
+    const bool one_word = l == Layout::U8 || tune_.wpl_bits < 2;
+    if (tune_.xlane == hipk::kXlaneAdd && one_word) {
+      k.drift = true;
+      if (tmax_req <= 0) k.tmax = 12;
+    } else if (tune_.xlane == hipk::kXlaneAuto && l == Layout::Bits && one_word && !tune_.skew &&
+               tune_.split == 0 && tune_.group != 0 && (tmax_req <= 0 || tmax_req == 12)) {
+      constexpr int64_t kT = 12;
+      const int64_t strips = ceil_div(ceil_div(cols, 32) + 16, 63);  // + a deep halo's words
+      if (strips * (rows / (2 * kT)) >= int64_t(16) * cus_) k = {int(kT), true};
+    }
+    return k;
+  }
+  void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override {
+    hipk::launch_rotate_cols(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), g, shift, stream_);
     HIP_CHECK(hipGetLastError());
   }
   // GOL_WG_TRACE=<launch index>:<csv path>: one life_block launch records
   // where and when each of its waves ran (grouped kernel, LifeBlockParams::
   // wg_trace); scripts/wg_trace.py turns the CSV into a per-CU makespan view.
-  void run_block_traced(const BlockArgs& a) {
+  int run_block_traced(const BlockArgs& a) {
     ++launches_;
     const size_t bytes = size_t(hipk::kWgTraceWaves) * 4 * sizeof(uint64_t);
     uint64_t* d = nullptr;
@@ -223,7 +252,7 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipMalloc(&d, bytes));
     HIP_CHECK(hipMemsetAsync(d, 0, bytes, stream_));
     tune_.wg_trace = d;
-    hipk::launch_life_block(a, tune_, stream_);
+    const int drift = hipk::launch_life_block(a, tune_, stream_);
     tune_.wg_trace = nullptr;
     HIP_CHECK(hipGetLastError());
     std::vector<uint64_t> h(size_t(hipk::kWgTraceWaves) * 4);
@@ -242,6 +271,7 @@ class HipBackend final : public Backend {
                    a.T, (long long)(a.row_hi - a.row_lo));
     }
     std::fclose(f);
+    return drift;
   }
   void check_device_errors() override {
     const uint32_t e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);

@@ -126,8 +126,9 @@ PYBIND11_MODULE(_gol, m) {
       .def("device", &Backend::device)
       .def("stream", [](const Backend& b) { return reinterpret_cast<std::uintptr_t>(b.stream()); })
       .def("synchronize", &Backend::synchronize, py::call_guard<py::gil_scoped_release>());
-  m.def("cpu_backend", [](int threads) { return std::shared_ptr<Backend>(make_cpu_backend(threads)); },
-        py::arg("threads") = 0);
+  m.def("cpu_backend",
+        [](int threads, int drift) { return std::shared_ptr<Backend>(make_cpu_backend(threads, drift)); },
+        py::arg("threads") = 0, py::arg("drift") = -1);
   m.def("hip_backend", [](int device) { return std::shared_ptr<Backend>(make_hip_backend(device)); },
         py::arg("device") = 0);
   m.def("hip_available", &hip_available);
@@ -245,6 +246,9 @@ PYBIND11_MODULE(_gol, m) {
       .def("overlap", &Engine::overlap)
       .def("graphs", &Engine::graphs)
       .def_property("generation", &Engine::generation, &Engine::set_generation)
+      .def_property_readonly("drift", &Engine::drift)
+      .def_property_readonly("drifting", &Engine::drifting)
+      .def("normalize", &Engine::normalize, py::call_guard<py::gil_scoped_release>())
       .def("current_buffer", [](const Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })
       .def("load_cells",
            [](Engine& e, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> a) {

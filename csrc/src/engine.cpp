@@ -29,8 +29,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     GOL_REQUIRE(cfg_.W % 32 == 0, "bit-packed layout needs width % 32 == 0 (use the u8 layout)");
   dec_ = Decomposition::make(cfg_.W, cfg_.H, tr_->size(), cfg_.decomp, unit);
 
-  tmax_ = cfg_.tmax > 0 ? cfg_.tmax : be_->preferred_tmax(cfg_.layout);
-  tmax_ = std::min(tmax_, 16);
+  const Backend::KernelChoice kc = be_->choose_kernel(cfg_.layout, rows().size(), cols().size(), cfg_.tmax);
+  tmax_ = std::min(kc.tmax, 16);
   // Epoch depth: a deeper halo means fewer latency-bound exchanges (or local
   // periodic fills: two ~5 us launches each) but ~D redundant rows per epoch.
   // With the grouped kernel the per-rank tile costs the same from 8T to 24T
@@ -46,7 +46,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   }
   D_ = std::max(1, D);
   tmax_ = std::min(tmax_, D_);
-  int hw = int(ceil_div(D_, 32));
+  // A drifting kernel (one-sided window, Backend::drifts) consumes 2 cells of
+  // left halo per generation and none on the right; it needs the tile to be
+  // the whole torus width so that the drift is a relabeling of columns.
+  drift_ok_ = kc.drift && dec_.Px == 1 && cfg_.W % 32 == 0;
+  int hw = int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32));
   Extent r = rows(), c = cols();
   g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
   poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : 256;
@@ -102,6 +106,7 @@ Engine::~Engine() {
 void Engine::load_cells(const uint8_t* cells, int64_t ld) {
   be_->load_owned(buf_[cur_], g_, cells, ld);
   be_->synchronize();
+  drift_ = 0;
 }
 
 void Engine::load_global(const uint8_t* grid, int64_t ld) {
@@ -110,6 +115,7 @@ void Engine::load_global(const uint8_t* grid, int64_t ld) {
 }
 
 void Engine::store_cells(uint8_t* cells, int64_t ld, bool ascii) {
+  normalize();
   be_->synchronize();
   be_->store_owned(buf_[cur_], g_, cells, ld, ascii);
 }
@@ -117,6 +123,16 @@ void Engine::store_cells(uint8_t* cells, int64_t ld, bool ascii) {
 void Engine::init_random(uint64_t seed, double density) {
   be_->init_random(buf_[cur_], g_, seed, density, rows().begin, cols().begin);
   be_->synchronize();
+  drift_ = 0;
+}
+
+void Engine::add_drift(int64_t cells) { drift_ = (drift_ + cells) % cfg_.W; }
+
+void Engine::normalize() {
+  if (drift_ == 0) return;
+  be_->rotate_cols(buf_[cur_], buf_[cur_ ^ 1], g_, drift_);
+  cur_ ^= 1;
+  drift_ = 0;
 }
 
 int64_t Engine::alive_count() {
@@ -240,7 +256,7 @@ void Engine::epoch_overlapped(int64_t d) {
   while (rem > 0) {
     const int T = pick_T(rem);
     Ts.push_back(T);
-    launch(buf_[cur_ ^ par], buf_[cur_ ^ par ^ 1], g_, T, Dv + a + T, Dv + H - a - T, gen_ + a);
+    add_drift(launch(buf_[cur_ ^ par], buf_[cur_ ^ par ^ 1], g_, T, Dv + a + T, Dv + H - a - T, gen_ + a));
     a += T;
     rem -= T;
     par ^= 1;
@@ -280,8 +296,8 @@ void Engine::run_epoch(int64_t d) {
   }
 }
 
-void Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
-                    int64_t gen_base) {
+int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
+                   int64_t gen_base) {
   BlockArgs a;
   a.in = in;
   a.out = out;
@@ -300,12 +316,14 @@ void Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_l
         (flags_ && gen_base + T < flags_base_ + flags_len_ && gen_base >= flags_base_) ? flags_ : nullptr;
   }
   a.flags_base = flags_base_;
-  be_->run_block(a);
+  a.allow_drift = drift_ok_;
+  const int drift = be_->run_block(a);
   ++launches_;
+  return drift;
 }
 
 void Engine::step_block(int T, int64_t row_lo, int64_t row_hi) {
-  launch(buf_[cur_], buf_[cur_ ^ 1], g_, T, row_lo, row_hi, gen_);
+  add_drift(launch(buf_[cur_], buf_[cur_ ^ 1], g_, T, row_lo, row_hi, gen_));
   cur_ ^= 1;
   gen_ += T;
 }
@@ -439,6 +457,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
       const int par = cur_;
       if (!graph_[par]) {
         const int64_t k0 = launches_;
+        const int64_t dr0 = drift_;
         capturing_ = true;
         epoch_start_ = gen_;
         be_->capture_begin();
@@ -448,10 +467,12 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
         capturing_ = false;
         graph_flip_[par] = cur_ ^ par;
         graph_kernels_[par] = launches_ - k0;
+        graph_drift_[par] = ((drift_ - dr0) % cfg_.W + cfg_.W) % cfg_.W;
         be_->graph_launch(graph_[par]);  // capture only recorded it
       } else {
         be_->graph_launch(graph_[par]);
         cur_ ^= graph_flip_[par];
+        add_drift(graph_drift_[par]);
         gen_ += D_;
         ++exchanges_;
         launches_ += graph_kernels_[par];

@@ -48,7 +48,7 @@ def test_every_temporal_block_size(gpu, tmax, layout):
 
 
 @pytest.mark.parametrize("wpl,xlane,skew", [(1, 0, 0), (1, 1, 0), (1, 2, 0), (2, 0, 0), (2, 2, 0), (1, 0, 1),
-                                            (1, 2, 1), (2, 0, 1)])
+                                            (1, 2, 1), (2, 0, 1), (1, 3, 0), (1, 3, 1)])
 @pytest.mark.parametrize("tmax", [1, 4, 8, 12, 16])
 def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
     """Every compiled life_block variant (words/lane x DPP|bpermute|carry x
@@ -71,7 +71,7 @@ def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
         assert (out == ref).all(), seed
 
 
-@pytest.mark.parametrize("xlane", [0, 2])
+@pytest.mark.parametrize("xlane", [0, 2, 3])
 @pytest.mark.parametrize("tmax", [1, 8, 16])
 def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
     monkeypatch.setenv("GOL_XLANE", str(xlane))
@@ -97,6 +97,47 @@ def test_grouped_schedule_vs_torch(gpu, monkeypatch, group, tmax, layout):
         gens = 2 * tmax + 3
         want = life_step_torch(g, gens, device="cuda")
         assert (life_step(g, gens, engine="hip", layout=layout, tmax=tmax) == want).all(), (W, H)
+
+
+@pytest.mark.parametrize("group", ["0", "4", "8", "-1"])
+@pytest.mark.parametrize("tmax", [2, 4, 8, 12, 16])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_adder_window_vs_torch(gpu, monkeypatch, group, tmax, layout):
+    """The DPP-free adder window (GOL_XLANE=3, kXlaneAdd: one-sided horizontal
+    window from add-with-carry lane masks, storage frame drifting T cells per
+    block) in every schedule, against the fp32 conv oracle; the drift is
+    rotated out by the read-out."""
+    monkeypatch.setenv("GOL_XLANE", "3")
+    monkeypatch.setenv("GOL_GROUP", group)
+    for W, H in [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (64, 40), (32, 3)]:
+        g = random_grid(W, H, W + H + tmax)
+        gens = 2 * tmax + 3
+        want = life_step_torch(g, gens, device="cuda")
+        sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout=layout, tmax=tmax), engine="hip")
+        sim.load(g)
+        sim.advance(gens)
+        assert sim.native_engine.drift == gens % W, (W, H)
+        assert (sim.tile() == want).all(), (W, H)
+
+
+@pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("1x8", 8)])
+@pytest.mark.parametrize("overlap", ["off", "on"])
+def test_adder_window_row_strips_and_termination(gpu, monkeypatch, spec, P, overlap):
+    """Row-strip subdomains on one GPU (the multi-GPU default decomposition)
+    with the drifting adder window: lockstep drift, overlapped edges, exact
+    Generations."""
+    monkeypatch.setenv("GOL_XLANE", "3")
+    for W, H, seed, density in [c for c in CONVERGING if c[0] % 32 == 0][:3] + [(256, 512, 77, 0.5)]:
+        if H < 8 * P:
+            continue
+        g = random_grid(W, H, seed, density)
+        ref, rgens, _ = reference_run(g)
+        grp = InProcessGroup(LifeConfig(W, H, decomp=spec, tmax=8, epoch=16, poll_gens=32, overlap=overlap), P,
+                             engine="hip")
+        grp.load(g)
+        reps = grp.run()
+        assert {r.generations for r in reps} == {rgens}, (W, H, seed)
+        assert (grp.gather() == ref).all(), (W, H, seed)
 
 
 @pytest.mark.parametrize("group", ["4", "8"])
