@@ -48,11 +48,12 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       // kernel; the byte layout spills at 4 waves/SIMD): lets small tiles
       // fill 4 waves per SIMD.
       const auto better = [](double a, double b) { return a > 0 && (b < 0 || a <= b); };
-      if constexpr (T == 16 && IO::kBits && IO::W == 1 && IO::XL == kXlaneDpp) {
+      if constexpr (IO::kBits && IO::W == 1 &&
+                    ((T == 16 && IO::XL == kXlaneDpp) || (T == 12 && IO::XL == kXlaneAdd))) {
         LifeBlockParams s8 = p;
         const double cs = tune.short_seg && (tune.group == 8 || tune.group < 0)
                               ? plan_short<T, 8>(s8, out_rows, simds, short_waves_per_simd<T, IO, 8>(),
-                                                 tune.target_waves)
+                                                 tune.target_waves, IO::XL)
                               : -1.0;
         if (cs > 0 && (tune.short_seg == 2 || (better(cs, c4) && better(cs, c8) && better(cs, cc))))
           return launch_short<T, IO, 8>(s8, s);

@@ -129,7 +129,7 @@ template <int T, class IO, int M, int Q>
 __global__ __launch_bounds__(64 * M) __attribute__((amdgpu_waves_per_eu(4)))
 void life_short_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
-  constexpr int kWaveOut = 64 * W - 2;
+  constexpr int kWaveOut = wave_out_words<IO::XL, W>();
   constexpr int kSlot = (T - 1) * 2 * W * 64;
   __shared__ uint32_t saved[M * kSlot];
   __shared__ uint32_t ready[M * T];
@@ -155,7 +155,7 @@ void life_short_kernel(const LifeBlockParams p) {
   for (int i = 0; i < W; ++i) {
     const int c = col + i;
     const bool ok = c >= 0 && c < p.Wp;
-    const bool halo = (lane == 0 && i == 0) || (lane == 63 && i == W - 1);
+    const bool halo = wave_halo<IO::XL, W>(lane, i);
     rd.ok[i] = ok;
     wr.own[i] = ok && !halo;
     fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
@@ -214,16 +214,15 @@ void life_short_kernel(const LifeBlockParams p) {
   }
 }
 
-// Segment lengths compiled for T = 16 (q < 2T; longer segments use the
-// grouped kernel).
+// Segment lengths compiled (q < 2T; longer segments use the grouped kernel):
+// T = 16 DPP window and T = 12 adder window.
 constexpr int kShortQ[] = {16, 18, 20, 22, 24, 26, 28, 30};
 
 // Plan over groups per strip and the compiled Q: non-last waves Q rows, the
 // last wave Lg - (M-1)Q >= 0 rows plus the redundant triangle (~T-1 rows).
 // Same makespan model as plan_group.  Returns the cost (p.grp_q = Q) or -1.
 template <int T, int M>
-double plan_short(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int target_waves) {
-  static constexpr double kT[] = {0, 1.2, 1.0, 0.97, 0.95};
+double plan_short(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int target_waves, int xl = kXlaneDpp) {
   constexpr double kOverhead = 0.4 * T;
   double best = 1e300;
   int64_t best_n = 0;
@@ -241,7 +240,7 @@ double plan_short(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int 
       const int64_t k = ceil_div(waves, int64_t(simds));
       const int64_t rounds = ceil_div(k, int64_t(occ));
       const int64_t kk = std::min<int64_t>(k, occ);
-      double cost = double(rounds) * (span + kOverhead) * double(kk) * kT[std::min<int64_t>(kk, 4)];
+      double cost = double(rounds) * (span + kOverhead) * double(kk) * issue_factor(xl, kk);
       if (target_waves > 0) cost = 1.0 + double(std::llabs(waves - int64_t(target_waves)));
       if (cost < best * 0.999) {
         best = cost;

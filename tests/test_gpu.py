@@ -162,28 +162,32 @@ def test_grouped_schedule_many_groups_and_termination(gpu, monkeypatch, group):
 
 @pytest.mark.parametrize("layout", ["bits", "u8"])  # u8: falls back to the grouped kernel
 @pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
-def test_short_segment_schedule_vs_torch(gpu, monkeypatch, layout, W, H):
+@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
+def test_short_segment_schedule_vs_torch(gpu, monkeypatch, layout, W, H, xlane, tmax):
     """Short-segment groups (csrc/kernels/life_short_impl.hpp: segments of
     Q < 2T rows, the whole sweep unrolled, level rows of the lower wave handed
     over through LDS with per-level flags) forced on, against the fp32 conv
     oracle; several segment lengths Q via the wave-count target."""
     monkeypatch.setenv("GOL_SHORT", "2")
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
     g = random_grid(W, H, W * 3 + H)
     want = life_step_torch(g, 35, device="cuda")
     for target in ("0", "100000", "3000"):
         monkeypatch.setenv("GOL_TARGET_WAVES", target)
-        assert (life_step(g, 35, engine="hip", layout=layout, tmax=16) == want).all(), target
+        assert (life_step(g, 35, engine="hip", layout=layout, tmax=tmax) == want).all(), target
 
 
-def test_short_segment_schedule_termination(gpu, monkeypatch):
+@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
+def test_short_segment_schedule_termination(gpu, monkeypatch, xlane, tmax):
     monkeypatch.setenv("GOL_SHORT", "2")
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
     monkeypatch.setenv("GOL_TARGET_WAVES", "100000")
     grid = np.zeros((1024, 512), dtype=np.uint8)
     W, H, seed, density = CONVERGING[5]
     grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(grid)
     for layout in ("bits", "u8"):
-        out, rep = simulate(grid, 1000, engine="hip", layout=layout, tmax=16)
+        out, rep = simulate(grid, 1000, engine="hip", layout=layout, tmax=tmax)
         assert rep.generations == rgens, layout
         assert (out == ref).all(), layout
 
