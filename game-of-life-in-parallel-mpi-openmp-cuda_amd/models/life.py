@@ -171,7 +171,8 @@ class Simulation:
                 "rank": self.rank, "ranks": d.nranks(), "tile_rows": g.H, "tile_cols": g.W,
                 "halo_rows": g.Dv, "halo_words": g.hw, "tmax": self._eng.tmax,
                 "epoch": self._eng.epoch_depth, "pitch": g.pitch, "overlap": self._eng.overlap(),
-                "graphs": self._eng.graphs()}
+                "graphs": self._eng.graphs(),
+                "kernel": "adder window (drifting frame)" if self._eng.drifting else "symmetric window"}
 
     # -- state -----------------------------------------------------------
     def load(self, grid: np.ndarray) -> None:

@@ -31,8 +31,8 @@ ARCH = os.environ.get("GOL_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/transport.cpp",
              "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp"]
-LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "u8_w1_dpp",
-                 "u8_w1_carry"]
+LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "bits_w1_add", "u8_w1_dpp",
+                 "u8_w1_carry", "u8_w1_add"]
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
             *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
             "kernels/tile_ops.hip"]
