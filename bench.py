@@ -66,7 +66,7 @@ def main() -> int:
     ap.add_argument("--tmax", type=int, default=0)
     ap.add_argument("--epoch", type=int, default=0)
     ap.add_argument("--poll", type=int, default=0)
-    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "edges"])
     ap.add_argument("--graphs", default="off", choices=["auto", "on", "off"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--repeats", type=int, default=1, help="timed repetitions (best is reported)")

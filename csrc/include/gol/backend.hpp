@@ -32,11 +32,18 @@ class Backend {
   virtual void copy_h2d(void* dst, const void* src, size_t bytes) = 0;        // synchronous
   virtual void copy_d2h(void* dst, const void* src, size_t bytes) = 0;        // synchronous
   virtual void copy_d2h_async(void* dst, const void* src, size_t bytes) = 0;  // into pinned
+  // Same, on `stream` (nullptr = the compute stream).
+  virtual void copy_d2h_async_on(void* dst, const void* src, size_t bytes, void* stream) {
+    (void)stream;
+    copy_d2h_async(dst, src, bytes);
+  }
   virtual void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch,
                              int64_t width_bytes, int64_t rows) = 0;
   virtual void synchronize() = 0;
   // Events: returns an opaque handle recorded on the stream.
   virtual void* event_record() = 0;
+  // Same, recorded on `stream` (nullptr = the compute stream).
+  virtual void* event_record_on(void* stream) { return stream ? nullptr : event_record(); }
   virtual void event_wait(void* ev) = 0;  // host blocks until the event completes
   virtual void event_destroy(void* ev) = 0;
   // Non-blocking: has the event completed?  (Synchronous backends: always.)
@@ -92,6 +99,8 @@ class Backend {
   // columns (left/right halo words of owned rows) and/or rows (full padded
   // rows of the top/bottom halo, which also fills the corners).
   virtual void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) = 0;
+  // Periodic column halos of padded rows [r0, r0 + n) only (whole-width tiles).
+  virtual void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n) = 0;
   // OR of all owned cells -> *flag (device) = 1 if any cell is alive.
   virtual void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) = 0;
   // Count of live owned cells (synchronous, for diagnostics/tests).

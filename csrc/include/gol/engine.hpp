@@ -38,9 +38,16 @@ struct EngineConfig {
   int tmax = 0;                    // max generations per kernel launch (0 = backend default)
   int epoch = 0;                   // generations per halo exchange (0 = auto)
   int poll_gens = 0;               // generations between termination polls (0 = auto)
-  // Overlap the north/south halo exchange with the interior of the epoch
-  // (edge strips recomputed in scratch tiles): 1 on when possible (Py > 1,
-  // H > 2D); 0 / -1 (auto) off - measured slower than the plain exchange.
+  // Overlap the north/south halo exchange with compute (row strips, Py > 1,
+  // H > 2D):
+  //   -1 auto / 1 on: early boundary - the last temporal block of an epoch
+  //      computes the 2 x D boundary rows first, sends them on the comm
+  //      stream and computes the interior while they travel; the flag
+  //      all-reduce of each poll runs on the same comm stream (all RCCL ops
+  //      of the communicator stay on one stream, in issue order);
+  //    2 edges: the edge strips are recomputed in scratch tiles while the
+  //      interior runs (round 1; eight small launches per epoch, slower);
+  //    0 off.
   int overlap = -1;
   // Check each termination poll one poll window later, so the host never
   // drains the device queue (stops are absorbing, so running past is exact).
@@ -98,7 +105,7 @@ class Engine {
   Extent cols() const { return dec_.cols(rank_); }
   int epoch_depth() const { return D_; }
   int tmax() const { return tmax_; }
-  bool overlap() const { return overlap_; }
+  bool overlap() const { return overlap_ || early_; }
   bool graphs() const { return use_graphs_; }
   int64_t generation() const { return gen_; }
   void set_generation(int64_t g) { gen_ = g; }
@@ -150,6 +157,16 @@ class Engine {
   int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base);
   void add_drift(int64_t cells);
   void exchange_columns(void* buf);
+  // Stream carrying this engine's transport operations (comm stream in the
+  // early-boundary schedule, else the compute stream), and the two orderings.
+  void* rccl_stream() const;
+  void comm_after_compute();
+  void compute_after_comm();
+  // Last block of a full epoch in the early-boundary schedule (engine.cpp).
+  void last_block_early(int T);
+  // Waits for an early exchange still in flight; `invalidate` when the
+  // buffers are about to change outside the schedule.
+  void settle_pending(bool invalidate);
   // d generations (d <= D_) with the row exchange overlapped (see engine.cpp).
   void epoch_overlapped(int64_t d);
   void run_epoch(int64_t d);
@@ -169,7 +186,12 @@ class Engine {
   int64_t flags_base_ = 0, flags_len_ = 0;
   uint32_t* alive_dev_ = nullptr;
   void* colbuf_[4] = {nullptr, nullptr, nullptr, nullptr};  // send W, send E, recv W, recv E
-  bool overlap_ = false;
+  bool overlap_ = false;             // edge-scratch schedule (overlap = 2)
+  bool early_ = false;               // early-boundary schedule (overlap = -1 / 1)
+  bool send_next_ = false;           // the current epoch is followed by another one in this run
+  bool rows_pending_ = false;        // halo rows of buf_[cur_] were sent early
+  void* rows_arrived_ = nullptr;     // comm-stream mark: they have arrived
+  int64_t early_sends_ = 0;
   bool use_graphs_ = false, capturing_ = false;
   int64_t* gen_dev_ = nullptr;        // device: (epoch start - flags_base_) for graph replays
   int64_t epoch_start_ = 0;

@@ -108,6 +108,8 @@ void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);
+// Column halos of padded rows [r0, r0 + nrows) only.
+void launch_fill_cols_rows(uint8_t* buf, const TileGeom& g, int64_t r0, int64_t nrows, hipStream_t s);
 void launch_fill_rows(uint8_t* buf, const TileGeom& g, hipStream_t s);
 // Fused cols+rows periodic fill (bit layout); false if the geometry needs the two-launch path.
 bool launch_fill_all(uint8_t* buf, const TileGeom& g, hipStream_t s);

@@ -226,16 +226,19 @@ void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s) {
 }
 
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s) {
-  if (g.hw == 0) return;
+  launch_fill_cols_rows(buf, g, g.row0(), g.H, s);
+}
+
+void launch_fill_cols_rows(uint8_t* buf, const TileGeom& g, int64_t r0, int64_t nrows, hipStream_t s) {
+  if (g.hw == 0 || nrows <= 0) return;
   if (g.layout == Layout::Bits) {
-    const int64_t n = g.H * 2 * g.hw;
+    const int64_t n = nrows * 2 * g.hw;
     hipLaunchKernelGGL(fill_cols_bits, dim3(grid_for(n)), dim3(kBlock), 0, s,
-                       reinterpret_cast<uint32_t*>(buf), g.pitch / 4, int64_t(g.row0()), g.H, g.hw,
-                       g.W / 32);
+                       reinterpret_cast<uint32_t*>(buf), g.pitch / 4, r0, nrows, g.hw, g.W / 32);
   } else {
-    const int64_t n = g.H * 2 * g.cell0();
-    hipLaunchKernelGGL(fill_cols_u8, dim3(grid_for(n)), dim3(kBlock), 0, s, buf, g.pitch,
-                       int64_t(g.row0()), g.H, g.cell0(), g.W);
+    const int64_t n = nrows * 2 * g.cell0();
+    hipLaunchKernelGGL(fill_cols_u8, dim3(grid_for(n)), dim3(kBlock), 0, s, buf, g.pitch, r0, nrows,
+                       g.cell0(), g.W);
   }
 }
 

@@ -70,6 +70,7 @@ class CpuBackend final : public Backend {
 
   int run_block(const BlockArgs& a) override;
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override;
+  void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n) override;
   void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {
     *flag = alive_count(buf, g) > 0 ? 1u : 0u;
   }
@@ -203,10 +204,23 @@ void CpuBackend::rotate_cols(const void* src, void* dst, const TileGeom& g, int6
 
 void CpuBackend::fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) {
   auto* p = static_cast<uint8_t*>(buf);
-  const int64_t H = g.H, W = g.W, c0 = g.cell0();
-  if (cols) {
-    pool_.parallel_for(H, [&](int64_t b, int64_t e) {
-      for (int64_t r = g.row0() + b; r < g.row0() + e; ++r) {
+  const int64_t H = g.H;
+  if (cols) fill_cols_rows(buf, g, g.row0(), H);
+  if (rows) {
+    for (int64_t r = 0; r < g.R(); ++r) {
+      if (r >= g.row0() && r < g.row0() + H) continue;
+      int64_t src = g.row0() + (((r - g.row0()) % H) + H) % H;
+      std::memcpy(p + r * g.pitch, p + src * g.pitch, size_t(g.pitch));
+    }
+  }
+}
+
+void CpuBackend::fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n) {
+  auto* p = static_cast<uint8_t*>(buf);
+  const int64_t W = g.W, c0 = g.cell0();
+  {
+    pool_.parallel_for(n, [&](int64_t b, int64_t e) {
+      for (int64_t r = r0 + b; r < r0 + e; ++r) {
         uint8_t* row = p + r * g.pitch;
         if (g.layout == Layout::Bits) {
           auto* w = reinterpret_cast<uint32_t*>(row);
@@ -224,13 +238,6 @@ void CpuBackend::fill_periodic(void* buf, const TileGeom& g, bool cols, bool row
         }
       }
     });
-  }
-  if (rows) {
-    for (int64_t r = 0; r < g.R(); ++r) {
-      if (r >= g.row0() && r < g.row0() + H) continue;
-      int64_t src = g.row0() + (((r - g.row0()) % H) + H) % H;
-      std::memcpy(p + r * g.pitch, p + src * g.pitch, size_t(g.pitch));
-    }
   }
 }
 

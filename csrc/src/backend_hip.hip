@@ -149,6 +149,9 @@ class HipBackend final : public Backend {
   void copy_d2h_async(void* d, const void* s, size_t n) override {
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
   }
+  void copy_d2h_async_on(void* d, const void* s, size_t n, void* stream) override {
+    HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream ? static_cast<hipStream_t>(stream) : stream_));
+  }
   void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
                      int64_t rows) override {
     if (rows <= 0 || width <= 0) return;
@@ -160,6 +163,12 @@ class HipBackend final : public Backend {
     hipEvent_t e;
     HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(e, stream_));
+    return e;
+  }
+  void* event_record_on(void* stream) override {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(e, stream ? static_cast<hipStream_t>(stream) : stream_));
     return e;
   }
   void event_wait(void* ev) override { HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(ev))); }
@@ -287,6 +296,10 @@ class HipBackend final : public Backend {
       if (cols) hipk::launch_fill_cols(p, g, stream_);
       if (rows) hipk::launch_fill_rows(p, g, stream_);
     }
+    HIP_CHECK(hipGetLastError());
+  }
+  void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n) override {
+    hipk::launch_fill_cols_rows(static_cast<uint8_t*>(buf), g, r0, n, stream_);
     HIP_CHECK(hipGetLastError());
   }
   void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {

@@ -29,7 +29,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     GOL_REQUIRE(cfg_.W % 32 == 0, "bit-packed layout needs width % 32 == 0 (use the u8 layout)");
   dec_ = Decomposition::make(cfg_.W, cfg_.H, tr_->size(), cfg_.decomp, unit);
 
-  const Backend::KernelChoice kc = be_->choose_kernel(cfg_.layout, rows().size(), cols().size(), cfg_.tmax);
+  // Every rank must take the same decision (a drifting frame or a schedule
+  // that moves a halo exchange is only consistent in lockstep), so it is
+  // made for the smallest tile of the decomposition, not this rank's.
+  const Backend::KernelChoice kc =
+      be_->choose_kernel(cfg_.layout, min_tile_rows(dec_), std::max<int64_t>(1, min_tile_cols(dec_)), cfg_.tmax);
   tmax_ = std::min(kc.tmax, 16);
   // Epoch depth: a deeper halo means fewer latency-bound exchanges (or local
   // periodic fills: two ~5 us launches each) but ~D redundant rows per epoch.
@@ -65,7 +69,9 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // opt-in: its edge strips run as small, latency-bound launches (eight per
   // epoch), which on the 32768 x 4096 per-rank tile cost 4x more than the
   // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
-  overlap_ = dec_.Py > 1 && cfg_.overlap > 0 && g_.H >= 2 * int64_t(D_) + 1;
+  const bool interior = min_tile_rows(dec_) >= 2 * int64_t(D_) + 1;  // on every rank
+  overlap_ = dec_.Py > 1 && cfg_.overlap == 2 && interior;
+  early_ = dec_.Py > 1 && dec_.Px == 1 && (cfg_.overlap == -1 || cfg_.overlap == 1) && interior;
   if (overlap_) {
     gs_ = TileGeom::make(cfg_.layout, D_, g_.W, D_, g_.hw);
     GOL_REQUIRE(gs_.pitch == g_.pitch, "edge scratch pitch mismatch");
@@ -78,6 +84,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
+  if (use_graphs_) early_ = false;  // captured epochs stay on one stream
   gen_ = cfg_.start_gen;
 }
 
@@ -104,6 +111,7 @@ Engine::~Engine() {
 }
 
 void Engine::load_cells(const uint8_t* cells, int64_t ld) {
+  settle_pending(true);
   be_->load_owned(buf_[cur_], g_, cells, ld);
   be_->synchronize();
   drift_ = 0;
@@ -115,12 +123,14 @@ void Engine::load_global(const uint8_t* grid, int64_t ld) {
 }
 
 void Engine::store_cells(uint8_t* cells, int64_t ld, bool ascii) {
+  settle_pending(false);
   normalize();
   be_->synchronize();
   be_->store_owned(buf_[cur_], g_, cells, ld, ascii);
 }
 
 void Engine::init_random(uint64_t seed, double density) {
+  settle_pending(true);
   be_->init_random(buf_[cur_], g_, seed, density, rows().begin, cols().begin);
   be_->synchronize();
   drift_ = 0;
@@ -130,6 +140,7 @@ void Engine::add_drift(int64_t cells) { drift_ = (drift_ + cells) % cfg_.W; }
 
 void Engine::normalize() {
   if (drift_ == 0) return;
+  settle_pending(true);  // the rotated copy has no halo rows
   be_->rotate_cols(buf_[cur_], buf_[cur_ ^ 1], g_, drift_);
   cur_ ^= 1;
   drift_ = 0;
@@ -204,7 +215,9 @@ void Engine::halo_exchange() {
         {true, nb[kSouth], base + H * pitch, bytes},          // my bottom rows -> south's top halo
         {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
     };
-    tr_->exchange(ops, be_->stream());
+    comm_after_compute();
+    tr_->exchange(ops, rccl_stream());
+    compute_after_comm();
     halo_bytes_ += 2 * int64_t(bytes);
   }
   ++exchanges_;
@@ -286,14 +299,89 @@ void Engine::run_epoch(int64_t d) {
     epoch_overlapped(d);
     return;
   }
-  halo_exchange();
+  if (rows_pending_) {
+    // The previous epoch sent this buffer's boundary rows early.
+    if (rows_arrived_) be_->stream_wait(nullptr, rows_arrived_);
+    rows_pending_ = false;
+    rows_arrived_ = nullptr;
+  } else {
+    halo_exchange();
+  }
   int64_t a = 0;
   while (d > 0) {
     const int T = pick_T(d);
-    step_block(T, a + T, g_.R() - a - T);
+    if (d == T && early_ && send_next_ && a + T == D_)
+      last_block_early(T);
+    else
+      step_block(T, a + T, g_.R() - a - T);
     a += T;
     d -= T;
   }
+}
+
+void* Engine::rccl_stream() const {
+  void* c = early_ ? be_->comm_stream() : nullptr;
+  return c ? c : be_->stream();
+}
+
+void Engine::comm_after_compute() {
+  if (void* c = early_ ? be_->comm_stream() : nullptr) be_->stream_wait(c, be_->stream_mark(nullptr));
+}
+
+void Engine::compute_after_comm() {
+  if (void* c = early_ ? be_->comm_stream() : nullptr) be_->stream_wait(nullptr, be_->stream_mark(c));
+}
+
+void Engine::settle_pending(bool invalidate) {
+  if (!rows_pending_) return;
+  if (rows_arrived_) be_->stream_wait(nullptr, rows_arrived_);
+  be_->synchronize();
+  if (invalidate) {
+    rows_pending_ = false;
+    rows_arrived_ = nullptr;
+  }
+}
+
+// Early-boundary schedule (Py > 1, Px == 1, H > 2D).  The reference waits for
+// every halo before computing (MPI_Startall + MPI_Waitall, src/game_mpi.c:
+// 392-401).  Here the last temporal block of a full epoch writes exactly the
+// owned rows, and the next epoch's halos are the first and last D of them.
+// So that block runs as three launches: the two boundary strips, then - with
+// their periodic column halos filled and the row exchange started on the comm
+// stream - the interior, which the exchange overlaps.  The next epoch's first
+// block waits for the arrival mark.  Every row is still computed once, so
+// the per-generation flags of the three launches OR together exactly.
+void Engine::last_block_early(int T) {
+  trace::Range tr("gol.last_block_early");
+  const int64_t Dv = g_.Dv, H = g_.H, D = D_, pitch = g_.pitch;
+  void* in = buf_[cur_];
+  void* out = buf_[cur_ ^ 1];
+  auto* base = static_cast<uint8_t*>(out);
+  const int drift = launch(in, out, g_, T, Dv, Dv + D, gen_);  // top boundary rows
+  launch(in, out, g_, T, Dv + H - D, Dv + H, gen_);            // bottom boundary rows
+  be_->fill_cols_rows(out, g_, Dv, D);
+  be_->fill_cols_rows(out, g_, Dv + H - D, D);
+  auto nb = dec_.neighbors(rank_);
+  const size_t bytes = size_t(Dv * pitch);
+  std::vector<P2POp> ops = {
+      {true, nb[kNorth], base + Dv * pitch, bytes},
+      {false, nb[kSouth], base + (Dv + H) * pitch, bytes},
+      {true, nb[kSouth], base + H * pitch, bytes},
+      {false, nb[kNorth], base, bytes},
+  };
+  void* comm = be_->comm_stream();
+  if (comm) be_->stream_wait(comm, be_->stream_mark(nullptr));
+  tr_->exchange(ops, comm ? comm : be_->stream());
+  rows_arrived_ = comm ? be_->stream_mark(comm) : nullptr;
+  rows_pending_ = true;
+  halo_bytes_ += 2 * int64_t(bytes);
+  ++exchanges_;
+  ++early_sends_;
+  launch(in, out, g_, T, Dv + D, Dv + H - D, gen_);  // interior, overlapping the exchange
+  be_->fill_cols_rows(out, g_, Dv + D, H - 2 * D);
+  add_drift(drift);
+  cur_ ^= 1;
+  gen_ += T;
 }
 
 int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
@@ -342,9 +430,13 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   const int64_t n = to - from;
   if (n <= 0) return p;
   uint32_t* dev = flags_ + (from + 1 - flags_base_);
-  if (tr_->size() > 1) tr_->allreduce_max_u32(dev, size_t(n), be_->stream());
-  be_->copy_d2h_async(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t));
-  p.ev = be_->event_record();
+  // Early-boundary schedule: reduce and copy on the comm stream, off the
+  // compute stream's critical path, in issue order with the halo exchanges.
+  void* comm = early_ ? be_->comm_stream() : nullptr;
+  comm_after_compute();
+  if (tr_->size() > 1) tr_->allreduce_max_u32(dev, size_t(n), rccl_stream());
+  be_->copy_d2h_async_on(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t), comm);
+  p.ev = be_->event_record_on(comm);
   ++polls_;
   return p;
 }
@@ -438,9 +530,12 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     be_->i64_async(gen_dev_, 0, /*add=*/false);  // first epoch starts at flags_base_
   }
   const int64_t g0 = graph_runs_;
-  const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_;
+  const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_, es0 = early_sends_;
   trace::Range trace_run("gol.run");
-  if (cfg_.timing_barriers) tr_->barrier();
+  if (cfg_.timing_barriers) {
+    settle_pending(false);  // one stream at a time on the communicator
+    tr_->barrier();
+  }
   be_->synchronize();
   auto t0 = std::chrono::steady_clock::now();
 
@@ -451,6 +546,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   bool have_pending = false;
   while (gen_ < limit) {
     const int64_t d = std::min<int64_t>(D_, limit - gen_);
+    send_next_ = gen_ + d < limit;
     if (use_graphs_ && d == D_) {
       // Full epochs replay a captured graph; the only per-epoch input is the
       // device generation offset, advanced by the graph itself.
@@ -502,21 +598,26 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   if (have_pending) poll_check(pending, &found);
   be_->synchronize();
   be_->check_device_errors();
-  if (cfg_.timing_barriers) tr_->barrier();
+  if (cfg_.timing_barriers) {
+    settle_pending(false);
+    tr_->barrier();
+  }
   auto t1 = std::chrono::steady_clock::now();
   res.loop_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   res.executed = gen_ - start;
   res.exchanges = exchanges_ - e0;
   res.polls = polls_ - p0;
   res.kernel_launches = launches_ - l0;
-  res.overlapped = overlap_;
+  res.overlapped = overlap_ || early_sends_ > es0;
   res.graph_launches = graph_runs_ - g0;
   res.halo_bytes = halo_bytes_ - hb0;
   res.generations = limit;
   if (found >= 0) {
     res.first_unchanged = found;
     be_->alive_any(buf_[cur_], g_, alive_dev_);
-    if (tr_->size() > 1) tr_->allreduce_max_u32(alive_dev_, 1, be_->stream());
+    comm_after_compute();
+    if (tr_->size() > 1) tr_->allreduce_max_u32(alive_dev_, 1, rccl_stream());
+    compute_after_comm();
     uint32_t alive = 0;
     be_->copy_d2h(&alive, alive_dev_, 4);
     res.extinct = !alive;

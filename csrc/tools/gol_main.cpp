@@ -75,7 +75,8 @@ struct Options {
                "  --comm thread|rccl          in-process halo transport\n"
                "  --decomp auto|PxQ           process grid (Px columns x Py rows)\n"
                "  --tmax T --epoch D --poll N temporal block, halo depth, poll interval\n"
-               "  --overlap auto|on|off       overlap the row halo exchange with the interior\n"
+               "  --overlap auto|on|off|edges overlap the row halo exchange with compute (early\n"
+               "                              boundary rows; edges = recomputed edge strips)\n"
                "  --graphs auto|on|off        replay full epochs as captured HIP graphs\n"
                "  --threads N                 host threads for the cpu engine\n"
                "  --style serial|mpi|async|collective|openmp|cuda\n"
@@ -120,7 +121,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--poll" || a == "--poll-every") o.poll = std::atoi(next().c_str());
     else if (a == "--overlap") {
       std::string v = next();
-      o.overlap = v == "on" ? 1 : v == "off" ? 0 : -1;
+      o.overlap = v == "on" ? 1 : v == "off" ? 0 : v == "edges" ? 2 : -1;
     } else if (a == "--graphs") {
       std::string v = next();
       o.graphs = v == "on" ? 1 : v == "off" ? 0 : -1;

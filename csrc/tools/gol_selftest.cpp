@@ -185,6 +185,7 @@ bool unit_checks() {
 }  // namespace
 
 int main() {
+  std::setvbuf(stdout, nullptr, _IOLBF, 0);  // progress survives a timeout kill
   const Case cases[] = {
       {96, 64, "1x2", 2, Layout::U8, 4, 8, 0, 40, 1, 0.5},
       {96, 64, "1x2", 2, Layout::U8, 4, 8, 1, 40, 1, 0.5},

@@ -39,8 +39,9 @@ def parse_args(argv=None):
                    help="generations per halo exchange (deep halo depth)")
     p.add_argument("--poll", "--poll-every", dest="poll", type=int, default=0,
                    help="generations between termination polls")
-    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
-                   help="overlap the row halo exchange with interior compute")
+    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "edges"],
+                   help="overlap the row halo exchange with compute: early boundary rows (auto/on), "
+                        "recomputed edge strips (edges), or off")
     p.add_argument("--graphs", default="off", choices=["auto", "on", "off"],
                    help="replay full epochs as captured HIP graphs")
     p.add_argument("--threads", type=int, default=0)

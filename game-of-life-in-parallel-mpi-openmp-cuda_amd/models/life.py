@@ -41,7 +41,7 @@ class LifeConfig:
     tmax: int = 0               # generations per kernel launch (0 = default 16)
     epoch: int = 0              # generations per halo exchange (0 = 4*tmax)
     poll_gens: int = 0          # generations between termination polls (0 = 256)
-    overlap: str = "auto"       # auto | on | off: overlap row halo exchange with the interior
+    overlap: str = "auto"       # auto | on | off | edges: overlap the row halo exchange with compute
     lagged_poll: bool = True    # check termination polls one window late (no queue drain)
     graphs: str = "off"         # auto | on | off: replay full epochs as captured HIP graphs
     start_gen: int = 0          # resume: generation number of the initial state
@@ -68,7 +68,7 @@ class LifeConfig:
         c.tmax = int(self.tmax)
         c.epoch = int(self.epoch)
         c.poll_gens = int(self.poll_gens)
-        c.overlap = {"auto": -1, "off": 0, "on": 1}[self.overlap]
+        c.overlap = {"auto": -1, "off": 0, "on": 1, "edges": 2}[self.overlap]
         c.lagged_poll = bool(self.lagged_poll)
         c.graphs = {"auto": -1, "off": 0, "on": 1}[self.graphs]
         c.start_gen = int(self.start_gen)

@@ -67,10 +67,11 @@ def test_drift_needs_whole_width_tiles(native, monkeypatch):
 
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x3", 3), ("1x4", 4)])
-@pytest.mark.parametrize("overlap", ["off", "on"])
+@pytest.mark.parametrize("overlap", ["off", "on", "edges"])
 def test_drift_row_strips_and_overlap(native, monkeypatch, spec, P, overlap):
     """Row strips (the multi-GPU default) drift in lockstep on every rank;
-    the overlapped epoch's edge scratch tiles drift with the interior."""
+    the early-boundary launches and the edge scratch tiles drift with the
+    interior."""
     monkeypatch.setenv("GOL_CPU_DRIFT", "1")
     W, H = 192, 120
     g = random_grid(W, H, P + 40)

@@ -320,7 +320,7 @@ def test_termination_gpu(gpu, W, H, seed, density):
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("2x2", 4), ("2x4", 8), ("3x3", 9)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-@pytest.mark.parametrize("overlap", ["off", "on"])
+@pytest.mark.parametrize("overlap", ["off", "on", "edges"])
 def test_multi_subdomain_one_gpu(gpu, spec, P, layout, overlap):
     W, H = 32 * 12, 300
     g = random_grid(W, H, 42)
@@ -330,7 +330,7 @@ def test_multi_subdomain_one_gpu(gpu, spec, P, layout, overlap):
     grp.load(g)
     reps = grp.run()
     assert all(r.generations == 150 for r in reps)
-    assert all(r.overlapped == (overlap == "on") for r in reps)
+    assert all(r.overlapped == (overlap == "edges" or (overlap == "on" and spec.startswith("1x"))) for r in reps)
     assert (grp.gather() == want).all()
 
 

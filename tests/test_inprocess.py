@@ -57,46 +57,74 @@ def test_random_init_decomposition_independent(native):
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x3", 3), ("2x2", 4), ("2x3", 6)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("tmax,epoch", [(4, 8), (8, 8), (4, 12), (2, 5)])
-def test_overlapped_exchange_matches_serial(native, spec, P, layout, tmax, epoch):
-    """Overlapped epochs (interior during the row exchange, edge strips in
-    scratch tiles) are bit-identical to the serial reference, including a
-    short final epoch (gens not a multiple of the epoch depth)."""
+@pytest.mark.parametrize("mode", ["on", "edges"])
+def test_overlapped_exchange_matches_serial(native, spec, P, layout, tmax, epoch, mode):
+    """Overlapped epochs are bit-identical to the serial reference, including
+    a short final epoch (gens not a multiple of the epoch depth):
+      on     early boundary rows: the last block of an epoch computes the 2D
+             boundary rows, sends them, then computes the interior (row
+             strips only, Px == 1);
+      edges  interior during the row exchange, edge strips in scratch tiles."""
     W, H = 192, 150
     g = random_grid(W, H, 77 + tmax)
     gens = 3 * epoch + epoch // 2 + 1
     ref, _, _ = reference_run(g, gens)
-    cfg = LifeConfig(W, H, gen_limit=gens, decomp=spec, layout=layout, tmax=tmax, epoch=epoch, overlap="on")
+    cfg = LifeConfig(W, H, gen_limit=gens, decomp=spec, layout=layout, tmax=tmax, epoch=epoch, overlap=mode)
     grp = InProcessGroup(cfg, P, engine="cpu")
     grp.load(g)
     reps = grp.run()
-    assert all(r.overlapped for r in reps)
+    want = mode == "edges" or spec.startswith("1x")
+    assert all(r.overlapped == want for r in reps)
     assert (grp.gather() == ref).all()
 
 
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
 @pytest.mark.parametrize("lagged", [True, False])
-def test_overlapped_termination(native, W, H, seed, density, lagged):
+@pytest.mark.parametrize("mode", ["on", "edges"])
+def test_overlapped_termination(native, W, H, seed, density, lagged, mode):
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
-    cfg = LifeConfig(W, H, decomp="1x2", layout="u8", tmax=2, epoch=3, poll_gens=4, overlap="on",
+    cfg = LifeConfig(W, H, decomp="1x2", layout="u8", tmax=2, epoch=3, poll_gens=4, overlap=mode,
                      lagged_poll=lagged)
     grp = InProcessGroup(cfg, 2, engine="cpu")
     grp.load(g)
     reps = grp.run()
     assert {r.generations for r in reps} == {rgens}
-    assert all(r.overlapped == (H // 2 >= 7) for r in reps)
+    assert all(r.overlapped == (H // 2 >= 7 and r.executed > 3) for r in reps)
     assert (grp.gather() == ref).all()
 
 
-def test_overlap_is_opt_in(native):
-    """auto = off (the edge strips are latency-bound small launches that cost
-    more than the exchange they hide); on requires H > 2D."""
-    auto = InProcessGroup(LifeConfig(64, 512, decomp="1x2", tmax=4, epoch=16), 2, engine="cpu")
-    assert not auto.sims[0].native_engine.overlap()
-    on = InProcessGroup(LifeConfig(64, 512, decomp="1x2", tmax=4, epoch=16, overlap="on"), 2, engine="cpu")
-    assert on.sims[0].native_engine.overlap()
-    short = InProcessGroup(LifeConfig(64, 40, decomp="1x2", tmax=4, epoch=16, overlap="on"), 2, engine="cpu")
-    assert not short.sims[0].native_engine.overlap()
+def test_overlap_modes(native):
+    """auto = on = early boundary rows on row strips with H > 2D; edges = the
+    round-1 edge-strip schedule; off; column decompositions do not overlap."""
+    def ov(**kw):
+        cfg = dict(decomp="1x2", tmax=4, epoch=16)
+        cfg.update(kw)
+        H = cfg.pop("H", 512)
+        return InProcessGroup(LifeConfig(64, H, **cfg), 2, engine="cpu").sims[0].native_engine.overlap()
+    assert ov() and ov(overlap="on") and ov(overlap="edges")
+    assert not ov(overlap="off")
+    assert not ov(H=40)  # tile rows 20 <= 2D
+    assert not ov(decomp="2x1")
+
+
+@pytest.mark.parametrize("lagged", [True, False])
+def test_early_boundary_across_runs_and_readouts(native, lagged):
+    """Chunked runs (run_until) and read-outs between them: an exchange sent at
+    the end of one run is consumed by the next, and a read-out in between
+    (tile(), which may rotate a drift out) never sees stale halos."""
+    W, H = 128, 160
+    g = random_grid(W, H, 5)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=10_000, decomp="1x2", tmax=4, epoch=8, poll_gens=8,
+                                    lagged_poll=lagged), 2, engine="cpu")
+    grp.load(g)
+    want = g
+    done = 0
+    for n in (20, 3, 40, 16, 9):
+        grp.parallel(lambda s: s.native_engine.run_until(s.generation + n))
+        done += n
+        want = reference_run(want, n, check_similarity=False)[0] if n else want
+        assert (grp.gather() == want).all(), done
 
 
 @pytest.mark.parametrize("overlap", ["off", "on"])
@@ -162,3 +190,21 @@ def test_thread_transport_pair_matching_two_ranks(native):
     for r in range(2):
         assert (halo_s[r] == top[1 - r]).all()  # south neighbour's top rows -> my bottom halo
         assert (halo_n[r] == bot[1 - r]).all()  # north neighbour's bottom rows -> my top halo
+
+
+@pytest.mark.parametrize("mode", ["auto", "edges"])
+def test_overlap_decision_is_global_on_uneven_tiles(native, mode):
+    """37 rows over 3 ranks = tiles of 12, 12, 13 rows; with D = 6 only the
+    13-row tile has H > 2D.  Every rank must take the same schedule (a rank
+    that exchanges early while the others reduce flags would deadlock), so
+    the decision uses the smallest tile."""
+    W, H = 96, 37
+    g = random_grid(W, H, 3)
+    ref, rgens, _ = reference_run(g, 50)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=50, decomp="1x3", layout="u8", tmax=2, epoch=6, overlap=mode), 3,
+                         engine="cpu")
+    assert len({s.native_engine.overlap() for s in grp.sims}) == 1
+    grp.load(g)
+    reps = grp.run()
+    assert {r.generations for r in reps} == {rgens}
+    assert (grp.gather() == ref).all()
