@@ -47,7 +47,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _claim_stdout() -> int:
+    """Route fd 1 to stderr for the whole run and return a private duplicate
+    of the real stdout.  The driver reads exactly one JSON line from rank 0's
+    stdout, but RCCL prints a version banner ("RCCL version : ...") to stdout
+    when a communicator is created (ours and torch.distributed's), and other
+    native libraries may print too; only the result line goes to the
+    duplicate."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    return real
+
+
 def main() -> int:
+    out_fd = _claim_stdout()
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="timed steps (one step = --gens-per-step generations)")
@@ -70,6 +84,10 @@ def main() -> int:
     ap.add_argument("--graphs", default="off", choices=["auto", "on", "off"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--repeats", type=int, default=1, help="timed repetitions (best is reported)")
+    ap.add_argument("--rehearse-rccl", action="store_true",
+                    help="one GPU: run the multi-rank row-strip schedule (epoch depth, early-boundary overlap, "
+                         "RCCL send/recv + all-reduce) against a 1-rank RCCL communicator that exchanges with "
+                         "itself; use with --height H/N to rehearse one rank of an N-GPU run")
     a = ap.parse_args()
 
     import torch  # noqa: PLC0415
@@ -92,6 +110,9 @@ def main() -> int:
 
         dist = init_process_group("nccl" if on_gpu else "gloo")
         transport = make_transport(a.comm, backend, local)
+    elif a.rehearse_rccl and on_gpu:
+        C = native()
+        transport = C.rccl_transport(C.rccl_unique_id(), 0, 1, local)
     else:
         transport = native().self_transport()
 
@@ -100,7 +121,8 @@ def main() -> int:
     gps = max(1, a.gens_per_step)
     total = a.prewarm + (a.warmup + a.steps * a.repeats) * gps
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
-                     poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs, timing_barriers=False)
+                     poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs, timing_barriers=False,
+                     self_exchange=bool(a.rehearse_rccl and world == 1))
     sim = Simulation(cfg, transport=transport, backend=backend)
     eng = sim.native_engine
     sim.init_random(a.seed, 0.5)
@@ -156,7 +178,8 @@ def main() -> int:
                 "model": f"Game of Life B3/S23 torus {S}x{Hg}",
                 "global_batch": 1,
                 "seq_len": S * Hg,
-                "parallelism": f"{desc['decomp']} row/col tiles, {'rccl' if world > 1 else 'single'} halos",
+                "parallelism": f"{desc['decomp']} row/col tiles, "
+                               f"{'rccl' if world > 1 else 'rccl-self (rehearsal)' if a.rehearse_rccl else 'single'} halos",
                 "grid": f"{S}x{Hg}",
                 "layout": a.layout,
                 "engine": backend.name(),
@@ -178,7 +201,7 @@ def main() -> int:
                 "baseline": "8.9e8 cell-updates/s (best reference run in BASELINE.md: MPI, 4 ranks, 2048^2, CPU)",
             },
         }
-        print(json.dumps(rec), flush=True)
+        os.write(out_fd, (json.dumps(rec) + "\n").encode())
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -40,6 +40,11 @@ class Backend {
   virtual void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch,
                              int64_t width_bytes, int64_t rows) = 0;
   virtual void synchronize() = 0;
+  // Host waits for `stream` (nullptr = the compute stream) to drain.
+  virtual void synchronize_stream(void* stream) {
+    (void)stream;
+    synchronize();
+  }
   // Events: returns an opaque handle recorded on the stream.
   virtual void* event_record() = 0;
   // Same, recorded on `stream` (nullptr = the compute stream).
@@ -99,8 +104,9 @@ class Backend {
   // columns (left/right halo words of owned rows) and/or rows (full padded
   // rows of the top/bottom halo, which also fills the corners).
   virtual void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) = 0;
-  // Periodic column halos of padded rows [r0, r0 + n) only (whole-width tiles).
-  virtual void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n) = 0;
+  // Periodic column halos of padded rows [r0, r0 + n) only (whole-width
+  // tiles), on `stream` (nullptr = the compute stream).
+  virtual void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n, void* stream = nullptr) = 0;
   // OR of all owned cells -> *flag (device) = 1 if any cell is alive.
   virtual void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) = 0;
   // Count of live owned cells (synchronous, for diagnostics/tests).

@@ -38,16 +38,16 @@ struct EngineConfig {
   int tmax = 0;                    // max generations per kernel launch (0 = backend default)
   int epoch = 0;                   // generations per halo exchange (0 = auto)
   int poll_gens = 0;               // generations between termination polls (0 = auto)
-  // Overlap the north/south halo exchange with compute (row strips, Py > 1,
-  // H > 2D):
-  //   -1 auto / 1 on: early boundary - the last temporal block of an epoch
-  //      computes the 2 x D boundary rows first, sends them on the comm
-  //      stream and computes the interior while they travel; the flag
-  //      all-reduce of each poll runs on the same comm stream (all RCCL ops
-  //      of the communicator stay on one stream, in issue order);
+  // Overlap communication with compute (multi-rank, opt-in; measured slower
+  // than the plain schedule with deep halos, docs/PERFORMANCE.md):
+  //    1 on: early boundary (row strips, H > 2D): the last temporal block of
+  //      an epoch computes the 2 x D boundary rows first (one dual launch on
+  //      the comm stream, waves at top issue priority), sends them, and
+  //      computes the interior while they travel; every transport operation,
+  //      the flag all-reduce included, runs on the comm stream;
   //    2 edges: the edge strips are recomputed in scratch tiles while the
-  //      interior runs (round 1; eight small launches per epoch, slower);
-  //    0 off.
+  //      interior runs (round 1; eight small launches per epoch);
+  //   -1 auto / 0 off: everything on the compute stream.
   int overlap = -1;
   // Check each termination poll one poll window later, so the host never
   // drains the device queue (stops are absorbing, so running past is exact).
@@ -66,6 +66,11 @@ struct EngineConfig {
   // rank 0 only, with no barrier (src/game_mpi.c:385-424).  A caller that
   // brackets the run itself (bench.py) turns them off.
   bool timing_barriers = true;
+  // Rehearsal of a multi-rank row-strip schedule on one rank: the north /
+  // south halos go through the transport (a 1-rank RCCL communicator sending
+  // to itself) instead of the local periodic fill, with the multi-rank epoch
+  // depth and overlap.  Results are identical (the torus wraps to self).
+  bool self_exchange = false;
 };
 
 struct RunResult {
@@ -154,7 +159,8 @@ class Engine {
   int pick_T(int64_t remaining) const;
   // One temporal block in <in> -> <out> for generations (gen_base, gen_base+T];
   // returns the frame drift of the launch (cells).
-  int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base);
+  int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base,
+             void* stream = nullptr, int64_t dual_offset = 0, bool prio_boost = false);
   void add_drift(int64_t cells);
   void exchange_columns(void* buf);
   // Stream carrying this engine's transport operations (comm stream in the
@@ -187,7 +193,8 @@ class Engine {
   uint32_t* alive_dev_ = nullptr;
   void* colbuf_[4] = {nullptr, nullptr, nullptr, nullptr};  // send W, send E, recv W, recv E
   bool overlap_ = false;             // edge-scratch schedule (overlap = 2)
-  bool early_ = false;               // early-boundary schedule (overlap = -1 / 1)
+  bool early_ = false;               // early-boundary schedule (overlap = 1)
+  bool comm_route_ = false;          // transport operations on the comm stream (multi-rank, overlap != 0)
   bool send_next_ = false;           // the current epoch is followed by another one in this run
   bool rows_pending_ = false;        // halo rows of buf_[cur_] were sent early
   void* rows_arrived_ = nullptr;     // comm-stream mark: they have arrived

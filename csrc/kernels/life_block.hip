@@ -55,7 +55,8 @@ int life_block_max_T(Layout layout, const LifeTuning& tune) {
 
 int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream) {
   const TileGeom& g = a.g;
-  GOL_REQUIRE(a.row_lo - a.T >= 0 && a.row_hi + a.T <= g.R() && a.row_lo < a.row_hi,
+  GOL_REQUIRE(a.row_lo - a.T >= 0 && a.row_hi + a.T + a.dual_offset <= g.R() && a.row_lo < a.row_hi &&
+                  a.dual_offset >= 0 && (a.dual_offset == 0 || a.dual_offset >= a.row_hi - a.row_lo),
               "life_block: row range outside the tile");
   GOL_REQUIRE(g.Wp() < (int64_t(1) << 30), "life_block: row too wide");
   // Row stores go through a buffer descriptor per row (num_records = pitch)
@@ -84,10 +85,19 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   }
   p.wg_trace = tune.wg_trace;
   p.err = tune.err;
+  p.row_alt = a.dual_offset;
+  p.prio_boost = a.prio_boost ? 1 : 0;
   const int64_t rows = a.row_hi - a.row_lo;
   int x = xlane_of(g.layout, w, tune);
   if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {
-    launch_life_step_lds(a, tune.lds_rows, stream);
+    BlockArgs b = a;
+    b.dual_offset = 0;
+    launch_life_step_lds(b, tune.lds_rows, stream);
+    if (a.dual_offset) {
+      b.row_lo += a.dual_offset;
+      b.row_hi += a.dual_offset;
+      launch_life_step_lds(b, tune.lds_rows, stream);
+    }
     return 0;
   }
   // The adder window drifts the storage frame by T cells (see kXlaneAdd); the

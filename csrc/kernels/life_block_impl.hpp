@@ -538,12 +538,17 @@ void life_block_kernel(const LifeBlockParams p) {
   const int lane = threadIdx.x & 63;
   // readfirstlane: the wave index is uniform, so everything derived from it
   // (segment bounds, loop trip counts) lives in SGPRs with scalar branches.
-  const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int64_t roff = 0;
+  if (p.row_alt && gw >= p.ncolw * p.nseg) {  // second range of a dual launch
+    gw -= p.ncolw * p.nseg;
+    roff = p.row_alt;
+  }
   if (gw >= p.ncolw * p.nseg) return;  // wave-uniform
   const int kcol = gw / p.nseg;
   const int seg = gw - kcol * p.nseg;
   // Balanced segments: the first `seg_rem` segments get one extra row.
-  const int64_t base = SPLIT ? p.row_lo - T : p.row_lo;
+  const int64_t base = (SPLIT ? p.row_lo - T : p.row_lo) + roff;
   const int64_t s0 = base + int64_t(seg) * p.seg_rows + min(seg, p.seg_rem);
   const int64_t s1 = s0 + p.seg_rows + (seg < p.seg_rem ? 1 : 0);
   const int64_t o0 = SPLIT ? s0 + T : s0;  // level-T output rows [o0, o1)
@@ -567,6 +572,7 @@ void life_block_kernel(const LifeBlockParams p) {
     fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
   }
 
+  if (p.prio_boost) __builtin_amdgcn_s_setprio(3);  // wave-uniform
   Levels<T, W> st;
 #pragma unroll
   for (int L = 0; L < T; ++L) {

@@ -23,9 +23,12 @@ constexpr int kSplitMaxRowsPerT = 8;
 template <int T, class IO>
 void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
   p.ncolw = int(ceil_div(p.Wp, wave_out_words<IO::XL, IO::W>()));
-  const int simds = 4 * std::max(1, tune.cus);
+  // A dual launch (two row ranges) has twice the waves per segment plan:
+  // the planners see 2 x ncolw strips, the kernels map the second half.
+  const int dual = p.row_alt ? 2 : 1;
+  const int simds = 4 * std::max(1, tune.cus) / dual;
   if constexpr (T >= 4) {
-    if (tune.group != 0 && tune.split == 0 && !tune.skew) {
+    if (tune.group != 0 && (tune.split == 0 || dual == 2) && !tune.skew) {
       // M = 4 or 8 waves per workgroup; auto (-1) takes the cheapest of
       // M = 4, M = 8 and the classic plan under the makespan model (classic
       // charged its redundant triangle, T-1 rows, at the triangles' ILP).
@@ -51,7 +54,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       if constexpr (IO::kBits && IO::W == 1 &&
                     ((T == 16 && IO::XL == kXlaneDpp) || (T == 12 && IO::XL == kXlaneAdd))) {
         LifeBlockParams s8 = p;
-        const double cs = tune.short_seg && (tune.group == 8 || tune.group < 0)
+        const double cs = tune.short_seg && dual == 1 && (tune.group == 8 || tune.group < 0)
                               ? plan_short<T, 8>(s8, out_rows, simds, short_waves_per_simd<T, IO, 8>(),
                                                  tune.target_waves, IO::XL)
                               : -1.0;
@@ -61,8 +64,8 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
       if (better(c8, cc)) return launch_group<T, IO, 8>(g8, s);
     }
-    bool split = tune.split > 0 && IO::XL != kXlaneAdd;
-    if (tune.split < 0 && !tune.skew && IO::XL != kXlaneAdd) {
+    bool split = tune.split > 0 && IO::XL != kXlaneAdd && dual == 1;
+    if (tune.split < 0 && !tune.skew && IO::XL != kXlaneAdd && dual == 1) {
       LifeBlockParams q = p;
       plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves);
       split = q.seg_rows < kSplitMaxRowsPerT * T;
@@ -88,7 +91,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
   const int occ = tune.skew ? waves_per_simd<T, IO, true, false>() : waves_per_simd<T, IO, false, false>();
   const bool skew = plan(p, T, out_rows, simds, occ, tune.min_seg_rows, tune.target_waves, -1, nullptr, IO::XL) &&
                     tune.skew;
-  const int waves = p.ncolw * p.nseg;
+  const int waves = p.ncolw * p.nseg * dual;
   const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
   if (skew)
     hipLaunchKernelGGL((life_block_kernel<T, IO, true>), grid, block, 0, s, p);

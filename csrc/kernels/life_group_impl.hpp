@@ -86,8 +86,13 @@ struct Prio {
   int done0 = 0;
   int next = 0;  // work at which the priority drops next
   int cur = kLevels - 1;
-  __device__ __forceinline__ explicit Prio(int wtot)
-      : quarter(max(1, wtot / max(kLevels, 1))), next(max(1, wtot / max(kLevels, 1))) {
+  bool boost = false;  // stay at priority 3 (prio_boost launches)
+  __device__ __forceinline__ Prio(int wtot, bool boost_)
+      : quarter(max(1, wtot / max(kLevels, 1))), next(max(1, wtot / max(kLevels, 1))), boost(boost_) {
+    if (boost) {
+      __builtin_amdgcn_s_setprio(3);
+      return;
+    }
 #if GOL_PRIO_BUCKETS
     if (cur == 3) __builtin_amdgcn_s_setprio(3);
     else if (cur == 2) __builtin_amdgcn_s_setprio(2);
@@ -96,7 +101,7 @@ struct Prio {
   }
   __device__ __forceinline__ void at(int done) {
 #if GOL_PRIO_BUCKETS
-    if (cur > 0 && done >= next) {  // wave-uniform; one scalar compare per step
+    if (!boost && cur > 0 && done >= next) {  // wave-uniform; one scalar compare per step
       next += quarter;
       --cur;
       if (cur == 2) __builtin_amdgcn_s_setprio(2);
@@ -190,9 +195,16 @@ void life_group_kernel(const LifeBlockParams p) {
   const int lane = threadIdx.x & 63;
   const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t t_start = p.wg_trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  const int kcol = blockIdx.x / p.nseg;
-  const int grp = blockIdx.x - kcol * p.nseg;
-  const int64_t G0 = p.row_lo + int64_t(grp) * p.seg_rows + min(grp, p.seg_rem);
+  if (p.prio_boost) __builtin_amdgcn_s_setprio(3);  // wave-uniform
+  int blk = blockIdx.x;
+  int64_t roff = 0;
+  if (p.row_alt && blk >= p.ncolw * p.nseg) {  // second range of a dual launch
+    blk -= p.ncolw * p.nseg;
+    roff = p.row_alt;
+  }
+  const int kcol = blk / p.nseg;
+  const int grp = blk - kcol * p.nseg;
+  const int64_t G0 = p.row_lo + roff + int64_t(grp) * p.seg_rows + min(grp, p.seg_rem);
   const int64_t G1 = G0 + p.seg_rows + (grp < p.seg_rem ? 1 : 0);
   const int64_t in0 = G0 + int64_t(m) * p.grp_q - T;
   const bool last = m == M - 1;
@@ -248,7 +260,7 @@ void life_group_kernel(const LifeBlockParams p) {
   int k = kPro;
   constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
   // Post-barrier work in level bodies: main loop + epilogue triangle.
-  Prio prio((kmain - kPro) * T + epi_work<T>(nfull));
+  Prio prio((kmain - kPro) * T + epi_work<T>(nfull), p.prio_boost != 0);
   for (; k + 3 <= kmain; k += 3) {
     prio.at((k - kPro) * T);
     wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
@@ -345,7 +357,8 @@ int group_waves_per_simd() {
 
 template <int T, class IO, int M>
 void launch_group(const LifeBlockParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((life_group_kernel<T, IO, M>), dim3(unsigned(int64_t(p.ncolw) * p.nseg)), dim3(64 * M), 0, s,
+  hipLaunchKernelGGL((life_group_kernel<T, IO, M>), dim3(unsigned(int64_t(p.ncolw) * p.nseg * (p.row_alt ? 2 : 1))),
+                     dim3(64 * M), 0, s,
                      p);
 }
 

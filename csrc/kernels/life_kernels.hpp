@@ -43,6 +43,10 @@ struct LifeBlockParams {
   // a kernel that has to give up (life_short_kernel's bounded LDS hand-off
   // wait) sets it instead of continuing silently with invalid rows.
   uint32_t* err;
+  // Dual launch (BlockArgs::dual_offset): blocks / waves past the first
+  // ncolw x nseg evaluate the same row range shifted by row_alt rows.
+  int64_t row_alt;
+  int prio_boost;  // BlockArgs::prio_boost
 };
 
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;

@@ -70,7 +70,7 @@ class CpuBackend final : public Backend {
 
   int run_block(const BlockArgs& a) override;
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override;
-  void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n) override;
+  void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n, void* stream = nullptr) override;
   void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {
     *flag = alive_count(buf, g) > 0 ? 1u : 0u;
   }
@@ -98,6 +98,15 @@ class CpuBackend final : public Backend {
 };
 
 int CpuBackend::run_block(const BlockArgs& a) {
+  if (a.dual_offset) {  // two row ranges: one block each, flags OR together
+    BlockArgs b = a;
+    b.dual_offset = 0;
+    const int drift = run_block(b);
+    b.row_lo += a.dual_offset;
+    b.row_hi += a.dual_offset;
+    run_block(b);
+    return drift;
+  }
   const TileGeom& g = a.g;
   const int T = a.T;
   const int64_t Wp = g.Wp();
@@ -215,7 +224,7 @@ void CpuBackend::fill_periodic(void* buf, const TileGeom& g, bool cols, bool row
   }
 }
 
-void CpuBackend::fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n) {
+void CpuBackend::fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n, void*) {
   auto* p = static_cast<uint8_t*>(buf);
   const int64_t W = g.W, c0 = g.cell0();
   {

@@ -159,6 +159,9 @@ class HipBackend final : public Backend {
                                hipMemcpyDefault, stream_));
   }
   void synchronize() override { HIP_CHECK(hipStreamSynchronize(stream_)); }
+  void synchronize_stream(void* s) override {
+    HIP_CHECK(hipStreamSynchronize(s ? static_cast<hipStream_t>(s) : stream_));
+  }
   void* event_record() override {
     hipEvent_t e;
     HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -199,6 +202,9 @@ class HipBackend final : public Backend {
     hipk::launch_i64(dev, v, add, stream_);
     HIP_CHECK(hipGetLastError());
   }
+  // Default priority: a high-priority stream (hipStreamCreateWithPriority)
+  // made every epoch ~0.9 ms slower in the one-GPU RCCL rehearsal
+  // (profiles/r02/rehearsal_overlap.jsonl).
   void* comm_stream() override {
     if (!comm_) HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
     return comm_;
@@ -218,7 +224,7 @@ class HipBackend final : public Backend {
   int run_block(const BlockArgs& a) override {
     if (trace_at_ >= 0 && launches_ == trace_at_) return run_block_traced(a);
     ++launches_;
-    const int drift = hipk::launch_life_block(a, tune_, stream_);
+    const int drift = hipk::launch_life_block(a, tune_, a.stream ? static_cast<hipStream_t>(a.stream) : stream_);
     HIP_CHECK(hipGetLastError());
     return drift;
   }
@@ -298,8 +304,8 @@ class HipBackend final : public Backend {
     }
     HIP_CHECK(hipGetLastError());
   }
-  void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n) override {
-    hipk::launch_fill_cols_rows(static_cast<uint8_t*>(buf), g, r0, n, stream_);
+  void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n, void* stream) override {
+    hipk::launch_fill_cols_rows(static_cast<uint8_t*>(buf), g, r0, n, stream ? static_cast<hipStream_t>(stream) : stream_);
     HIP_CHECK(hipGetLastError());
   }
   void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {

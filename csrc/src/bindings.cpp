@@ -198,6 +198,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_readwrite("overlap", &EngineConfig::overlap)
       .def_readwrite("lagged_poll", &EngineConfig::lagged_poll)
       .def_readwrite("timing_barriers", &EngineConfig::timing_barriers)
+      .def_readwrite("self_exchange", &EngineConfig::self_exchange)
       .def_readwrite("graphs", &EngineConfig::graphs)
       .def_readwrite("watchdog_s", &EngineConfig::watchdog_s);
 

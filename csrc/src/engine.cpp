@@ -41,7 +41,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // (profiles/sweep_epoch_group.jsonl; 4T is 4 % slower), so one rank uses 8T
   // and several ranks 16T: half the RCCL exchanges (4 per 1000 generations),
   // each one latency-bound.
-  int D = cfg_.epoch > 0 ? cfg_.epoch : (tr_->size() > 1 ? 16 : 8) * tmax_;
+  const bool row_exchange = dec_.Py > 1 || cfg_.self_exchange;
+  int D = cfg_.epoch > 0 ? cfg_.epoch : (tr_->size() > 1 || cfg_.self_exchange ? 16 : 8) * tmax_;
   if (dec_.Py > 1) D = int(std::min<int64_t>(D, min_tile_rows(dec_)));
   if (dec_.Px > 1) {
     int64_t cap = 32 * (min_tile_cols(dec_) / 32);
@@ -70,8 +71,15 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // epoch), which on the 32768 x 4096 per-rank tile cost 4x more than the
   // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
   const bool interior = min_tile_rows(dec_) >= 2 * int64_t(D_) + 1;  // on every rank
-  overlap_ = dec_.Py > 1 && cfg_.overlap == 2 && interior;
-  early_ = dec_.Py > 1 && dec_.Px == 1 && (cfg_.overlap == -1 || cfg_.overlap == 1) && interior;
+  overlap_ = row_exchange && cfg_.overlap == 2 && interior;
+  early_ = row_exchange && dec_.Px == 1 && cfg_.overlap == 1 && interior;
+  // With the early-boundary schedule every transport operation runs on the
+  // comm stream (one stream per communicator, in issue order), so the flag
+  // all-reduce of a poll runs beside the compute stream.  Not by default: in
+  // the one-GPU RCCL rehearsal each cross-stream event hop around an exchange
+  // cost more than the all-reduce it takes off the compute stream
+  // (profiles/r02/rehearsal_overlap.jsonl).
+  comm_route_ = early_;
   if (overlap_) {
     gs_ = TileGeom::make(cfg_.layout, D_, g_.W, D_, g_.hw);
     GOL_REQUIRE(gs_.pitch == g_.pitch, "edge scratch pitch mismatch");
@@ -84,7 +92,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
-  if (use_graphs_) early_ = false;  // captured epochs stay on one stream
+  if (use_graphs_) early_ = comm_route_ = false;  // captured epochs stay on one stream
   gen_ = cfg_.start_gen;
 }
 
@@ -196,7 +204,7 @@ void Engine::halo_exchange() {
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
   const int64_t H = g_.H, pitch = g_.pitch;
-  if (dec_.Px == 1 && dec_.Py == 1) {  // one rank: both periodic fills, one launch
+  if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange) {  // one rank: both periodic fills, one launch
     be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/true);
     ++exchanges_;
     return;
@@ -204,7 +212,7 @@ void Engine::halo_exchange() {
   // Phase A: west/east halo columns of the owned rows.
   exchange_columns(buf);
   // Phase B: north/south halo rows over the full padded width.
-  if (dec_.Py == 1) {
+  if (dec_.Py == 1 && !cfg_.self_exchange) {
     be_->fill_periodic(buf, g_, /*cols=*/false, /*rows=*/true);
   } else {
     const int64_t Dv = g_.Dv;
@@ -320,16 +328,16 @@ void Engine::run_epoch(int64_t d) {
 }
 
 void* Engine::rccl_stream() const {
-  void* c = early_ ? be_->comm_stream() : nullptr;
+  void* c = (comm_route_ || early_) ? be_->comm_stream() : nullptr;
   return c ? c : be_->stream();
 }
 
 void Engine::comm_after_compute() {
-  if (void* c = early_ ? be_->comm_stream() : nullptr) be_->stream_wait(c, be_->stream_mark(nullptr));
+  if (void* c = (comm_route_ || early_) ? be_->comm_stream() : nullptr) be_->stream_wait(c, be_->stream_mark(nullptr));
 }
 
 void Engine::compute_after_comm() {
-  if (void* c = early_ ? be_->comm_stream() : nullptr) be_->stream_wait(nullptr, be_->stream_mark(c));
+  if (void* c = (comm_route_ || early_) ? be_->comm_stream() : nullptr) be_->stream_wait(nullptr, be_->stream_mark(c));
 }
 
 void Engine::settle_pending(bool invalidate) {
@@ -346,21 +354,25 @@ void Engine::settle_pending(bool invalidate) {
 // every halo before computing (MPI_Startall + MPI_Waitall, src/game_mpi.c:
 // 392-401).  Here the last temporal block of a full epoch writes exactly the
 // owned rows, and the next epoch's halos are the first and last D of them.
-// So that block runs as three launches: the two boundary strips, then - with
-// their periodic column halos filled and the row exchange started on the comm
-// stream - the interior, which the exchange overlaps.  The next epoch's first
-// block waits for the arrival mark.  Every row is still computed once, so
-// the per-generation flags of the three launches OR together exactly.
+// So that block is split: on the comm stream, one dual launch computes the two
+// D-row boundary strips, fills their periodic column halos and starts the row
+// exchange; on the compute stream the interior runs at the same time (the
+// GPU runs both kernels concurrently: the boundary launch has few waves).  The
+// next epoch's first block waits for the exchange's arrival mark.  Every row
+// is still computed once, so the per-generation flags of both launches OR
+// together exactly; the poll's flag reduction is ordered after both.
 void Engine::last_block_early(int T) {
   trace::Range tr("gol.last_block_early");
   const int64_t Dv = g_.Dv, H = g_.H, D = D_, pitch = g_.pitch;
   void* in = buf_[cur_];
   void* out = buf_[cur_ ^ 1];
   auto* base = static_cast<uint8_t*>(out);
-  const int drift = launch(in, out, g_, T, Dv, Dv + D, gen_);  // top boundary rows
-  launch(in, out, g_, T, Dv + H - D, Dv + H, gen_);            // bottom boundary rows
-  be_->fill_cols_rows(out, g_, Dv, D);
-  be_->fill_cols_rows(out, g_, Dv + H - D, D);
+  void* comm = be_->comm_stream();
+  if (comm) be_->stream_wait(comm, be_->stream_mark(nullptr));  // this block's input is complete
+  // Boundary strips [Dv, Dv + D) and [Dv + H - D, Dv + H), one launch.
+  const int drift = launch(in, out, g_, T, Dv, Dv + D, gen_, comm, H - D, /*prio_boost=*/true);
+  be_->fill_cols_rows(out, g_, Dv, D, comm);
+  be_->fill_cols_rows(out, g_, Dv + H - D, D, comm);
   auto nb = dec_.neighbors(rank_);
   const size_t bytes = size_t(Dv * pitch);
   std::vector<P2POp> ops = {
@@ -369,15 +381,13 @@ void Engine::last_block_early(int T) {
       {true, nb[kSouth], base + H * pitch, bytes},
       {false, nb[kNorth], base, bytes},
   };
-  void* comm = be_->comm_stream();
-  if (comm) be_->stream_wait(comm, be_->stream_mark(nullptr));
   tr_->exchange(ops, comm ? comm : be_->stream());
   rows_arrived_ = comm ? be_->stream_mark(comm) : nullptr;
   rows_pending_ = true;
   halo_bytes_ += 2 * int64_t(bytes);
   ++exchanges_;
   ++early_sends_;
-  launch(in, out, g_, T, Dv + D, Dv + H - D, gen_);  // interior, overlapping the exchange
+  launch(in, out, g_, T, Dv + D, Dv + H - D, gen_);  // interior, concurrent with the above
   be_->fill_cols_rows(out, g_, Dv + D, H - 2 * D);
   add_drift(drift);
   cur_ ^= 1;
@@ -385,7 +395,7 @@ void Engine::last_block_early(int T) {
 }
 
 int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
-                   int64_t gen_base) {
+                   int64_t gen_base, void* stream, int64_t dual_offset, bool prio_boost) {
   BlockArgs a;
   a.in = in;
   a.out = out;
@@ -405,6 +415,9 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   }
   a.flags_base = flags_base_;
   a.allow_drift = drift_ok_;
+  a.stream = stream;
+  a.dual_offset = dual_offset;
+  a.prio_boost = prio_boost;
   const int drift = be_->run_block(a);
   ++launches_;
   return drift;
@@ -432,7 +445,7 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   uint32_t* dev = flags_ + (from + 1 - flags_base_);
   // Early-boundary schedule: reduce and copy on the comm stream, off the
   // compute stream's critical path, in issue order with the halo exchanges.
-  void* comm = early_ ? be_->comm_stream() : nullptr;
+  void* comm = (comm_route_ || early_) ? be_->comm_stream() : nullptr;
   comm_after_compute();
   if (tr_->size() > 1) tr_->allreduce_max_u32(dev, size_t(n), rccl_stream());
   be_->copy_d2h_async_on(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t), comm);

@@ -35,8 +35,11 @@ void ThreadTransport::fault_delay() {
 // Rendezvous exchange: sends publish the sender's buffer, the receiver copies
 // straight out of it (device-to-device for HIP backends on one device) and
 // marks it consumed; the sender returns once all its messages are consumed.
-void ThreadTransport::exchange(const std::vector<P2POp>& ops, void*) {
-  backend_->synchronize();  // sender data must be complete before publishing
+void ThreadTransport::exchange(const std::vector<P2POp>& ops, void* stream) {
+  // Sender data must be complete before publishing: it may come from the
+  // compute stream or from the stream the engine enqueued this exchange on.
+  backend_->synchronize();
+  if (stream) backend_->synchronize_stream(stream);
   fault_delay();
   std::vector<std::shared_ptr<ThreadHub::Msg>> sent;
   {
@@ -86,7 +89,8 @@ void ThreadTransport::exchange(const std::vector<P2POp>& ops, void*) {
   });
 }
 
-void ThreadTransport::allreduce_max_u32(uint32_t* buf, size_t n, void*) {
+void ThreadTransport::allreduce_max_u32(uint32_t* buf, size_t n, void* stream) {
+  if (stream) backend_->synchronize_stream(stream);  // flags written on that stream
   std::vector<uint32_t> local(n);
   backend_->copy_d2h(local.data(), buf, n * sizeof(uint32_t));
   std::unique_lock<std::mutex> lk(hub_->mu);

@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <unistd.h>
+
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -28,6 +31,26 @@
 namespace gol {
 namespace {
 
+// RCCL prints a version banner ("RCCL version : ...", HIP/ROCm versions,
+// hostname, library path) to stdout when the library initialises.  Stdout
+// belongs to the program: the reference's "Generations:" lines, bench.py's
+// one JSON line.  Library initialisation runs with fd 1 pointed at stderr.
+struct StdoutToStderr {
+  int saved = -1;
+  StdoutToStderr() {
+    std::fflush(stdout);
+    saved = dup(1);
+    if (saved >= 0) dup2(2, 1);
+  }
+  ~StdoutToStderr() {
+    std::fflush(stdout);
+    if (saved >= 0) {
+      dup2(saved, 1);
+      close(saved);
+    }
+  }
+};
+
 class RcclTransport final : public Transport {
  public:
   RcclTransport(const std::vector<uint8_t>& uid, int rank, int nranks, int device)
@@ -36,7 +59,10 @@ class RcclTransport final : public Transport {
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     if (hipSetDevice(dev_) != hipSuccess) fail("hipSetDevice failed for RCCL transport");
-    NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+    {
+      StdoutToStderr quiet;
+      NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+    }
     if (hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking) != hipSuccess)
       fail("hipStreamCreate failed");
     if (hipMalloc(&barrier_buf_, 64) != hipSuccess) fail("hipMalloc failed");
@@ -88,7 +114,10 @@ class RcclTransport final : public Transport {
 
 std::vector<uint8_t> rccl_unique_id() {
   ncclUniqueId id;
-  NCCL_CHECK(ncclGetUniqueId(&id));
+  {
+    StdoutToStderr quiet;
+    NCCL_CHECK(ncclGetUniqueId(&id));
+  }
   std::vector<uint8_t> v(sizeof(id));
   std::memcpy(v.data(), &id, sizeof(id));
   return v;

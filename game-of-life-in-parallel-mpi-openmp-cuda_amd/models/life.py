@@ -47,6 +47,7 @@ class LifeConfig:
     start_gen: int = 0          # resume: generation number of the initial state
     sim_phase: int = 0          # resume: similarity counter at start_gen
     timing_barriers: bool = True  # barrier + sync around each run's loop (off: the caller brackets it)
+    self_exchange: bool = False   # rehearse the multi-rank row-halo schedule on one rank (transport to self)
 
     def resolved_layout(self) -> str:
         if self.layout == "auto":
@@ -74,6 +75,7 @@ class LifeConfig:
         c.start_gen = int(self.start_gen)
         c.sim_phase = int(self.sim_phase)
         c.timing_barriers = bool(self.timing_barriers)
+        c.self_exchange = bool(self.self_exchange)
         return c
 
 

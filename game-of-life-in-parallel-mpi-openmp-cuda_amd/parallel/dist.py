@@ -17,9 +17,11 @@ transport is one of:
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import datetime
 import os
+import sys
 from typing import Optional
 
 import numpy as np
@@ -33,6 +35,22 @@ def env_rank() -> tuple[int, int, int]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     return rank, world, local
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """fd 1 -> stderr inside the block.  RCCL prints a version banner to stdout
+    when a communicator is created; stdout carries the program's own output
+    (the reference's stdout lines, bench.py's JSON line)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def init_process_group(backend: Optional[str] = None, timeout_s: int = 600):
@@ -51,8 +69,11 @@ def init_process_group(backend: Optional[str] = None, timeout_s: int = 600):
     if backend == "nccl":
         torch.cuda.set_device(local)
         kw["device_id"] = torch.device("cuda", local)
-    dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    with stdout_to_stderr():
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        if backend == "nccl":
+            dist.barrier()  # creates torch's communicator now, while stdout is diverted
     return dist
 
 

@@ -381,6 +381,36 @@ def test_rccl_single_rank_self_exchange(gpu):
     assert flags.tolist() == [3, 0, 7]
 
 
+@pytest.mark.parametrize("overlap", ["off", "on", "edges"])
+@pytest.mark.parametrize("xlane", [0, -1])
+def test_rccl_self_exchange_rehearsal(gpu, monkeypatch, overlap, xlane):
+    """The multi-rank row-strip schedule on one GPU (bench.py --rehearse-rccl):
+    row halos through a 1-rank RCCL communicator sending to itself on the
+    comm stream, early-boundary dual launch concurrent with the interior,
+    against the fp32 conv oracle and the exact Generations."""
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    C = gpu
+    W, H = 32 * 96, 1200
+    g = random_grid(W, H, 31)
+    gens = 300
+    want = life_step_torch(g, gens, device="cuda")
+    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0)
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=12 if xlane else 16, epoch=96, overlap=overlap,
+                                self_exchange=True), transport=tr, backend=C.hip_backend(0))
+    sim.load(g)
+    rep = sim.advance(gens)
+    assert rep.exchanges >= gens // 96 and rep.overlapped == (overlap != "off")
+    assert (sim.tile() == want).all()
+    for cw, ch, seed, density in [c for c in CONVERGING if c[0] % 32 == 0]:
+        grid = random_grid(cw, ch, seed, density)
+        ref, rgens, _ = reference_run(grid)
+        s2 = Simulation(LifeConfig(cw, ch, tmax=4, epoch=8, poll_gens=16, overlap=overlap, self_exchange=True),
+                        transport=tr, backend=C.hip_backend(0))
+        s2.load(grid)
+        assert s2.run().generations == rgens
+        assert (s2.tile() == ref).all()
+
+
 def test_torch_tensor_views_of_engine_buffers(gpu):
     import torch
 

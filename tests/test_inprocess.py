@@ -95,17 +95,18 @@ def test_overlapped_termination(native, W, H, seed, density, lagged, mode):
 
 
 def test_overlap_modes(native):
-    """auto = on = early boundary rows on row strips with H > 2D; edges = the
-    round-1 edge-strip schedule; off; column decompositions do not overlap."""
+    """on = early boundary rows on row strips with H > 2D; edges = the
+    round-1 edge-strip schedule; auto only moves the transport operations to
+    the comm stream; column decompositions do not overlap."""
     def ov(**kw):
         cfg = dict(decomp="1x2", tmax=4, epoch=16)
         cfg.update(kw)
         H = cfg.pop("H", 512)
         return InProcessGroup(LifeConfig(64, H, **cfg), 2, engine="cpu").sims[0].native_engine.overlap()
-    assert ov() and ov(overlap="on") and ov(overlap="edges")
-    assert not ov(overlap="off")
-    assert not ov(H=40)  # tile rows 20 <= 2D
-    assert not ov(decomp="2x1")
+    assert ov(overlap="on") and ov(overlap="edges")
+    assert not ov() and not ov(overlap="off")
+    assert not ov(H=40, overlap="on")  # tile rows 20 <= 2D
+    assert not ov(decomp="2x1", overlap="on")
 
 
 @pytest.mark.parametrize("lagged", [True, False])
@@ -207,4 +208,23 @@ def test_overlap_decision_is_global_on_uneven_tiles(native, mode):
     grp.load(g)
     reps = grp.run()
     assert {r.generations for r in reps} == {rgens}
+    assert (grp.gather() == ref).all()
+
+
+@pytest.mark.parametrize("overlap", ["off", "on", "edges"])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_self_exchange_rehearsal(native, overlap, layout):
+    """One rank rehearsing the multi-rank row-strip schedule (bench.py
+    --rehearse-rccl): halos go through the transport to itself, with the
+    multi-rank epoch depth and overlap; results equal the serial loop."""
+    W, H = 128, 200
+    g = random_grid(W, H, 12)
+    ref, rgens, _ = reference_run(g, 120)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=120, layout=layout, tmax=4, epoch=16, overlap=overlap,
+                                    self_exchange=True), 1, engine="cpu")
+    grp.load(g)
+    (rep,) = grp.run()
+    assert rep.generations == rgens
+    assert rep.exchanges >= 120 // 16 and rep.halo_bytes > 0
+    assert rep.overlapped == (overlap != "off")
     assert (grp.gather() == ref).all()
