@@ -5,6 +5,7 @@ regular objects.  bench.py loads one with GOL_NATIVE_SO=alt_so/<name>/_gol.so,
 so several kernel builds can be A/B-timed in one GPU call on one device.
 
     python scripts/build_alt.py epi4 -DGOL_EPI_SCHED=4 -DGOL_GROUP_T16_WAVES=3
+    python scripts/build_alt.py add12 --tu=kernels/life_block_bits_w1_add.hip -DGOL_GROUP_T16_ADD_WAVES=4
 """
 import sys
 from pathlib import Path
@@ -16,8 +17,10 @@ from gol_amd import native_build as nb  # noqa: E402
 
 def main() -> int:
     name, flags = sys.argv[1], sys.argv[2:]
-    nb.build()
     tu = "kernels/life_block_bits_w1_dpp.hip"
+    if flags and flags[0].startswith("--tu="):
+        tu, flags = flags[0][5:], flags[1:]
+    nb.build()
     obj = nb.BUILD / f"alt_{name}.o"
     cmd = nb._compile_cmd(nb.CSRC / tu, obj)
     i = cmd.index("-c")
