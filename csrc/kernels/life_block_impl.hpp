@@ -349,9 +349,9 @@ __device__ __forceinline__ Vec<W> levels_full(Levels<T, W>& st, const Vec<W>& cu
 // Triangular prologue, fully unrolled: at step K only levels 1..K/2 hold
 // valid rows, so only those are evaluated; level K/2+1 just fills its
 // window.
-template <int T, class IO, int K, class Save, class Bottom>
-__device__ __forceinline__ void prologue_tri(Levels<T, IO::W>& st, RowReader<IO>& rd, const Save& save,
-                                             const Bottom& bottom) {
+// RD: RowReader<IO>, or any source with take<S>(k) (life_pipe_impl.hpp's ring).
+template <int T, class IO, int K, class Save, class Bottom, class RD>
+__device__ __forceinline__ void prologue_tri(Levels<T, IO::W>& st, RD& rd, const Save& save, const Bottom& bottom) {
   if constexpr (K < 2 * T) {
     constexpr int S = K % 3;
     constexpr int nfull = K / 2;
@@ -360,7 +360,7 @@ __device__ __forceinline__ void prologue_tri(Levels<T, IO::W>& st, RowReader<IO>
     // in0 + nfull + 1 (K odd) are the top boundary state.
     if constexpr (nfull >= 1 && nfull < T) save(nfull, K - 2 * nfull, cur);
     if constexpr (nfull < T) level_store<T, IO, S, nfull>(st, cur);
-    prologue_tri<T, IO, K + 1, Save, Bottom>(st, rd, save, bottom);
+    prologue_tri<T, IO, K + 1>(st, rd, save, bottom);
   }
 }
 

@@ -5,10 +5,13 @@
 //            the rows allow M segments of 2T rows per group (GOL_GROUP)
 //   short    life_short_kernel (life_short_impl.hpp): grouped, segments of
 //            Q < 2T rows, when the makespan model prefers it (GOL_SHORT)
+//   pipe     life_pipe_kernel (life_pipe_impl.hpp): grouped, each segment's
+//            levels split over a wave pair (GOL_PIPE)
 //   classic  life_block_kernel: T < 4, short tiles, GOL_GROUP=0, GOL_SKEW=1
 //   split    life_block_kernel<SPLIT> + life_split_down_kernel: GOL_SPLIT=1
 #pragma once
 
+#include "life_pipe_impl.hpp"
 #include "life_short_impl.hpp"
 
 namespace gol {
@@ -60,6 +63,23 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
                               : -1.0;
         if (cs > 0 && (tune.short_seg == 2 || (better(cs, c4) && better(cs, c8) && better(cs, cc))))
           return launch_short<T, IO, 8>(s8, s);
+      }
+      // Level-pipelined pairs (T/2 + T/2 levels): twice the waves per SIMD.
+      if constexpr (IO::kBits && IO::W == 1 && (T == 12 || T == 16) &&
+                    (IO::XL == kXlaneDpp || IO::XL == kXlaneAdd)) {
+        constexpr int T1 = T / 2, T2 = T - T / 2;
+        if (tune.pipe && dual == 1) {
+          LifeBlockParams p8 = p, p4 = p;
+          const double cp8 = plan_pipe<T1, T2, 8>(p8, out_rows, simds, pipe_waves_per_simd<T1, T2, IO, 8>(),
+                                                  tune.target_waves, IO::XL);
+          const double cp4 = plan_pipe<T1, T2, 4>(p4, out_rows, simds, pipe_waves_per_simd<T1, T2, IO, 4>(),
+                                                  tune.target_waves, IO::XL);
+          const bool forced = tune.pipe == 2;
+          const bool use8 = cp8 > 0 && (better(cp8, cp4) || cp4 < 0);
+          const double cp = use8 ? cp8 : cp4;
+          if (cp > 0 && (forced || (better(cp, c4) && better(cp, c8) && better(cp, cc))))
+            return use8 ? launch_pipe<T1, T2, IO, 8>(p8, s) : launch_pipe<T1, T2, IO, 4>(p4, s);
+        }
       }
       if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
       if (better(c8, cc)) return launch_group<T, IO, 8>(g8, s);

@@ -78,6 +78,7 @@ struct LifeTuning {
   int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
   int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
+  int pipe = 0;             // level-pipelined wave pairs (life_pipe_impl.hpp): 0 off, 1 by the model, 2 forced
   uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
   uint32_t* err = nullptr;       // LifeBlockParams::err
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).

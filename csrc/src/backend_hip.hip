@@ -68,6 +68,7 @@ class HipBackend final : public Backend {
     // Short-segment groups (life_short_impl.hpp): exact, but 10-20 % slower
     // than the grouped kernel on the per-rank tile (profiles/sweep_short_segments.jsonl).
     tune_.short_seg = env_int("GOL_SHORT", 0);
+    tune_.pipe = env_int("GOL_PIPE", 0);
     if (const char* t = std::getenv("GOL_WG_TRACE")) {
       const std::string v(t);
       const size_t c = v.find(':');

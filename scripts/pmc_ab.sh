@@ -5,10 +5,12 @@
 set -euo pipefail
 export TMPDIR=/tmp
 args="$1"; shift
+# PMC="<counters>" overrides the default set (at most 8 SQ_ counters per pass).
+PMC=${PMC:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"}
 mkdir -p gpurun_out/pmc_ab
 for spec in "$@"; do
   IFS=: read -r label envs <<< "$spec"
-  env $envs timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE \
+  env $envs timeout -s KILL 120 rocprofv3 --pmc $PMC \
     --output-format csv -d gpurun_out/pmc_ab/$label -o run -- python3 bench.py $args > gpurun_out/pmc_ab/$label.json 2> gpurun_out/pmc_ab/$label.err
 done
 python3 - "$@" <<'PY'

@@ -192,6 +192,42 @@ def test_short_segment_schedule_termination(gpu, monkeypatch, xlane, tmax):
         assert (out == ref).all(), layout
 
 
+@pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
+@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (3, 16), (0, 12)])
+def test_pipe_schedule_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
+    """Level-pipelined wave pairs (csrc/kernels/life_pipe_impl.hpp: stage A
+    runs levels 0..T/2-1 and hands its rows to stage B through an LDS ring)
+    forced on, against the fp32 conv oracle; several group shapes via the
+    wave-count target."""
+    monkeypatch.setenv("GOL_PIPE", "2")
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    g = random_grid(W, H, W * 5 + H)
+    want = life_step_torch(g, 2 * tmax + 11, device="cuda")
+    for target in ("0", "100000", "3000"):
+        monkeypatch.setenv("GOL_TARGET_WAVES", target)
+        sim = Simulation(LifeConfig(W, H, gen_limit=2 * tmax + 11, tmax=tmax), engine="hip")
+        assert "pipe=forced" in sim.describe()["backend"]
+        sim.load(g)
+        sim.advance(2 * tmax + 11)
+        assert (sim.tile() == want).all(), target
+
+
+@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
+def test_pipe_schedule_termination(gpu, monkeypatch, xlane, tmax):
+    """Exact Generations with the pipelined pairs: both stages raise their
+    levels' change flags."""
+    monkeypatch.setenv("GOL_PIPE", "2")
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    monkeypatch.setenv("GOL_TARGET_WAVES", "100000")
+    grid = np.zeros((1024, 512), dtype=np.uint8)
+    W, H, seed, density = CONVERGING[5]
+    grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(grid)
+    out, rep = simulate(grid, 1000, engine="hip", tmax=tmax)
+    assert rep.generations == rgens
+    assert (out == ref).all()
+
+
 def test_grouped_schedule_is_the_default(gpu):
     sim = Simulation(LifeConfig(4096, 2048), engine="hip")
     assert "group=8" in sim.describe()["backend"]
