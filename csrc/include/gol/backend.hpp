@@ -82,6 +82,10 @@ class Backend {
   // Whether run_block may drift the frame for this layout when allowed
   // (the engine then sizes the left halo for the one-sided light cone).
   virtual bool drifts(Layout) const { return false; }
+  // Whether run_block honours BlockArgs::full_width for this layout (wraps
+  // column reads within the owned words): the engine then skips the periodic
+  // column fills of whole-width tiles.
+  virtual bool wraps_columns(Layout) const { return false; }
   // Owned rows of src rotated left by `shift` cells (0 < shift < W) into dst:
   // dst cell x = src cell (x + shift) mod W.  Halos of dst are not written.
   virtual void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) = 0;

@@ -88,6 +88,9 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   p.err = tune.err;
   p.row_alt = a.dual_offset;
   p.prio_boost = a.prio_boost ? 1 : 0;
+  p.wrap_w = a.full_width && tune.wrap && g.W % 32 == 0 ? int(g.W / 32) : 0;
+  p.fold = 1;
+  p.fold_lanes = 64;
   const int64_t rows = a.row_hi - a.row_lo;
   int x = xlane_of(g.layout, w, tune);
   if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {

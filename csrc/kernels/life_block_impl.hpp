@@ -114,6 +114,69 @@ __device__ __forceinline__ bool wave_halo(int lane, int i) {
   return (lane == 0 && i == 0) || (XL != kXlaneAdd && lane == 63 && i == W - 1);
 }
 
+// Column map of one lane (all life_block kernels).
+//   Halo mode (p.wrap_w == 0): the lane's words are padded-row words
+//   kcol * kWaveOut - 1 + W * lane + i; the engine keeps the halo columns
+//   valid (periodic fill or column exchange).
+//   Wrap mode (p.wrap_w > 0: the tile is the whole torus width, Px == 1): the
+//   lane's logical words lc = kcol * kWaveOut - 1 + W * lane + i are owned
+//   words mod wrap_w, read at own_w0 + (lc mod wrap_w); halo columns are
+//   neither read nor written, and the strips cover wrap_w words instead of
+//   the padded width.
+//   Folded strip (wrap mode, W == 1, life_group_kernel): the narrow last strip
+//   of rem words is packed `nsub` times into one wave, as sub-strips of
+//   sub_lanes = rem + halo lanes each; lane = sub * sub_lanes + j, and sub
+//   runs the rows of another group (life_group_impl.hpp).
+template <class IO>
+struct LaneCols {
+  static constexpr int W = IO::W;
+  int store_col;  // Writer::col (padded word of the lane's word 0)
+  int sub;        // sub-strip of a folded strip (0 otherwise)
+  bool ok[W], own[W];
+  int off[W];
+  uint32_t fmask[W];
+};
+
+template <class IO>
+__device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int kcol, int lane, int sub_lanes = 64,
+                                                  int nsub = 1) {
+  constexpr int W = IO::W, XL = IO::XL;
+  constexpr int kWaveOut = wave_out_words<XL, W>();
+  LaneCols<IO> c;
+  int j = lane;
+  c.sub = 0;
+  if (sub_lanes < 64) {
+    c.sub = lane / sub_lanes;
+    j = lane - c.sub * sub_lanes;
+  }
+  const int lc0 = kcol * kWaveOut - 1 + W * j;
+  if (p.wrap_w == 0) {
+    c.store_col = lc0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      const int cc = lc0 + i;
+      c.ok[i] = cc >= 0 && cc < p.Wp;
+      c.own[i] = c.ok[i] && !wave_halo<XL, W>(lane, i);
+      c.fmask[i] = (c.own[i] && cc >= p.own_w0 && cc < p.own_w1) ? (cc == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
+      c.off[i] = min(max(cc, 0), p.Wp - 1);
+    }
+    return c;
+  }
+  const int ww = p.wrap_w;
+  c.store_col = p.own_w0 + lc0;
+  const bool live = c.sub < nsub;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const int lc = lc0 + i;
+    const bool halo = sub_lanes < 64 ? (j == 0 || (XL != kXlaneAdd && j == sub_lanes - 1)) : wave_halo<XL, W>(lane, i);
+    c.ok[i] = true;
+    c.own[i] = live && !halo && lc >= 0 && lc < ww;
+    c.fmask[i] = c.own[i] ? (lc == ww - 1 ? p.last_mask : ~0u) : 0u;
+    c.off[i] = p.own_w0 + ((lc % ww) + ww) % ww;
+  }
+  return c;
+}
+
 // One-sided window for the adder mode: l1 = cells x-1, l2 = cells x-2 at bit
 // x.  v_add_co_u32 doubles a word (shift left by one) and leaves every lane's
 // top bit in an SGPR-pair lane mask; s_lshl_b64 moves each mask bit one lane
@@ -433,6 +496,9 @@ struct BottomSaver {
 // per-lane `if (own) store` puts an exec-masked block around every row store;
 // in the grouped kernel's straight-line epilogue those 32 blocks drove hipcc
 // to 400 registers.
+// Folded strips (LaneCols::sub) store rows of several groups from one wave:
+// lane rows sit `roff` bytes below the wave's row, and the descriptor spans
+// `nrec` bytes (0: one row).
 template <class IO>
 struct Writer {
   static constexpr int W = IO::W;
@@ -441,10 +507,13 @@ struct Writer {
   int64_t pitch;
   int col;
   bool own[W];
+  int roff = 0;
+  int nrec = 0;
   __device__ __forceinline__ void row(int64_t r, const Vec<W>& v) const {
-    const BufRsrc rs = __builtin_amdgcn_make_buffer_rsrc(out + r * pitch, short(0), int(pitch), kBufFlags);
+    const BufRsrc rs =
+        __builtin_amdgcn_make_buffer_rsrc(out + r * pitch, short(0), nrec ? nrec : int(pitch), kBufFlags);
 #pragma unroll
-    for (int i = 0; i < W; ++i) IO::store_buf(rs, own[i] ? (col + i) * IO::kWordBytes : kDrop, v.w[i]);
+    for (int i = 0; i < W; ++i) IO::store_buf(rs, own[i] ? (col + i) * IO::kWordBytes + roff : kDrop, v.w[i]);
   }
 };
 
@@ -534,7 +603,6 @@ template <int T, class IO, bool SKEW, bool SPLIT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<T, IO, SKEW, SPLIT>())))
 void life_block_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
-  constexpr int kWaveOut = wave_out_words<IO::XL, W>();  // words produced per wave
   const int lane = threadIdx.x & 63;
   // readfirstlane: the wave index is uniform, so everything derived from it
   // (segment bounds, loop trip counts) lives in SGPRs with scalar branches.
@@ -555,21 +623,18 @@ void life_block_kernel(const LifeBlockParams p) {
   const int64_t o1 = SPLIT ? s1 - T : s1;
   if (!SPLIT && o0 >= o1) return;  // wave-uniform
 
-  // Lane words: col .. col+W-1 (padded word index); the wave's first and
-  // last words are halo words.
-  const int col = kcol * kWaveOut - 1 + W * lane;
+  // Lane words (lane_cols): the wave's first and last words are halo words.
+  const LaneCols<IO> lc = lane_cols<IO>(p, kcol, lane);
+  const int col = lc.store_col;
   const int64_t pitch = p.pitch;
   RowReader<IO> rd;
   Writer<IO> wr;
   uint32_t fmask[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    const int c = col + i;
-    const bool ok = c >= 0 && c < p.Wp;
-    const bool halo = wave_halo<IO::XL, W>(lane, i);
-    rd.ok[i] = ok;
-    wr.own[i] = ok && !halo;
-    fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
+    rd.ok[i] = lc.ok[i];
+    wr.own[i] = lc.own[i];
+    fmask[i] = lc.fmask[i];
   }
 
   if (p.prio_boost) __builtin_amdgcn_s_setprio(3);  // wave-uniform
@@ -590,7 +655,7 @@ void life_block_kernel(const LifeBlockParams p) {
   rd.pitch = pitch;
   rd.kmax = kend - 1;
 #pragma unroll
-  for (int i = 0; i < W; ++i) rd.off[i] = min(max(col + i, 0), p.Wp - 1);
+  for (int i = 0; i < W; ++i) rd.off[i] = lc.off[i];
   rd.init();
   wr.out = p.out + (o0 - T) * pitch;  // level-T row of step k: o0 - 2T + k
   wr.pitch = pitch;

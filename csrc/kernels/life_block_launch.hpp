@@ -25,10 +25,27 @@ constexpr int kSplitMaxRowsPerT = 8;
 
 template <int T, class IO>
 void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
-  p.ncolw = int(ceil_div(p.Wp, wave_out_words<IO::XL, IO::W>()));
+  constexpr int kWaveOut = wave_out_words<IO::XL, IO::W>();
+  // Wrap mode (p.wrap_w > 0) covers the owned words only (lane_cols).
+  p.ncolw = int(ceil_div(p.wrap_w ? p.wrap_w : p.Wp, kWaveOut));
   // A dual launch (two row ranges) has twice the waves per segment plan:
   // the planners see 2 x ncolw strips, the kernels map the second half.
   const int dual = p.row_alt ? 2 : 1;
+  // Folded last strip (grouped kernel): 32768 cells are 16 strips of 63
+  // words + 16 words; the last strip's 17 lanes fit three times in a wave,
+  // so it costs a third of a strip instead of a whole one.  Lane offsets of
+  // a folded wave span its groups' rows in one descriptor (< 2^30 bytes).
+  p.fold = 1;
+  p.fold_lanes = 64;
+  if (p.wrap_w && IO::W == 1 && dual == 1 && tune.fold && p.ncolw >= 2 &&
+      (out_rows + 2) * p.pitch < (int64_t(1) << 30)) {
+    const int lanes = p.wrap_w - (p.ncolw - 1) * kWaveOut + (IO::XL == kXlaneAdd ? 1 : 2);
+    const int f = std::min(4, 64 / lanes);
+    if (f >= 2) {
+      p.fold = f;
+      p.fold_lanes = lanes;
+    }
+  }
   const int simds = 4 * std::max(1, tune.cus) / dual;
   if constexpr (T >= 4) {
     if (tune.group != 0 && (tune.split == 0 || dual == 2) && !tune.skew) {
@@ -84,8 +101,9 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
       if (better(c8, cc)) return launch_group<T, IO, 8>(g8, s);
     }
-    bool split = tune.split > 0 && IO::XL != kXlaneAdd && dual == 1;
-    if (tune.split < 0 && !tune.skew && IO::XL != kXlaneAdd && dual == 1) {
+    // The split kernels address boundary states by padded column: halo mode only.
+    bool split = tune.split > 0 && IO::XL != kXlaneAdd && dual == 1 && p.wrap_w == 0;
+    if (tune.split < 0 && !tune.skew && IO::XL != kXlaneAdd && dual == 1 && p.wrap_w == 0) {
       LifeBlockParams q = p;
       plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves);
       split = q.seg_rows < kSplitMaxRowsPerT * T;

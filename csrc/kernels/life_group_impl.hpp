@@ -189,7 +189,6 @@ template <int T, class IO, int M>
 __global__ __launch_bounds__(64 * M) __attribute__((amdgpu_waves_per_eu(group_min_waves<T, IO>())))
 void life_group_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
-  constexpr int kWaveOut = wave_out_words<IO::XL, W>();
   constexpr int kSlot = (T - 1) * 2 * W * 64;  // dwords per boundary
   __shared__ uint32_t saved[M * kSlot];
   const int lane = threadIdx.x & 63;
@@ -202,10 +201,27 @@ void life_group_kernel(const LifeBlockParams p) {
     blk -= p.ncolw * p.nseg;
     roff = p.row_alt;
   }
-  const int kcol = blk / p.nseg;
-  const int grp = blk - kcol * p.nseg;
-  const int64_t G0 = p.row_lo + roff + int64_t(grp) * p.seg_rows + min(grp, p.seg_rem);
-  const int64_t G1 = G0 + p.seg_rows + (grp < p.seg_rem ? 1 : 0);
+  // Folded last strip (wrap mode): one block runs p.fold groups of the
+  // narrow last strip side by side in lane sub-strips.  Every sub-strip then
+  // takes the largest group size (a smaller group starts one row early and
+  // recomputes its upper neighbour's last row, identically), so the wave's
+  // control flow is the same for all of them; lanes carry their group's row
+  // offset in their read / store offsets.
+  int kcol, grp, nsub = 1, sub_lanes = 64;
+  if (p.fold > 1 && blk >= (p.ncolw - 1) * p.nseg) {
+    kcol = p.ncolw - 1;
+    grp = (blk - kcol * p.nseg) * p.fold;
+    nsub = p.fold;
+    sub_lanes = p.fold_lanes;
+  } else {
+    kcol = blk / p.nseg;
+    grp = blk - kcol * p.nseg;
+  }
+  const auto group_end = [&](int g) {
+    return p.row_lo + roff + int64_t(g) * p.seg_rows + min(g, p.seg_rem) + p.seg_rows + (g < p.seg_rem ? 1 : 0);
+  };
+  const int64_t G1 = group_end(grp);
+  const int64_t G0 = G1 - p.seg_rows - (nsub > 1 ? (p.seg_rem > 0 ? 1 : 0) : (grp < p.seg_rem ? 1 : 0));
   const int64_t in0 = G0 + int64_t(m) * p.grp_q - T;
   const bool last = m == M - 1;
   constexpr int kPro = 2 * T;
@@ -217,19 +233,22 @@ void life_group_kernel(const LifeBlockParams p) {
   const int kmain = last ? kend - (kend - kPro) % 3 : p.grp_q;
   const int nfull = last ? (kend - kPro) % 3 : 2 * T;
 
-  const int col = kcol * kWaveOut - 1 + W * lane;
+  const LaneCols<IO> lc = lane_cols<IO>(p, kcol, lane, sub_lanes, nsub);
   const int64_t pitch = p.pitch;
-  RowReader<IO> rd;
+  int64_t dl = 0;  // rows between this lane's group and the wave's (folded strips)
   Writer<IO> wr;
+  if (nsub > 1) {
+    dl = group_end(min(grp + min(lc.sub, nsub - 1), p.nseg - 1)) - G1;
+    wr.roff = int(dl * pitch);
+    wr.nrec = int((group_end(min(grp + nsub - 1, p.nseg - 1)) - G1 + 1) * pitch);
+  }
+  RowReader<IO> rd;
   uint32_t fmask[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    const int c = col + i;
-    const bool ok = c >= 0 && c < p.Wp;
-    const bool halo = wave_halo<IO::XL, W>(lane, i);
-    rd.ok[i] = ok;
-    wr.own[i] = ok && !halo;
-    fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
+    rd.ok[i] = lc.ok[i];
+    wr.own[i] = lc.own[i];
+    fmask[i] = lc.fmask[i];
   }
 
   Levels<T, W> st;
@@ -247,11 +266,11 @@ void life_group_kernel(const LifeBlockParams p) {
   rd.pitch = pitch;
   rd.kmax = last ? kend - 1 : kmain + 1;
 #pragma unroll
-  for (int i = 0; i < W; ++i) rd.off[i] = min(max(col + i, 0), p.Wp - 1);
+  for (int i = 0; i < W; ++i) rd.off[i] = lc.off[i] + int(dl * (pitch / IO::kWordBytes));
   rd.init();
   wr.out = p.out + in0 * pitch;  // level-T row of step k: in0 + k - T
   wr.pitch = pitch;
-  wr.col = col;
+  wr.col = lc.store_col;
 
   const LdsSaver<T, W> saver{saved + m * kSlot, lane};
   prologue_tri<T, IO, 0>(st, rd, saver, NoBottom{});
@@ -296,6 +315,10 @@ void life_group_kernel(const LifeBlockParams p) {
 // few for M segments of 2T rows.
 template <int T, int M>
 double plan_group(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int target_waves, int xl = kXlaneDpp) {
+  // A folded last strip (p.fold groups per block) costs 1/fold of a strip.
+  const auto strip_groups = [&](int64_t n) {
+    return p.fold > 1 ? int64_t(p.ncolw - 1) * n + ceil_div(n, int64_t(p.fold)) : int64_t(p.ncolw) * n;
+  };
   constexpr double kOverhead = 0.4 * T;  // the two triangles (4T steps) run at lower ILP
   const int64_t max_n = out_rows / (int64_t(M - 1) * 2 * T + 1);
   int64_t best_n = 0;
@@ -316,7 +339,7 @@ double plan_group(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int 
       }
     }
     if (q == 0) continue;
-    const int64_t waves = int64_t(p.ncolw) * n * M;
+    const int64_t waves = strip_groups(n) * M;
     const int64_t k = ceil_div(waves, int64_t(simds));
     const int64_t rounds = ceil_div(k, int64_t(occ));
     const int64_t kk = std::min<int64_t>(k, occ);
@@ -357,9 +380,9 @@ int group_waves_per_simd() {
 
 template <int T, class IO, int M>
 void launch_group(const LifeBlockParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((life_group_kernel<T, IO, M>), dim3(unsigned(int64_t(p.ncolw) * p.nseg * (p.row_alt ? 2 : 1))),
-                     dim3(64 * M), 0, s,
-                     p);
+  const int64_t blocks = p.fold > 1 ? int64_t(p.ncolw - 1) * p.nseg + ceil_div(int64_t(p.nseg), int64_t(p.fold))
+                                    : int64_t(p.ncolw) * p.nseg * (p.row_alt ? 2 : 1);
+  hipLaunchKernelGGL((life_group_kernel<T, IO, M>), dim3(unsigned(blocks)), dim3(64 * M), 0, s, p);
 }
 
 }  // namespace lb

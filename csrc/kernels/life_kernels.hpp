@@ -47,6 +47,13 @@ struct LifeBlockParams {
   // ncolw x nseg evaluate the same row range shifted by row_alt rows.
   int64_t row_alt;
   int prio_boost;  // BlockArgs::prio_boost
+  // Wrap mode (BlockArgs::full_width): owned words per row, 0 = halo mode
+  // (life_block_impl.hpp lane_cols).
+  int wrap_w;
+  // Folded last strip (life_group_kernel, wrap mode): `fold` groups per
+  // block in sub-strips of fold_lanes lanes; 1 = no folding.
+  int fold;
+  int fold_lanes;
 };
 
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
@@ -79,6 +86,8 @@ struct LifeTuning {
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
   int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
   int pipe = 0;             // level-pipelined wave pairs (life_pipe_impl.hpp): 0 off, 1 by the model, 2 forced
+  bool wrap = true;         // wrap mode on whole-width tiles (BlockArgs::full_width, lane_cols)
+  bool fold = true;         // folded last strip in wrap mode (life_group_kernel)
   uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
   uint32_t* err = nullptr;       // LifeBlockParams::err
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).

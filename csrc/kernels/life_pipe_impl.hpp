@@ -218,7 +218,6 @@ __global__ __launch_bounds__(128 * M) void life_pipe_kernel(const LifeBlockParam
   constexpr int W = IO::W;
   constexpr int T = T1 + T2;
   constexpr int kProA = PipeGeom<T1, T2, M>::kProA, kProB = PipeGeom<T1, T2, M>::kProB;
-  constexpr int kWaveOut = wave_out_words<IO::XL, W>();
   constexpr int kSlotA = T1 * 2 * W * 64;        // levels 1..T1, rows b + L, b + L + 1
   constexpr int kSlotB = (T2 - 1) * 2 * W * 64;  // local levels 1..T2-1
   constexpr int kRing = kPipeRing * W * 64;
@@ -248,17 +247,15 @@ __global__ __launch_bounds__(128 * M) void life_pipe_kernel(const LifeBlockParam
   const bool last = m == M - 1;
   const int kendA = int(G1 + T - in0);
 
-  const int col = kcol * kWaveOut - 1 + W * lane;
+  const LaneCols<IO> lc = lane_cols<IO>(p, kcol, lane);
+  const int col = lc.store_col;
   const int64_t pitch = p.pitch;
-  bool ok[W];
   uint32_t fmask[W];
   Writer<IO> wr;
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    const int c = col + i;
-    ok[i] = c >= 0 && c < p.Wp;
-    wr.own[i] = ok[i] && !wave_halo<IO::XL, W>(lane, i);
-    fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
+    wr.own[i] = lc.own[i];
+    fmask[i] = lc.fmask[i];
   }
   PipeRing<W> ring{rings + m * kRing, ctrs + 2 * m, ctrs + 2 * m + 1, p.err, lane};
 
@@ -268,8 +265,8 @@ __global__ __launch_bounds__(128 * M) void life_pipe_kernel(const LifeBlockParam
     RowReader<IO> rd;
 #pragma unroll
     for (int i = 0; i < W; ++i) {
-      rd.ok[i] = ok[i];
-      rd.off[i] = min(max(col + i, 0), p.Wp - 1);
+      rd.ok[i] = lc.ok[i];
+      rd.off[i] = lc.off[i];
     }
     rd.base = p.in + in0 * pitch;  // input row of step k: in0 + k
     rd.pitch = pitch;

@@ -129,7 +129,6 @@ template <int T, class IO, int M, int Q>
 __global__ __launch_bounds__(64 * M) __attribute__((amdgpu_waves_per_eu(4)))
 void life_short_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
-  constexpr int kWaveOut = wave_out_words<IO::XL, W>();
   constexpr int kSlot = (T - 1) * 2 * W * 64;
   __shared__ uint32_t saved[M * kSlot];
   __shared__ uint32_t ready[M * T];
@@ -146,19 +145,17 @@ void life_short_kernel(const LifeBlockParams p) {
   const bool last = m == M - 1;
   const int kend = int(G1 + T - in0);  // last wave: level-T rows up to G1 - 1
 
-  const int col = kcol * kWaveOut - 1 + W * lane;
+  const LaneCols<IO> lc = lane_cols<IO>(p, kcol, lane);
+  const int col = lc.store_col;
   const int64_t pitch = p.pitch;
   RowReader<IO> rd;
   Writer<IO> wr;
   uint32_t fmask[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    const int c = col + i;
-    const bool ok = c >= 0 && c < p.Wp;
-    const bool halo = wave_halo<IO::XL, W>(lane, i);
-    rd.ok[i] = ok;
-    wr.own[i] = ok && !halo;
-    fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
+    rd.ok[i] = lc.ok[i];
+    wr.own[i] = lc.own[i];
+    fmask[i] = lc.fmask[i];
   }
   Levels<T, W> st;
 #pragma unroll
@@ -174,7 +171,7 @@ void life_short_kernel(const LifeBlockParams p) {
   rd.pitch = pitch;
   rd.kmax = last ? kend - 1 : Q + 1;
 #pragma unroll
-  for (int i = 0; i < W; ++i) rd.off[i] = min(max(col + i, 0), p.Wp - 1);
+  for (int i = 0; i < W; ++i) rd.off[i] = lc.off[i];
   rd.init();
   wr.out = p.out + in0 * pitch;  // level-T row of step k: in0 + k - T
   wr.pitch = pitch;

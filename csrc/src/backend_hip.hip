@@ -69,6 +69,8 @@ class HipBackend final : public Backend {
     // than the grouped kernel on the per-rank tile (profiles/sweep_short_segments.jsonl).
     tune_.short_seg = env_int("GOL_SHORT", 0);
     tune_.pipe = env_int("GOL_PIPE", 0);
+    tune_.wrap = env_int("GOL_WRAP", 1) != 0;
+    tune_.fold = env_int("GOL_FOLD", 1) != 0;
     if (const char* t = std::getenv("GOL_WG_TRACE")) {
       const std::string v(t);
       const size_t c = v.find(':');
@@ -253,6 +255,7 @@ class HipBackend final : public Backend {
     }
     return k;
   }
+  bool wraps_columns(Layout l) const override { return tune_.wrap && !(l == Layout::U8 && tune_.u8_lds); }
   void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override {
     hipk::launch_rotate_cols(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), g, shift, stream_);
     HIP_CHECK(hipGetLastError());

@@ -55,6 +55,9 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // left halo per generation and none on the right; it needs the tile to be
   // the whole torus width so that the drift is a relabeling of columns.
   drift_ok_ = kc.drift && dec_.Px == 1 && cfg_.W % 32 == 0;
+  // Whole-width tiles on a backend that wraps column reads (lane_cols in the
+  // HIP kernels) never read their halo columns: no column fills.
+  cols_filled_ = !(dec_.Px == 1 && cfg_.W % 32 == 0 && be_->wraps_columns(cfg_.layout));
   int hw = int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32));
   Extent r = rows(), c = cols();
   g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
@@ -174,7 +177,7 @@ void Engine::exchange_columns(void* buf) {
   auto nb = dec_.neighbors(rank_);
   const int64_t H = g_.H, pitch = g_.pitch;
   if (dec_.Px == 1) {
-    be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/false);
+    if (cols_filled_) be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/false);
     return;
   }
   const int64_t halo = 32 * int64_t(g_.hw);
@@ -205,7 +208,7 @@ void Engine::halo_exchange() {
   auto nb = dec_.neighbors(rank_);
   const int64_t H = g_.H, pitch = g_.pitch;
   if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange) {  // one rank: both periodic fills, one launch
-    be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/true);
+    be_->fill_periodic(buf, g_, /*cols=*/cols_filled_, /*rows=*/true);
     ++exchanges_;
     return;
   }
@@ -371,8 +374,10 @@ void Engine::last_block_early(int T) {
   if (comm) be_->stream_wait(comm, be_->stream_mark(nullptr));  // this block's input is complete
   // Boundary strips [Dv, Dv + D) and [Dv + H - D, Dv + H), one launch.
   const int drift = launch(in, out, g_, T, Dv, Dv + D, gen_, comm, H - D, /*prio_boost=*/true);
-  be_->fill_cols_rows(out, g_, Dv, D, comm);
-  be_->fill_cols_rows(out, g_, Dv + H - D, D, comm);
+  if (cols_filled_) {
+    be_->fill_cols_rows(out, g_, Dv, D, comm);
+    be_->fill_cols_rows(out, g_, Dv + H - D, D, comm);
+  }
   auto nb = dec_.neighbors(rank_);
   const size_t bytes = size_t(Dv * pitch);
   std::vector<P2POp> ops = {
@@ -388,7 +393,7 @@ void Engine::last_block_early(int T) {
   ++exchanges_;
   ++early_sends_;
   launch(in, out, g_, T, Dv + D, Dv + H - D, gen_);  // interior, concurrent with the above
-  be_->fill_cols_rows(out, g_, Dv + D, H - 2 * D);
+  if (cols_filled_) be_->fill_cols_rows(out, g_, Dv + D, H - 2 * D);
   add_drift(drift);
   cur_ ^= 1;
   gen_ += T;
@@ -415,6 +420,7 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   }
   a.flags_base = flags_base_;
   a.allow_drift = drift_ok_;
+  a.full_width = dec_.Px == 1 && cfg_.W % 32 == 0;
   a.stream = stream;
   a.dual_offset = dual_offset;
   a.prio_boost = prio_boost;

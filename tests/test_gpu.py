@@ -228,6 +228,52 @@ def test_pipe_schedule_termination(gpu, monkeypatch, xlane, tmax):
     assert (out == ref).all()
 
 
+@pytest.mark.parametrize("words", [79, 93, 136, 1024])
+@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (0, 8), (3, 4)])
+@pytest.mark.parametrize("wrap,fold", [("1", "1"), ("1", "0"), ("0", "0")])
+def test_wrap_and_folded_strip_vs_torch(gpu, monkeypatch, words, xlane, tmax, wrap, fold):
+    """Wrap mode (whole-width tiles read owned words mod the width, no halo
+    columns; csrc/kernels/life_block_impl.hpp lane_cols) and the folded last
+    strip (life_group_kernel: the narrow last strip's lanes packed 2-4 times
+    into one wave, each sub-strip running another group's rows) against the
+    fp32 conv oracle.  Widths: 79 / 93 / 136 words leave a last strip of
+    16 / 30 / 10 words (fold 3 / 2 / 4); several group counts, including ones
+    that leave a partial fold and unequal group sizes."""
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    monkeypatch.setenv("GOL_WRAP", wrap)
+    monkeypatch.setenv("GOL_FOLD", fold)
+    W, H = 32 * words, 613 if words < 1024 else 300
+    g = random_grid(W, H, words * 7 + tmax)
+    gens = 2 * tmax + 5
+    want = life_step_torch(g, gens, device="cuda")
+    for target in ("0", "2000", "100000"):
+        monkeypatch.setenv("GOL_TARGET_WAVES", target)
+        sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax), engine="hip")
+        sim.load(g)
+        sim.advance(gens)
+        assert (sim.tile() == want).all(), target
+
+
+@pytest.mark.parametrize("xlane", [0, 3])
+def test_folded_strip_termination_and_row_strips(gpu, monkeypatch, xlane):
+    """Exact Generations with a folded last strip (the change flags of every
+    sub-strip), and row-strip subdomains (Px = 1, so wrap mode on every rank)."""
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    monkeypatch.setenv("GOL_TARGET_WAVES", "3000")
+    grid = np.zeros((700, 32 * 79), dtype=np.uint8)
+    W, H, seed, density = CONVERGING[5]
+    grid[300:300 + H, 2500 - W:2500] = random_grid(W, H, seed, density)  # straddles the folded strip
+    ref, rgens, _ = reference_run(grid)
+    out, rep = simulate(grid, 1000, engine="hip", tmax=12 if xlane == 3 else 16)
+    assert rep.generations == rgens
+    assert (out == ref).all()
+    grp = InProcessGroup(LifeConfig(32 * 79, 700, decomp="1x3", tmax=8, epoch=16, poll_gens=32), 3, engine="hip")
+    grp.load(grid)
+    reps = grp.run()
+    assert {r.generations for r in reps} == {rgens}
+    assert (grp.gather() == ref).all()
+
+
 def test_grouped_schedule_is_the_default(gpu):
     sim = Simulation(LifeConfig(4096, 2048), engine="hip")
     assert "group=8" in sim.describe()["backend"]
@@ -461,11 +507,14 @@ def test_torch_tensor_views_of_engine_buffers(gpu):
 
 
 @pytest.mark.parametrize("W,H,epoch", [(64, 5, 32), (96, 70, 64), (2048, 40, 128), (32, 1, 16)])
-def test_fused_periodic_fill_matches_cpu_buffer(gpu, W, H, epoch):
+def test_fused_periodic_fill_matches_cpu_buffer(gpu, monkeypatch, W, H, epoch):
     """Single-rank halo_exchange is one fused launch (fill_all_bits): the whole
     padded buffer (column halos, halo rows and corners, multi-wrap when Dv > H)
-    must equal the CPU backend's two-pass fill."""
+    must equal the CPU backend's two-pass fill.  Halo mode (GOL_WRAP=0): in
+    wrap mode the engine fills no column halos."""
     import torch
+
+    monkeypatch.setenv("GOL_WRAP", "0")
 
     from gol_amd.parallel.dist import tensor_view
 
