@@ -57,6 +57,10 @@ class Transport {
   // Throws if the communicator has failed asynchronously (RCCL async error);
   // called by the engine while it waits on the device.
   virtual void check_health() {}
+  // allreduce_max_u32 runs on a communicator of its own, so it may be
+  // enqueued on another stream than exchange() and run concurrently with it
+  // (the engine then reduces termination flags beside the compute stream).
+  virtual bool side_reduce() const { return false; }
 };
 
 // Single rank: nothing to exchange with.

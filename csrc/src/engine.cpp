@@ -61,7 +61,10 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   int hw = int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32));
   Extent r = rows(), c = cols();
   g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
-  poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : 256;
+  // Several ranks: every poll is a flag all-reduce on the compute stream
+  // (latency-bound), so poll half as often; a stop is still exact and at most
+  // two windows late.
+  poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : (tr_->size() > 1 || cfg_.self_exchange) ? 512 : 256;
 
   for (auto& b : buf_) b = be_->alloc(size_t(g_.bytes()));
   alive_dev_ = static_cast<uint32_t*>(be_->alloc(64));
@@ -96,6 +99,17 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
   if (use_graphs_) early_ = comm_route_ = false;  // captured epochs stay on one stream
+  // Side polls: with a transport whose flag reduction has its own
+  // communicator (RCCL), a poll's all-reduce and D2H copy run on the comm
+  // stream after a mark on the compute stream, which never waits for them:
+  // the reduction's latency leaves the critical path.  The halo exchanges
+  // stay on the compute stream.
+  // Opt-in (GOL_SIDE_POLL=1): in the one-GPU RCCL rehearsal the cross-stream
+  // hop cost ~10 us per poll, more than the 1-rank reduction it hides
+  // (profiles/r02/side_poll_ab.jsonl); with 8 ranks the reduction is longer.
+  const char* side = std::getenv("GOL_SIDE_POLL");
+  poll_side_ = tr_->side_reduce() && be_->is_device() && !early_ && !comm_route_ && !use_graphs_ && side &&
+               std::atoi(side) != 0;
   gen_ = cfg_.start_gen;
 }
 
@@ -449,6 +463,17 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   const int64_t n = to - from;
   if (n <= 0) return p;
   uint32_t* dev = flags_ + (from + 1 - flags_base_);
+  if (poll_side_) {
+    // Flags of (from, to] are complete at the compute stream's current mark.
+    void* side = be_->comm_stream();
+    be_->stream_wait(side, be_->stream_mark(nullptr));
+    // The one-rank RCCL rehearsal reduces too, through its 1-rank communicator.
+    if (tr_->size() > 1 || cfg_.self_exchange) tr_->allreduce_max_u32(dev, size_t(n), side);
+    be_->copy_d2h_async_on(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t), side);
+    p.ev = be_->event_record_on(side);
+    ++polls_;
+    return p;
+  }
   // Early-boundary schedule: reduce and copy on the comm stream, off the
   // compute stream's critical path, in issue order with the halo exchanges.
   void* comm = (comm_route_ || early_) ? be_->comm_stream() : nullptr;
@@ -615,6 +640,9 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     }
   }
   if (have_pending) poll_check(pending, &found);
+  // A poll issued just before an early stop may still run on the side stream;
+  // the final alive reduction below uses the same communicator.
+  if (poll_side_) be_->synchronize_stream(be_->comm_stream());
   be_->synchronize();
   be_->check_device_errors();
   if (cfg_.timing_barriers) {

@@ -62,6 +62,10 @@ class RcclTransport final : public Transport {
     {
       StdoutToStderr quiet;
       NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+      // Termination-flag reductions get their own communicator: RCCL orders
+      // the operations of one communicator by issue, and running two streams
+      // on one communicator could interleave differently on different ranks.
+      NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
     }
     if (hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking) != hipSuccess)
       fail("hipStreamCreate failed");
@@ -71,6 +75,7 @@ class RcclTransport final : public Transport {
     hipSetDevice(dev_);
     if (barrier_buf_) hipFree(barrier_buf_);
     if (barrier_stream_) hipStreamDestroy(barrier_stream_);
+    if (flags_comm_) ncclCommDestroy(flags_comm_);
     if (comm_) ncclCommDestroy(comm_);
   }
   int rank() const override { return rank_; }
@@ -89,8 +94,9 @@ class RcclTransport final : public Transport {
     NCCL_CHECK(ncclGroupEnd());
   }
   void allreduce_max_u32(uint32_t* buf, size_t n, void* stream) override {
-    NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, comm_, static_cast<hipStream_t>(stream)));
+    NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, flags_comm_, static_cast<hipStream_t>(stream)));
   }
+  bool side_reduce() const override { return true; }
   void barrier() override {
     NCCL_CHECK(ncclAllReduce(barrier_buf_, barrier_buf_, 1, ncclUint32, ncclMax, comm_, barrier_stream_));
     if (hipStreamSynchronize(barrier_stream_) != hipSuccess) fail("RCCL barrier failed");
@@ -98,14 +104,17 @@ class RcclTransport final : public Transport {
   bool capturable() const override { return true; }  // grouped send/recv are stream-ordered
   void check_health() override {
     ncclResult_t r = ncclSuccess;
-    NCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
-    if (r != ncclSuccess && r != ncclInProgress)
-      fail(std::string("RCCL communicator failed asynchronously: ") + ncclGetErrorString(r));
+    for (ncclComm_t c : {comm_, flags_comm_}) {
+      NCCL_CHECK(ncclCommGetAsyncError(c, &r));
+      if (r != ncclSuccess && r != ncclInProgress)
+        fail(std::string("RCCL communicator failed asynchronously: ") + ncclGetErrorString(r));
+    }
   }
 
  private:
   int rank_, size_, dev_;
   ncclComm_t comm_ = nullptr;
+  ncclComm_t flags_comm_ = nullptr;  // allreduce_max_u32 (side_reduce)
   hipStream_t barrier_stream_ = nullptr;
   void* barrier_buf_ = nullptr;
 };

@@ -463,14 +463,17 @@ def test_rccl_single_rank_self_exchange(gpu):
     assert flags.tolist() == [3, 0, 7]
 
 
-@pytest.mark.parametrize("overlap", ["off", "on", "edges"])
+@pytest.mark.parametrize("overlap,side", [("off", "1"), ("off", "0"), ("on", "1"), ("edges", "1")])
 @pytest.mark.parametrize("xlane", [0, -1])
-def test_rccl_self_exchange_rehearsal(gpu, monkeypatch, overlap, xlane):
+def test_rccl_self_exchange_rehearsal(gpu, monkeypatch, overlap, side, xlane):
     """The multi-rank row-strip schedule on one GPU (bench.py --rehearse-rccl):
     row halos through a 1-rank RCCL communicator sending to itself on the
     comm stream, early-boundary dual launch concurrent with the interior,
-    against the fp32 conv oracle and the exact Generations."""
+    termination polls reduced on the side stream through the transport's
+    flags communicator (GOL_SIDE_POLL, overlap off), against the fp32 conv
+    oracle and the exact Generations."""
     monkeypatch.setenv("GOL_XLANE", str(xlane))
+    monkeypatch.setenv("GOL_SIDE_POLL", side)
     C = gpu
     W, H = 32 * 96, 1200
     g = random_grid(W, H, 31)
