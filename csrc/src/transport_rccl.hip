@@ -14,6 +14,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -62,10 +63,12 @@ class RcclTransport final : public Transport {
     {
       StdoutToStderr quiet;
       NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
-      // Termination-flag reductions get their own communicator: RCCL orders
-      // the operations of one communicator by issue, and running two streams
-      // on one communicator could interleave differently on different ranks.
-      NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
+      // Side-stream polls (GOL_SIDE_POLL=1, the same on every rank): the
+      // termination-flag reductions get their own communicator.  RCCL orders
+      // the operations of one communicator by issue, and two streams on one
+      // communicator could interleave differently on different ranks.
+      const char* side = std::getenv("GOL_SIDE_POLL");
+      if (side && std::atoi(side) != 0) NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
     }
     if (hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking) != hipSuccess)
       fail("hipStreamCreate failed");
@@ -94,9 +97,10 @@ class RcclTransport final : public Transport {
     NCCL_CHECK(ncclGroupEnd());
   }
   void allreduce_max_u32(uint32_t* buf, size_t n, void* stream) override {
-    NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, flags_comm_, static_cast<hipStream_t>(stream)));
+    NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, flags_comm_ ? flags_comm_ : comm_,
+                             static_cast<hipStream_t>(stream)));
   }
-  bool side_reduce() const override { return true; }
+  bool side_reduce() const override { return flags_comm_ != nullptr; }
   void barrier() override {
     NCCL_CHECK(ncclAllReduce(barrier_buf_, barrier_buf_, 1, ncclUint32, ncclMax, comm_, barrier_stream_));
     if (hipStreamSynchronize(barrier_stream_) != hipSuccess) fail("RCCL barrier failed");
@@ -105,6 +109,7 @@ class RcclTransport final : public Transport {
   void check_health() override {
     ncclResult_t r = ncclSuccess;
     for (ncclComm_t c : {comm_, flags_comm_}) {
+      if (!c) continue;
       NCCL_CHECK(ncclCommGetAsyncError(c, &r));
       if (r != ncclSuccess && r != ncclInProgress)
         fail(std::string("RCCL communicator failed asynchronously: ") + ncclGetErrorString(r));
