@@ -106,9 +106,10 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   }
   // The adder window drifts the storage frame by T cells (see kXlaneAdd); the
   // engine allows that only for whole-width tiles of 32-cell words, and the
-  // left halo must hold the 2T cells its one-sided light cone consumes.
+  // left halo must hold the 2T cells its one-sided light cone consumes (wrap
+  // mode reads the wrapped owned words instead).
   if (x == kXlaneAuto) x = kXlaneAdd;  // the engine decided through allow_drift
-  if (x == kXlaneAdd && !(a.allow_drift && 32 * g.hw >= 2 * a.T)) x = kXlaneDpp;
+  if (x == kXlaneAdd && !(a.allow_drift && (p.wrap_w > 0 || 32 * g.hw >= 2 * a.T))) x = kXlaneDpp;
   if (x == kXlaneAdd) {
     (g.layout == Layout::U8 ? launch_u8_w1_add : launch_bits_w1_add)(p, rows, a.T, tune, stream);
     return a.T;

@@ -58,7 +58,9 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // Whole-width tiles on a backend that wraps column reads (lane_cols in the
   // HIP kernels) never read their halo columns: no column fills.
   cols_filled_ = !(dec_.Px == 1 && cfg_.W % 32 == 0 && be_->wraps_columns(cfg_.layout));
-  int hw = int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32));
+  // Halo columns: none when the kernels wrap (smaller rows to exchange and
+  // fill); else D cells per side, 2D on the left for the drifting window.
+  int hw = cols_filled_ ? int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32)) : 0;
   Extent r = rows(), c = cols();
   g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
   // Several ranks: every poll is a flag all-reduce on the compute stream
