@@ -63,6 +63,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   int hw = cols_filled_ ? int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32)) : 0;
   Extent r = rows(), c = cols();
   g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
+  // Experiment knob: extra bytes per padded row (multiple of 256).
+  if (const char* pad = std::getenv("GOL_PITCH_PAD")) g_.pitch += 256 * (std::max(0, std::atoi(pad)) / 256);
   // Several ranks: every poll is a flag all-reduce on the compute stream
   // (latency-bound), so poll half as often; a stop is still exact and at most
   // two windows late.
