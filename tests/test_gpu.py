@@ -254,6 +254,24 @@ def test_wrap_and_folded_strip_vs_torch(gpu, monkeypatch, words, xlane, tmax, wr
         assert (sim.tile() == want).all(), target
 
 
+@pytest.mark.parametrize("words", [1, 2, 3, 31, 32, 33, 62, 63, 64, 65, 94, 125, 126, 127, 129, 190])
+@pytest.mark.parametrize("xlane", [0, 3])
+def test_wrap_mode_widths_vs_torch(gpu, monkeypatch, words, xlane):
+    """Wrap mode across torus widths: narrower than one strip (lanes wrap
+    several times around the row), one word either side of a strip boundary,
+    and every fold factor of the last strip (1-4)."""
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    W, H = 32 * words, 97 + words
+    g = random_grid(W, H, words * 13 + xlane)
+    for tmax in (16, 12, 4):
+        gens = tmax + 7
+        want = life_step_torch(g, gens, device="cuda")
+        sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax), engine="hip")
+        sim.load(g)
+        sim.advance(gens)
+        assert (sim.tile() == want).all(), tmax
+
+
 @pytest.mark.parametrize("xlane", [0, 3])
 def test_folded_strip_termination_and_row_strips(gpu, monkeypatch, xlane):
     """Exact Generations with a folded last strip (the change flags of every
