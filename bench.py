@@ -122,7 +122,8 @@ def main() -> int:
     total = a.prewarm + (a.warmup + a.steps * a.repeats) * gps
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
                      poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs, timing_barriers=False,
-                     self_exchange=bool(a.rehearse_rccl and world == 1))
+                     self_exchange=bool(a.rehearse_rccl and world == 1),
+                     watchdog_s=300.0)  # a stuck rank or kernel fails the run instead of hanging it
     sim = Simulation(cfg, transport=transport, backend=backend)
     eng = sim.native_engine
     sim.init_random(a.seed, 0.5)

@@ -38,9 +38,9 @@ class LifeConfig:
     sim_freq: int = 3
     layout: str = "auto"        # auto | bits | u8
     decomp: str = "auto"        # auto | PxQ
-    tmax: int = 0               # generations per kernel launch (0 = default 16)
-    epoch: int = 0              # generations per halo exchange (0 = 4*tmax)
-    poll_gens: int = 0          # generations between termination polls (0 = 256)
+    tmax: int = 0               # generations per kernel launch (0 = the backend's choice: 12 adder / 16 DPP)
+    epoch: int = 0              # generations per halo exchange (0 = 8*tmax, 16*tmax with several ranks)
+    poll_gens: int = 0          # generations between termination polls (0 = 256, 512 with several ranks)
     overlap: str = "auto"       # auto | on | off | edges: overlap the row halo exchange with compute
     lagged_poll: bool = True    # check termination polls one window late (no queue drain)
     graphs: str = "off"         # auto | on | off: replay full epochs as captured HIP graphs
@@ -48,6 +48,7 @@ class LifeConfig:
     sim_phase: int = 0          # resume: similarity counter at start_gen
     timing_barriers: bool = True  # barrier + sync around each run's loop (off: the caller brackets it)
     self_exchange: bool = False   # rehearse the multi-rank row-halo schedule on one rank (transport to self)
+    watchdog_s: float = 0.0       # fail when a termination poll waits longer (0 = GOL_WATCHDOG_S or 900 s)
 
     def resolved_layout(self) -> str:
         if self.layout == "auto":
@@ -76,6 +77,7 @@ class LifeConfig:
         c.sim_phase = int(self.sim_phase)
         c.timing_barriers = bool(self.timing_barriers)
         c.self_exchange = bool(self.self_exchange)
+        c.watchdog_s = float(self.watchdog_s)
         return c
 
 
