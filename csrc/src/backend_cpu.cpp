@@ -26,6 +26,39 @@ inline void unpack32(uint32_t w, uint8_t* p) {
   for (int j = 0; j < 32; ++j) p[j] = uint8_t((w >> j) & 1u);
 }
 
+// Horizontal 3-sums of one row of Wp words; w[-1] and w[Wp] are zero pads.
+// Plain word loops the compiler vectorises (no cross-iteration state).
+inline void hsum_row(const uint32_t* w, int64_t Wp, uint32_t* h0, uint32_t* h1) {
+  for (int64_t c = 0; c < Wp; ++c) {
+    const uint32_t x = w[c];
+    const uint32_t l = (x << 1) | (w[c - 1] >> 31);  // cell x-1 at bit of x
+    const uint32_t r = (x >> 1) | (w[c + 1] << 31);  // cell x+1
+    h0[c] = l ^ x ^ r;
+    h1[c] = (l & x) | (r & (l ^ x));
+  }
+}
+
+// B3/S23 of a row from the horizontal sums (a, b, c = rows above / at /
+// below; suffix 0 / 1 = sum bits) and the centre cells; returns
+// the OR of (new ^ old) over the owned cells.  S = x0 + 2 (x1 + y0) + 4 y1:
+// born / survives at S == 3, survives at S == 4.
+inline uint32_t rule_row(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
+                         const uint32_t* c0, const uint32_t* c1, const uint32_t* mid, int64_t Wp,
+                         const uint32_t* owned, uint32_t* out) {
+  uint32_t acc = 0;
+  for (int64_t c = 0; c < Wp; ++c) {
+    const uint32_t p0 = a0[c] ^ b0[c], p1 = a1[c] ^ b1[c];
+    const uint32_t x0 = p0 ^ c0[c], x1 = (a0[c] & b0[c]) | (c0[c] & p0);
+    const uint32_t y0 = p1 ^ c1[c], y1 = (a1[c] & b1[c]) | (c1[c] & p1);
+    const uint32_t s3 = ~y1 & (x1 ^ y0);
+    const uint32_t s4 = ~(x1 ^ y0) & (x1 ^ y1);
+    const uint32_t nw = (x0 & s3) | (~x0 & mid[c] & s4);
+    out[c] = nw;
+    acc |= (nw ^ mid[c]) & owned[c];
+  }
+  return acc;
+}
+
 // Mask of owned cells inside padded word c.
 inline uint32_t owned_mask(const TileGeom& g, int64_t c) {
   int64_t lo = g.cell0(), hi = g.cell0() + g.W;
@@ -112,73 +145,92 @@ int CpuBackend::run_block(const BlockArgs& a) {
   const int64_t Wp = g.Wp();
   const int64_t r0 = a.row_lo - T, r1 = a.row_hi + T;  // input rows
   GOL_REQUIRE(r0 >= 0 && r1 <= g.R() && a.row_lo < a.row_hi && T >= 1, "run_block: bad row range");
-  const int64_t nr = r1 - r0;
-  std::vector<uint32_t> lvl[2] = {std::vector<uint32_t>(size_t(nr * Wp)),
-                                  std::vector<uint32_t>(size_t(nr * Wp))};
-  auto* in = static_cast<const uint8_t*>(a.in);
-  pool_.parallel_for(nr, [&](int64_t b, int64_t e) {
-    for (int64_t i = b; i < e; ++i)
-      for (int64_t c = 0; c < Wp; ++c) lvl[0][size_t(i * Wp + c)] = read_word(in, g, r0 + i, c);
-  });
   std::vector<uint32_t> owned(static_cast<size_t>(Wp));
   for (int64_t c = 0; c < Wp; ++c) owned[size_t(c)] = owned_mask(g, c);
-
-  for (int lev = 1; lev <= T; ++lev) {
-    const auto& src = lvl[(lev - 1) & 1];
-    auto& dst = lvl[lev & 1];
-    // Level `lev` is valid on rows [r0 + lev, r1 - lev).
-    const int64_t lo = lev, hi = nr - lev;
-    std::vector<uint8_t> any(size_t(hi - lo), 0);
-    pool_.parallel_for(hi - lo, [&](int64_t b, int64_t e) {
-      for (int64_t k = b; k < e; ++k) {
-        const int64_t i = lo + k;
-        const uint32_t* up = &src[size_t((i - 1) * Wp)];
-        const uint32_t* mid = &src[size_t(i * Wp)];
-        const uint32_t* dn = &src[size_t((i + 1) * Wp)];
-        uint32_t* out = &dst[size_t(i * Wp)];
-        uint32_t acc = 0;
-        for (int64_t c = 0; c < Wp; ++c) {
-          auto nb = [&](const uint32_t* row) {
-            return hsum_host(c > 0 ? row[c - 1] : 0u, row[c], c + 1 < Wp ? row[c + 1] : 0u);
-          };
-          uint32_t nw = rule_host(nb(up), nb(mid), nb(dn), mid[c]);
-          out[c] = nw;
-          acc |= (nw ^ mid[c]) & owned[size_t(c)];
-        }
-        any[size_t(k)] = acc != 0;
-      }
-    }, 8);
-    if (a.changed) {
-      bool ch = std::any_of(any.begin(), any.end(), [](uint8_t v) { return v != 0; });
-      const int64_t idx = a.gen_dev ? *a.gen_dev + a.gen_rel + (lev - 1) : a.gen_base + lev - a.flags_base;
-      if (ch) a.changed[idx] = 1u;
-    }
-  }
-  auto& fin = lvl[T & 1];
   // Drift emulation: the HIP adder window stores generation t+1's cell x-1 at
   // column x, so after T levels the row sits T cells to the right with zeros
   // (junk on the GPU) entering at the left edge of the padded row.
   const int drift = (drift_ && a.allow_drift && T < 32 && 32 * g.hw >= 2 * T) ? T : 0;
-  if (drift) {
-    pool_.parallel_for(a.row_hi - a.row_lo, [&](int64_t b, int64_t e) {
-      for (int64_t k = b; k < e; ++k) {
-        uint32_t* w = &fin[size_t((a.row_lo + k - r0) * Wp)];
-        for (int64_t c = Wp - 1; c >= 0; --c) w[c] = (w[c] << drift) | (c > 0 ? w[c - 1] >> (32 - drift) : 0u);
-      }
-    });
-  }
+
+  // Row bands: each task runs all T levels of its output rows [lo, hi) on the
+  // trapezoid [lo - T + L, hi + T - L) of level L, in private buffers (the
+  // host counterpart of the GPU's temporal blocking: no barrier per level).
+  // Level rows outside the band are recomputed by both neighbours; every
+  // computed row is a valid row, so the per-band change flags OR together
+  // into the block's per-generation flags exactly.
+  const int64_t out_rows = a.row_hi - a.row_lo;
+  const int64_t bs = std::max<int64_t>(4 * int64_t(T), ceil_div(out_rows, 2 * int64_t(pool_.size())));
+  const int64_t nb = ceil_div(out_rows, bs);
+  std::vector<uint8_t> any(size_t(nb * T), 0);
+  auto* in = static_cast<const uint8_t*>(a.in);
   auto* out = static_cast<uint8_t*>(a.out);
-  pool_.parallel_for(a.row_hi - a.row_lo, [&](int64_t b, int64_t e) {
-    for (int64_t k = b; k < e; ++k) {
-      const int64_t r = a.row_lo + k;
-      const uint32_t* src = &fin[size_t((r - r0) * Wp)];
-      uint8_t* row = out + r * g.pitch;
-      if (g.layout == Layout::Bits)
-        std::memcpy(row, src, size_t(4 * Wp));
-      else
-        for (int64_t c = 0; c < Wp; ++c) unpack32(src[c], row + 32 * c);
+  const int64_t P = Wp + 2;  // row stride of the level buffers: a zero word either side
+  pool_.parallel_for(nb, [&](int64_t b0, int64_t b1) {
+    // Row sweep with a 3-row window per level (the GPU kernel's schedule on
+    // the host): input row k enters level 0, level L's window yields level
+    // L+1's row k - L - 1, so a band's working set is T x 3 rows, cache-
+    // resident, instead of whole level planes.  Per-thread scratch is kept
+    // across blocks (fresh large vectors were mmap'd and page-faulted every
+    // block, which serialised the threads).
+    const int64_t S = P + 2 * Wp;  // one window slot: padded cells, h0, h1
+    thread_local std::vector<uint32_t> win, outrow;
+    thread_local std::vector<int64_t> cnt;
+    if (win.size() < size_t(int64_t(T) * 3 * S)) win.resize(size_t(int64_t(T) * 3 * S));
+    if (outrow.size() < size_t(P)) outrow.resize(size_t(P));
+    cnt.assign(size_t(T), 0);
+    auto cells = [&](int L, int64_t slot) { return &win[size_t((L * 3 + slot) * S + 1)]; };
+    auto hs0 = [&](int L, int64_t slot) { return &win[size_t((L * 3 + slot) * S + P)]; };
+    auto hs1 = [&](int L, int64_t slot) { return &win[size_t((L * 3 + slot) * S + P + Wp)]; };
+    for (int L = 0; L < T; ++L)
+      for (int64_t sl = 0; sl < 3; ++sl) cells(L, sl)[-1] = cells(L, sl)[Wp] = 0u;  // zero pads
+    outrow[0] = outrow[size_t(P - 1)] = 0u;
+    for (int64_t band = b0; band < b1; ++band) {
+      const int64_t lo = a.row_lo + band * bs, hi = std::min(lo + bs, a.row_hi);
+      std::fill(cnt.begin(), cnt.end(), 0);
+      std::vector<uint32_t> acc(size_t(T), 0u);
+      for (int64_t r = lo - T; r < hi + T; ++r) {
+        const int64_t s0 = cnt[0] % 3;
+        uint32_t* w = cells(0, s0);
+        if (g.layout == Layout::Bits)
+          std::memcpy(w, in + r * g.pitch, size_t(4 * Wp));
+        else
+          for (int64_t c = 0; c < Wp; ++c) w[c] = read_word(in, g, r, c);
+        hsum_row(w, Wp, hs0(0, s0), hs1(0, s0));
+        ++cnt[0];
+        for (int L = 0; L < T && cnt[size_t(L)] >= 3; ++L) {
+          const int64_t n = cnt[size_t(L)];
+          const int64_t sa = (n - 3) % 3, sb = (n - 2) % 3, sc = (n - 1) % 3;
+          const bool last = L + 1 == T;
+          const int64_t sd = last ? 0 : cnt[size_t(L + 1)] % 3;
+          uint32_t* dst = last ? &outrow[1] : cells(L + 1, sd);
+          acc[size_t(L)] |= rule_row(hs0(L, sa), hs1(L, sa), hs0(L, sb), hs1(L, sb), hs0(L, sc), hs1(L, sc),
+                                     cells(L, sb), Wp, owned.data(), dst);
+          if (!last) {
+            hsum_row(dst, Wp, hs0(L + 1, sd), hs1(L + 1, sd));
+            ++cnt[size_t(L + 1)];
+            continue;
+          }
+          // Level-T row lo + n - 3 (n rows received by level T-1 so far).
+          if (drift)
+            for (int64_t c = Wp - 1; c >= 0; --c)
+              dst[c] = (dst[c] << drift) | (c > 0 ? dst[c - 1] >> (32 - drift) : 0u);
+          uint8_t* row = out + (lo + n - 3) * g.pitch;
+          if (g.layout == Layout::Bits)
+            std::memcpy(row, dst, size_t(4 * Wp));
+          else
+            for (int64_t c = 0; c < Wp; ++c) unpack32(dst[c], row + 32 * c);
+        }
+      }
+      for (int L = 0; L < T; ++L) any[size_t(band * T + L)] = acc[size_t(L)] != 0;
     }
   });
+  if (a.changed)
+    for (int L = 1; L <= T; ++L) {
+      bool ch = false;
+      for (int64_t b = 0; b < nb && !ch; ++b) ch = any[size_t(b * T + L - 1)] != 0;
+      const int64_t idx = a.gen_dev ? *a.gen_dev + a.gen_rel + (L - 1) : a.gen_base + L - a.flags_base;
+      if (ch) a.changed[idx] = 1u;
+    }
   return drift;
 }
 
