@@ -4,7 +4,9 @@
 // termination, decomposition) is testable without a GPU; (2) it is the
 // multi-threaded CPU engine that replaces the reference's OpenMP variant
 // (src/game_openmp.c:29-112); (3) it is an independent oracle for the HIP
-// kernels (same bit-sliced rule as common.hpp, but plain word loops).
+// kernels (the bit-sliced rule written as plain boolean word expressions, not
+// the kernels' v_bitop3 truth tables).  run_block sweeps per-thread row bands
+// with a 3-row window per level, like the GPU kernel's register schedule.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
