@@ -28,10 +28,18 @@ inline void unpack32(uint32_t w, uint8_t* p) {
   for (int j = 0; j < 32; ++j) p[j] = uint8_t((w >> j) & 1u);
 }
 
+// ifunc resolvers run before the ThreadSanitizer runtime is up and crash it,
+// so sanitizer builds of the host self test use the default clone only.
+#if defined(__SANITIZE_THREAD__)
+#define GOL_ROW_CLONES
+#else
+#define GOL_ROW_CLONES __attribute__((target_clones("avx2", "default")))
+#endif
+
 // Horizontal 3-sums of one row of Wp words; w[-1] and w[Wp] are zero pads.
 // Plain word loops the compiler vectorises (no cross-iteration state); an
 // AVX2 clone is picked at load time where the CPU has it.
-__attribute__((target_clones("avx2", "default"))) void hsum_row(const uint32_t* w, int64_t Wp, uint32_t* h0,
+GOL_ROW_CLONES void hsum_row(const uint32_t* w, int64_t Wp, uint32_t* h0,
                                                                 uint32_t* h1) {
   for (int64_t c = 0; c < Wp; ++c) {
     const uint32_t x = w[c];
@@ -46,7 +54,7 @@ __attribute__((target_clones("avx2", "default"))) void hsum_row(const uint32_t* 
 // below; suffix 0 / 1 = sum bits) and the centre cells; returns
 // the OR of (new ^ old) over the owned cells.  S = x0 + 2 (x1 + y0) + 4 y1:
 // born / survives at S == 3, survives at S == 4.
-__attribute__((target_clones("avx2", "default"))) uint32_t rule_row(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
+GOL_ROW_CLONES uint32_t rule_row(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
                          const uint32_t* c0, const uint32_t* c1, const uint32_t* mid, int64_t Wp,
                          const uint32_t* owned, uint32_t* out) {
   uint32_t acc = 0;
