@@ -98,6 +98,33 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
             return use8 ? launch_pipe<T1, T2, IO, 8>(p8, s) : launch_pipe<T1, T2, IO, 4>(p4, s);
         }
       }
+      // Chained groups (GOL_CHAIN): every group boundary shared through
+      // global memory, so no wave carries a redundant triangle but the
+      // strip's last.  Stream launches only (the flags count launches, so a
+      // replayed graph would see its own stale flags).
+      if (tune.chain && tune.chain_ok && tune.chain_mem && tune.chain_seq && dual == 1 &&
+          (tune.group == 8 || tune.group < 0)) {
+        LifeBlockParams ch = p;
+        ch.fold = 1;
+        ch.fold_lanes = 64;
+        const double cch =
+            plan_chain<T, 8>(ch, out_rows, simds, group_waves_per_simd<T, IO, 8>(), tune.target_waves, IO::XL);
+        // Opt-in: +2 % on the 8-GPU rank tile, -1 to -3 % on larger tiles and
+        // -12 % on 8192^2, where the folded last strip it gives up is worth
+        // more; choosing it per launch by the model measured slower than
+        // either (profiles/r02/chain_*.jsonl).
+        if (cch > 0) {
+          constexpr int64_t kSlot = int64_t(T - 1) * 2 * IO::W * 64;
+          const int64_t slots = int64_t(ch.ncolw) * ch.nseg;
+          ch.chain_flag = tune.chain_mem(0, size_t(slots) * 4);
+          ch.chain_buf = tune.chain_mem(1, size_t(slots * kSlot) * 4);
+          // 0 = never written, ~0 = the probe's marker
+          if (++*tune.chain_seq == 0 || *tune.chain_seq == 0xFFFFFFFFu) *tune.chain_seq = 1;
+          ch.chain_seq = *tune.chain_seq;
+          if (tune.chain == 2) ch.chain_seq = 0xFFFFFFFFu;  // timing probe: no wait, no fetch (wrong rows)
+          return launch_group<T, IO, 8>(ch, s);
+        }
+      }
       if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
       if (better(c8, cc)) return launch_group<T, IO, 8>(g8, s);
     }

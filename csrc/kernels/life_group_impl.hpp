@@ -47,7 +47,8 @@ namespace lb {
 // LDS slot of one boundary: [L-1][j][word i][lane] (lane-contiguous: a wave's
 // access is 64 consecutive dwords, conflict-free).  Slot m holds wave m's
 // top rows; wave 0 writes slot 0, which nobody reads (a branch around the
-// stores splits the prologue into ~30 blocks and doubled the registers).
+// stores splits the prologue into ~30 blocks and doubled the registers;
+// chained groups reuse it after the prologue barrier, chain_fetch).
 template <int T, int W>
 struct LdsSaver {
   uint32_t* slot;
@@ -57,6 +58,57 @@ struct LdsSaver {
     for (int i = 0; i < W; ++i) slot[(((L - 1) * 2 + j) * W + i) * 64 + lane] = v.w[i];
   }
 };
+
+// The grouped kernel's saver: LdsSaver, and with chained groups
+// (LifeBlockParams::chain_buf) wave 0 also stores its rows to the group's
+// global slot through `pub`, whose num_records is 0 for every
+// other wave, so their copies are dropped by the range check without a branch
+// in the unrolled prologue.  sc1: written through to the device-coherent level
+// (the reading group may run on another XCD, behind another L2).
+constexpr int kCpolSc1 = 16;
+template <int T, int W>
+struct ChainSaver {
+  uint32_t* slot;
+  int lane;
+  BufRsrc pub;
+  __device__ __forceinline__ void operator()(int L, int j, const Vec<W>& v) const {
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      const int idx = (((L - 1) * 2 + j) * W + i) * 64 + lane;
+      slot[idx] = v.w[i];
+      __builtin_amdgcn_raw_buffer_store_b32(v.w[i], pub, idx * 4, 0, kCpolSc1);
+    }
+  }
+};
+
+// Chained groups: the last wave of a group (not the strip's last) waits until
+// the group below has published its wave 0 rows (flag == chain_seq) and
+// copies them into LDS slot 0, which nobody reads once the prologue barrier
+// has passed.  Deadlock-free: chained strips are launched bottom group first
+// (life_group_kernel's block order), so the group waited on was dispatched
+// earlier, and its wave 0 publishes right after its prologue, before it waits
+// on anything.  Bounded (~0.1 s): giving up raises the launch's error word
+// (Backend::check_device_errors) instead of hanging the GPU.
+template <int T, int W>
+__device__ __forceinline__ void chain_fetch(const LifeBlockParams& p, int64_t slot_below, int64_t flag_below,
+                                            uint32_t* lds_slot, int lane) {
+  constexpr int kRows = (T - 1) * 2 * W;
+  bool arrived = false;
+  for (int spin = 0; spin < (1 << 16); ++spin) {  // each poll is an L2-bypassing load (~1-2 us)
+    if (__hip_atomic_load(p.chain_flag + flag_below, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.chain_seq) {
+      arrived = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (!arrived && p.err && lane == 0) __hip_atomic_store(p.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // LDS-DMA (global_load_lds, sc1): all rows in flight at once, no VGPRs.
+  const uint32_t* src = p.chain_buf + slot_below;
+#pragma unroll 1
+  for (int r = 0; r < kRows; ++r)
+    __builtin_amdgcn_global_load_lds(src + r * 64 + lane, lds_slot + r * 64, 4, 0, kCpolSc1);
+  __builtin_amdgcn_s_waitcnt(0);
+}
 
 #ifndef GOL_PRIO_BUCKETS
 #define GOL_PRIO_BUCKETS 4
@@ -207,6 +259,7 @@ void life_group_kernel(const LifeBlockParams p) {
   // recomputes its upper neighbour's last row, identically), so the wave's
   // control flow is the same for all of them; lanes carry their group's row
   // offset in their read / store offsets.
+  const bool chain = p.chain_buf != nullptr;  // fold == 1, row_alt == 0 (launch_T)
   int kcol, grp, nsub = 1, sub_lanes = 64;
   if (p.fold > 1 && blk >= (p.ncolw - 1) * p.nseg) {
     kcol = p.ncolw - 1;
@@ -216,21 +269,28 @@ void life_group_kernel(const LifeBlockParams p) {
   } else {
     kcol = blk / p.nseg;
     grp = blk - kcol * p.nseg;
+    if (chain) grp = p.nseg - 1 - grp;  // bottom group first: see chain_fetch
   }
   const auto group_end = [&](int g) {
     return p.row_lo + roff + int64_t(g) * p.seg_rows + min(g, p.seg_rem) + p.seg_rows + (g < p.seg_rem ? 1 : 0);
   };
-  const int64_t G1 = group_end(grp);
+  // Chained strips: wave wi = grp M + m starts at row_lo + wi q + 3 min(wi, x),
+  // the first x = seg_rem waves taking q + 3 rows; the strip's last wave ends
+  // at chain_end.
+  const int wi = grp * M + m;
+  const int64_t G1 = chain ? p.chain_end : group_end(grp);
   const int64_t G0 = G1 - p.seg_rows - (nsub > 1 ? (p.seg_rem > 0 ? 1 : 0) : (grp < p.seg_rem ? 1 : 0));
-  const int64_t in0 = G0 + int64_t(m) * p.grp_q - T;
-  const bool last = m == M - 1;
+  const int64_t in0 = chain ? p.row_lo + int64_t(wi) * p.grp_q + 3 * min(wi, p.seg_rem) - T
+                            : G0 + int64_t(m) * p.grp_q - T;
+  const bool chain_down = chain && m == M - 1 && grp < p.nseg - 1;  // fed by the group below
+  const bool last = m == M - 1 && !chain_down;
   constexpr int kPro = 2 * T;
   // Steps of the 3-step main loop end at kmain: q for waves 0..M-2 ((q - 2T)
   // % 3 == 0 by plan); the last wave's classic end (level-T rows up to
   // G1 - 1) takes kend steps, of which the last (kend - 2T) % 3 run as the
   // epilogue's plain input steps.
   const int kend = int(G1 + T - in0);
-  const int kmain = last ? kend - (kend - kPro) % 3 : p.grp_q;
+  const int kmain = last ? kend - (kend - kPro) % 3 : p.grp_q + (chain && wi < p.seg_rem ? 3 : 0);
   const int nfull = last ? (kend - kPro) % 3 : 2 * T;
 
   const LaneCols<IO> lc = lane_cols<IO>(p, kcol, lane, sub_lanes, nsub);
@@ -272,8 +332,22 @@ void life_group_kernel(const LifeBlockParams p) {
   wr.pitch = pitch;
   wr.col = lc.store_col;
 
-  const LdsSaver<T, W> saver{saved + m * kSlot, lane};
+  const int64_t chain_at = int64_t(kcol) * p.nseg + grp;  // this group's chain slot / flag
+  const bool publish = chain && m == 0 && grp > 0;
+  const ChainSaver<T, W> saver{saved + m * kSlot, lane,
+                             __builtin_amdgcn_make_buffer_rsrc(chain ? p.chain_buf + chain_at * kSlot : nullptr,
+                                                               short(0), publish ? kSlot * 4 : 0, kBufFlags)};
+  // A publishing wave runs its prologue at top priority and publishes before
+  // the barrier: its store round trip then overlaps the other waves'
+  // prologues, and the group above finds the rows ready when its last wave
+  // reaches the epilogue (on small tiles that wave has no main loop between).
+  if (publish) __builtin_amdgcn_s_setprio(3);
   prologue_tri<T, IO, 0>(st, rd, saver, NoBottom{});
+  if (publish) {  // wave-uniform: the rows are written through, then the flag
+    __builtin_amdgcn_s_waitcnt(0);
+    if (lane == 0) __hip_atomic_store(p.chain_flag + chain_at, p.chain_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!p.prio_boost) __builtin_amdgcn_s_setprio(0);
+  }
   __syncthreads();  // every wave's boundary rows are in LDS
 
   int k = kPro;
@@ -288,7 +362,9 @@ void life_group_kernel(const LifeBlockParams p) {
   }
 
   prio.done0 = (kmain - kPro) * T;
-  epilogue_tri<T, IO, 0, S0>(st, rd, saved + (m + 1) * kSlot, lane, wr, k, nfull, prio);  // k == kmain
+  if (chain_down && p.chain_seq != 0xFFFFFFFFu) chain_fetch<T, W>(p, (chain_at + 1) * kSlot, chain_at + 1, saved, lane);
+  epilogue_tri<T, IO, 0, S0>(st, rd, saved + (chain_down ? 0 : m + 1) * kSlot, lane, wr, k, nfull,
+                             prio);  // k == kmain
   prio.reset();
 
   if (p.changed) {
@@ -359,6 +435,66 @@ double plan_group(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int 
   p.seg_rows = int(out_rows / best_n);
   p.seg_rem = int(out_rows % best_n);
   p.grp_q = best_q;
+  return best;
+}
+
+// Plan of a chained launch (LifeBlockParams::chain_buf): n groups per strip,
+// waves of q or q + 3 rows (q >= 2T, (q - 2T) % 3 == 0; the first x take
+// q + 3) except the strip's last wave, which takes the remaining
+// r = out_rows - (n M - 1) q - 3x >= 0 rows with the classic end (span
+// r + T - 1).  No group boundary keeps a redundant triangle and no wave but
+// one per strip carries one.  Same makespan model as plan_group.  Returns
+// the cost, or -1 when no plan fits.
+template <int T, int M>
+double plan_chain(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int target_waves, int xl) {
+  constexpr double kOverhead = 0.4 * T;
+  const int64_t max_n = out_rows / (int64_t(M) * 2 * T);
+  int64_t best_n = 0, best_x = 0;
+  int best_q = 0;
+  double best = 1e300;
+  for (int64_t n = 1; n <= max_n; ++n) {
+    const int64_t nw = n * M;
+    const int64_t ideal = std::max<int64_t>(2 * T, (out_rows + T - 1) / nw);
+    int q = 0;
+    int64_t qx = 0;
+    double span = 1e300;
+    for (int64_t c = ideal - 6; c <= ideal + 3; ++c) {
+      if (c < 2 * T || (c - 2 * T) % 3 != 0) continue;
+      const int64_t rest = out_rows - (nw - 1) * c;  // the +3s and the last wave
+      if (rest < 0) continue;
+      const int64_t want_r = std::max<int64_t>(0, c + 4 - T);  // last wave's span ~ c + 3
+      const int64_t x = std::min<int64_t>(nw - 1, std::max<int64_t>(0, (rest - want_r) / 3));
+      const int64_t r = rest - 3 * x;
+      const double sp = std::max<double>(double(c + (x > 0 ? 3 : 0)), double(r + T - 1));
+      if (sp < span) {
+        span = sp;
+        q = int(c);
+        qx = x;
+      }
+    }
+    if (q == 0) continue;
+    const int64_t waves = int64_t(p.ncolw) * nw;
+    const int64_t k = ceil_div(waves, int64_t(simds));
+    const int64_t rounds = ceil_div(k, int64_t(occ));
+    const int64_t kk = std::min<int64_t>(k, occ);
+    double cost = double(rounds) * (span + kOverhead) * double(kk) * issue_factor(xl, kk);
+    if (target_waves > 0)
+      cost = 1.0 + double(std::llabs(waves - int64_t(target_waves)));
+    else if (rounds > 4)
+      break;
+    if (cost < best * 0.999) {
+      best = cost;
+      best_n = n;
+      best_q = q;
+      best_x = qx;
+    }
+  }
+  if (best_n == 0) return -1.0;
+  p.nseg = int(best_n);
+  p.grp_q = best_q;
+  p.seg_rows = 0;
+  p.seg_rem = int(best_x);  // waves with q + 3 rows
+  p.chain_end = p.row_lo + out_rows;
   return best;
 }
 

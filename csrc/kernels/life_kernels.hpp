@@ -54,6 +54,17 @@ struct LifeBlockParams {
   // block in sub-strips of fold_lanes lanes; 1 = no folding.
   int fold;
   int fold_lanes;
+  // Chained groups (life_group_kernel, LifeTuning::chain; null chain_buf =
+  // off): the last wave of group g ends like an inner wave, with the inverted
+  // triangle fed by group g + 1's wave 0 through global memory, so no group
+  // boundary keeps a redundant triangle.  Per (strip, group) slot: wave 0's
+  // saved boundary rows in chain_buf, and chain_flag = chain_seq once they are
+  // written.  Every group is M x grp_q rows but a strip's last one, which ends
+  // at chain_end.
+  uint32_t* chain_buf;
+  uint32_t* chain_flag;
+  uint32_t chain_seq;
+  int64_t chain_end;
 };
 
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
@@ -88,6 +99,13 @@ struct LifeTuning {
   int pipe = 0;             // level-pipelined wave pairs (life_pipe_impl.hpp): 0 off, 1 by the model, 2 forced
   bool wrap = true;         // wrap mode on whole-width tiles (BlockArgs::full_width, lane_cols)
   bool fold = true;         // folded last strip in wrap mode (life_group_kernel)
+  int chain = 0;            // chained groups (LifeBlockParams::chain_buf): 0 off, 1 on, 2 timing probe
+  bool chain_ok = false;    // this launch may use the chain memory (the backend's own stream, not captured)
+  uint32_t* chain_seq = nullptr;  // host launch counter of the chain flags
+  // Device memory of at least n bytes that persists across launches, stream-
+  // ordered like `scratch`: which = 0 the chain flags (zeroed when allocated),
+  // 1 the chain slots.
+  std::function<uint32_t*(int which, size_t n)> chain_mem;
   uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
   uint32_t* err = nullptr;       // LifeBlockParams::err
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).

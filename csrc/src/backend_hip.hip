@@ -71,6 +71,20 @@ class HipBackend final : public Backend {
     tune_.pipe = env_int("GOL_PIPE", 0);
     tune_.wrap = env_int("GOL_WRAP", 1) != 0;
     tune_.fold = env_int("GOL_FOLD", 1) != 0;
+    tune_.chain = env_int("GOL_CHAIN", 0);
+    tune_.chain_seq = &chain_seq_;
+    tune_.chain_mem = [this](int which, size_t n) -> uint32_t* {
+      void*& buf = chain_[which & 1];
+      size_t& cap = chain_bytes_[which & 1];
+      if (n > cap) {
+        HIP_CHECK(hipStreamSynchronize(stream_));  // earlier launches may still use it
+        if (buf) HIP_CHECK(hipFree(buf));
+        HIP_CHECK(hipMalloc(&buf, n));
+        if (which == 0) HIP_CHECK(hipMemsetAsync(buf, 0, n, stream_));
+        cap = n;
+      }
+      return static_cast<uint32_t*>(buf);
+    };
     if (const char* t = std::getenv("GOL_WG_TRACE")) {
       const std::string v(t);
       const size_t c = v.find(':');
@@ -100,6 +114,8 @@ class HipBackend final : public Backend {
     if (comm_) hipStreamSynchronize(comm_);
     if (stage_) hipFree(stage_);
     if (scratch_) hipFree(scratch_);
+    for (void* c : chain_)
+      if (c) hipFree(c);
     if (err_host_) hipHostFree(err_host_);
     for (auto& e : marks_)
       if (e) hipEventDestroy(e);
@@ -225,6 +241,11 @@ class HipBackend final : public Backend {
   }
 
   int run_block(const BlockArgs& a) override {
+    if (tune_.chain) {  // chained groups: own stream only, never inside a graph capture
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      tune_.chain_ok = (!a.stream || a.stream == stream_) && hipStreamIsCapturing(stream_, &cs) == hipSuccess &&
+                       cs == hipStreamCaptureStatusNone;
+    }
     if (trace_at_ >= 0 && launches_ == trace_at_) return run_block_traced(a);
     ++launches_;
     const int drift = hipk::launch_life_block(a, tune_, a.stream ? static_cast<hipStream_t>(a.stream) : stream_);
@@ -296,8 +317,9 @@ class HipBackend final : public Backend {
     const uint32_t e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
     if (e != 0) {
       *err_host_ = 0;
-      fail("life_short kernel: a wave gave up waiting for its neighbour's LDS rows (device error word " +
-           std::to_string(e) + "); the rows of that launch are invalid");
+      fail(std::string(e == 2 ? "life_group kernel (chained groups): a wave gave up waiting for the group below"
+                              : "life_short kernel: a wave gave up waiting for its neighbour's LDS rows") +
+           " (device error word " + std::to_string(e) + "); the rows of that launch are invalid");
     }
   }
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override {
@@ -388,6 +410,9 @@ class HipBackend final : public Backend {
   hipStream_t comm_ = nullptr;
   void* scratch_ = nullptr;  // split-schedule boundary states
   size_t scratch_bytes_ = 0;
+  void* chain_[2] = {nullptr, nullptr};  // chained groups: flags, slots (LifeTuning::chain_mem)
+  size_t chain_bytes_[2] = {0, 0};
+  uint32_t chain_seq_ = 0;
   int64_t launches_ = 0;
   int64_t trace_at_ = -1;
   std::string trace_path_;

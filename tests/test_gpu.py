@@ -228,6 +228,52 @@ def test_pipe_schedule_termination(gpu, monkeypatch, xlane, tmax):
     assert (out == ref).all()
 
 
+@pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100),
+                                 (32768, 600)])
+@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (0, 8), (3, 4), (0, 12)])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_chained_groups_vs_torch(gpu, monkeypatch, W, H, xlane, tmax, layout):
+    """Chained groups (GOL_CHAIN=1, life_group_impl.hpp chain_fetch: the last
+    wave of every group but a strip's last ends with the inverted triangle fed
+    by the next group's wave 0 through global memory and a per-launch flag)
+    against the fp32 conv oracle; few, many (several dispatch rounds) and a
+    middle number of groups via the wave-count target."""
+    monkeypatch.setenv("GOL_CHAIN", "1")
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    g = random_grid(W, H, W * 7 + H)
+    gens = 2 * tmax + 11
+    want = life_step_torch(g, gens, device="cuda")
+    for target in ("0", "100000", "3000"):
+        monkeypatch.setenv("GOL_TARGET_WAVES", target)
+        sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout=layout, tmax=tmax), engine="hip")
+        assert " chain" in sim.describe()["backend"]
+        sim.load(g)
+        sim.advance(gens)
+        assert (sim.tile() == want).all(), target
+
+
+@pytest.mark.parametrize("graphs", ["off", "on"])
+def test_chained_groups_termination_and_row_strips(gpu, monkeypatch, graphs):
+    """Exact Generations with chained groups, in graph capture (where the
+    chain is off) and on 1x4 row-strip subdomains of one GPU."""
+    monkeypatch.setenv("GOL_CHAIN", "1")
+    monkeypatch.setenv("GOL_TARGET_WAVES", "100000")
+    grid = np.zeros((1024, 512), dtype=np.uint8)
+    W, H, seed, density = CONVERGING[5]
+    grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(grid)
+    for layout in ("bits", "u8"):
+        out, rep = simulate(grid, 1000, engine="hip", layout=layout, tmax=16, graphs=graphs)
+        assert rep.generations == rgens, layout
+        assert (out == ref).all(), layout
+    grp = InProcessGroup(LifeConfig(512, 1024, decomp="1x4", tmax=16, epoch=64, poll_gens=64, graphs=graphs), 4,
+                         engine="hip")
+    grp.load(grid)
+    reps = grp.run()
+    assert {r.generations for r in reps} == {rgens}
+    assert (grp.gather() == ref).all()
+
+
 @pytest.mark.parametrize("words", [79, 93, 136, 1024])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (0, 8), (3, 4)])
 @pytest.mark.parametrize("wrap,fold", [("1", "1"), ("1", "0"), ("0", "0")])
