@@ -102,13 +102,14 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       // global memory, so no wave carries a redundant triangle but the
       // strip's last.  Stream launches only (the flags count launches, so a
       // replayed graph would see its own stale flags).
-      if (tune.chain && tune.chain_ok && tune.chain_mem && tune.chain_seq && dual == 1 &&
-          (tune.group == 8 || tune.group < 0)) {
+      if (tune.chain && tune.chain_ok && tune.chain_mem && tune.chain_seq && dual == 1) {
         LifeBlockParams ch = p;
         ch.fold = 1;
         ch.fold_lanes = 64;
+        const bool m4 = tune.group == 4;  // 4-wave groups: every 4th boundary chained
         const double cch =
-            plan_chain<T, 8>(ch, out_rows, simds, group_waves_per_simd<T, IO, 8>(), tune.target_waves, IO::XL);
+            m4 ? plan_chain<T, 4>(ch, out_rows, simds, group_waves_per_simd<T, IO, 4>(), tune.target_waves, IO::XL)
+               : plan_chain<T, 8>(ch, out_rows, simds, group_waves_per_simd<T, IO, 8>(), tune.target_waves, IO::XL);
         // Opt-in: +2 % on the 8-GPU rank tile, -1 to -3 % on larger tiles and
         // -12 % on 8192^2, where the folded last strip it gives up is worth
         // more; choosing it per launch by the model measured slower than
@@ -122,7 +123,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
           if (++*tune.chain_seq == 0 || *tune.chain_seq == 0xFFFFFFFFu) *tune.chain_seq = 1;
           ch.chain_seq = *tune.chain_seq;
           if (tune.chain == 2) ch.chain_seq = 0xFFFFFFFFu;  // timing probe: no wait, no fetch (wrong rows)
-          return launch_group<T, IO, 8>(ch, s);
+          return m4 ? launch_group<T, IO, 4>(ch, s) : launch_group<T, IO, 8>(ch, s);
         }
       }
       if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
