@@ -46,7 +46,10 @@ std::string life_block_variant(Layout layout, const LifeTuning& tune) {
          (grouped ? (tune.group < 0 ? std::string(" group=auto") : " group=" + std::to_string(tune.group)) : "") +
          (grouped && tune.short_seg == 1 ? " short=auto" : grouped && tune.short_seg == 2 ? " short=forced" : "") +
          (grouped && tune.pipe == 1 ? " pipe=auto" : grouped && tune.pipe == 2 ? " pipe=forced" : "") +
-         (grouped && tune.chain == 1 ? " chain" : grouped && tune.chain == 2 ? " chain=probe" : "");
+         (grouped && tune.chain == 1    ? " chain"
+          : grouped && tune.chain == 2 ? " chain=probe"
+          : grouped && tune.chain < 0  ? " chain=tuned"
+                                       : "");
 }
 
 int life_block_max_T(Layout layout, const LifeTuning& tune) {

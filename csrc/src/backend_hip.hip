@@ -11,6 +11,8 @@
 #include <array>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -71,7 +73,9 @@ class HipBackend final : public Backend {
     tune_.pipe = env_int("GOL_PIPE", 0);
     tune_.wrap = env_int("GOL_WRAP", 1) != 0;
     tune_.fold = env_int("GOL_FOLD", 1) != 0;
-    tune_.chain = env_int("GOL_CHAIN", 0);
+    chain_mode_ = env_int("GOL_CHAIN", -1);
+    tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
+    tune_log_ = env_int("GOL_TUNE_LOG", 0) != 0;
     tune_.chain_seq = &chain_seq_;
     tune_.chain_mem = [this](int which, size_t n) -> uint32_t* {
       void*& buf = chain_[which & 1];
@@ -116,6 +120,11 @@ class HipBackend final : public Backend {
     if (scratch_) hipFree(scratch_);
     for (void* c : chain_)
       if (c) hipFree(c);
+    for (auto& p : pending_) {
+      hipEventDestroy(p.e0);
+      hipEventDestroy(p.e1);
+    }
+    for (hipEvent_t e : free_events_) hipEventDestroy(e);
     if (err_host_) hipHostFree(err_host_);
     for (auto& e : marks_)
       if (e) hipEventDestroy(e);
@@ -124,8 +133,10 @@ class HipBackend final : public Backend {
   }
 
   std::string name() const override {
-    return "hip:" + std::to_string(dev_) + ":" + arch_ + " [" + hipk::life_block_variant(Layout::Bits, tune_) +
-           "; " + hipk::life_block_variant(Layout::U8, tune_) + "]";
+    hipk::LifeTuning t = tune_;
+    t.chain = chain_mode_;
+    return "hip:" + std::to_string(dev_) + ":" + arch_ + " [" + hipk::life_block_variant(Layout::Bits, t) +
+           "; " + hipk::life_block_variant(Layout::U8, t) + "]";
   }
   int preferred_tmax(Layout l) const override { return hipk::life_block_max_T(l, tune_); }
   bool is_device() const override { return true; }
@@ -241,16 +252,99 @@ class HipBackend final : public Backend {
   }
 
   int run_block(const BlockArgs& a) override {
-    if (tune_.chain) {  // chained groups: own stream only, never inside a graph capture
+    if (chain_mode_) {  // chained groups: own stream only, never inside a graph capture
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       tune_.chain_ok = (!a.stream || a.stream == stream_) && hipStreamIsCapturing(stream_, &cs) == hipSuccess &&
                        cs == hipStreamCaptureStatusNone;
     }
     if (trace_at_ >= 0 && launches_ == trace_at_) return run_block_traced(a);
     ++launches_;
-    const int drift = hipk::launch_life_block(a, tune_, a.stream ? static_cast<hipStream_t>(a.stream) : stream_);
+    hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
+    Pending* timed = nullptr;
+    if (chain_mode_ < 0) timed = autotune_chain(a);
+    if (timed) HIP_CHECK(hipEventRecord(timed->e0, s));
+    const int drift = hipk::launch_life_block(a, tune_, s);
     HIP_CHECK(hipGetLastError());
+    if (timed) HIP_CHECK(hipEventRecord(timed->e1, s));
     return drift;
+  }
+
+  // Launch-shape autotuning of the chained groups (GOL_CHAIN=-1).  Chaining
+  // changes nothing but the inside of a launch (same rows, same flags), so
+  // every rank may decide for itself.  Per launch shape (layout, T, rows / 256,
+  // row width, dual, drift, whole width) the first kTrials launches of each
+  // option are timed with events, alternating; the completed timings are
+  // collected without blocking at later launches, and the shape keeps the
+  // option whose median is >= 1 % faster (else the plain grouped kernel).
+  // Measured: +2 % on the 8-GPU rank tile, -1...-12 % on other tiles
+  // (docs/PERFORMANCE.md), so no static rule picks it well.
+  static constexpr int kTrials = 3;
+  using TuneKey = std::array<int64_t, 7>;
+  struct TuneStats {
+    std::vector<float> ms[2];
+    int issued[2] = {0, 0};
+    int pick = -1;
+  };
+  struct Pending {
+    TuneKey key;
+    int opt;
+    hipEvent_t e0, e1;
+  };
+  Pending* autotune_chain(const BlockArgs& a) {
+    collect_tuning();
+    tune_.chain = 0;
+    if (!tune_.chain_ok) return nullptr;
+    const TuneKey key{int64_t(a.g.layout), a.T, (a.row_hi - a.row_lo) >> 8, a.g.Wp(), a.dual_offset != 0,
+                      a.allow_drift, a.full_width};
+    TuneStats& st = tuned_[key];
+    if (st.pick >= 0) {
+      tune_.chain = st.pick;
+      return nullptr;
+    }
+    const int opt = st.issued[0] <= st.issued[1] ? 0 : 1;
+    if (st.issued[opt] >= kTrials) return nullptr;  // trials in flight: plain kernel, untimed
+    ++st.issued[opt];
+    tune_.chain = opt;
+    Pending p{key, opt, event_take(), event_take()};
+    pending_.push_back(p);
+    return &pending_.back();
+  }
+  void collect_tuning() {
+    while (!pending_.empty()) {
+      Pending& p = pending_.front();
+      const hipError_t q = hipEventQuery(p.e1);
+      if (q == hipErrorNotReady) break;
+      HIP_CHECK(q);
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, p.e0, p.e1));
+      TuneStats& st = tuned_[p.key];
+      st.ms[p.opt].push_back(ms);
+      if (st.pick < 0 && int(st.ms[0].size()) >= kTrials && int(st.ms[1].size()) >= kTrials) {
+        const auto median = [](std::vector<float> v) {
+          std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+          return v[v.size() / 2];
+        };
+        const float m0 = median(st.ms[0]), m1 = median(st.ms[1]);
+        st.pick = m1 < 0.99f * m0 ? 1 : 0;
+        if (tune_log_)
+          std::fprintf(stderr, "gol autotune: layout %d T %d rows~%lld x %lld words: plain %.1f us, chained %.1f us -> %s\n",
+                       int(p.key[0]), int(p.key[1]), (long long)(p.key[2] << 8), (long long)p.key[3], 1e3 * m0,
+                       1e3 * m1, st.pick ? "chained" : "plain");
+      }
+      free_events_.push_back(p.e0);
+      free_events_.push_back(p.e1);
+      pending_.pop_front();
+    }
+  }
+  hipEvent_t event_take() {
+    if (free_events_.empty()) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreate(&e));
+      return e;
+    }
+    hipEvent_t e = free_events_.back();
+    free_events_.pop_back();
+    return e;
   }
   bool drifts(Layout l) const override {
     return tune_.xlane == hipk::kXlaneAdd && (l == Layout::Bits ? tune_.wpl_bits < 2 : true);
@@ -413,6 +507,11 @@ class HipBackend final : public Backend {
   void* chain_[2] = {nullptr, nullptr};  // chained groups: flags, slots (LifeTuning::chain_mem)
   size_t chain_bytes_[2] = {0, 0};
   uint32_t chain_seq_ = 0;
+  int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, 2 timing probe, -1 autotuned per launch shape
+  bool tune_log_ = false;
+  std::map<TuneKey, TuneStats> tuned_;
+  std::deque<Pending> pending_;  // timed trial launches not collected yet
+  std::vector<hipEvent_t> free_events_;
   int64_t launches_ = 0;
   int64_t trace_at_ = -1;
   std::string trace_path_;

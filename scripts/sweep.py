@@ -43,6 +43,9 @@ def main() -> int:
                 return 1
             rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
             rec["sweep_config"] = line
+            tune = [ln for ln in r.stderr.splitlines() if "autotune" in ln]
+            if tune:
+                rec["autotune_log"] = tune[:64]
             rec["wall_s"] = round(time.time() - t0, 2)
             f.write(json.dumps(rec) + "\n")
             f.flush()
