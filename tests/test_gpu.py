@@ -252,6 +252,25 @@ def test_chained_groups_vs_torch(gpu, monkeypatch, W, H, xlane, tmax, layout):
         assert (sim.tile() == want).all(), target
 
 
+def test_chain_autotuning_is_exact(gpu, monkeypatch, capfd):
+    """Default launch-shape autotuning (GOL_CHAIN=-1): trial launches of both
+    options (timed with events) and the settled choice give the same rows as
+    the fp32 conv oracle, and every launch shape reaches a decision."""
+    monkeypatch.setenv("GOL_CHAIN", "-1")
+    monkeypatch.setenv("GOL_TUNE_LOG", "1")
+    W, H, gens = 8192, 1024, 16 * 12
+    g = random_grid(W, H, 4242)
+    want = life_step_torch(g, gens, device="cuda")
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=16, epoch=32), engine="hip")
+    assert "chain=tuned" in sim.describe()["backend"]
+    sim.load(g)
+    sim.advance(gens // 2)  # the trials (6 launches per shape); returns with the device idle
+    sim.advance(gens - gens // 2)  # collects them and runs the settled choice
+    assert (sim.tile() == want).all()
+    err = capfd.readouterr().err
+    assert "gol autotune:" in err and ("-> plain" in err or "-> chained" in err), err[-2000:]
+
+
 @pytest.mark.parametrize("graphs", ["off", "on"])
 def test_chained_groups_termination_and_row_strips(gpu, monkeypatch, graphs):
     """Exact Generations with chained groups, in graph capture (where the
