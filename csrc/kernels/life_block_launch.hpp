@@ -176,6 +176,12 @@ void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const Lif
     case 8: launch_T<8, IO>(p, out_rows, tune, s); break;
     case 12: launch_T<12, IO>(p, out_rows, tune, s); break;
     case 16: launch_T<16, IO>(p, out_rows, tune, s); break;
+    case 24:  // byte layout only: HBM-bound, so a deeper pass pays (one read + write per launch)
+      if constexpr (!IO::kBits) {
+        launch_T<24, IO>(p, out_rows, tune, s);
+        break;
+      }
+      [[fallthrough]];
     default: fail("life_block: unsupported temporal block size " + std::to_string(T));
   }
 }
