@@ -281,6 +281,15 @@ struct BitsIO {
   }
 };
 
+// Byte-layout cache policies (experiment knobs; aux bits of the buffer
+// store: 2 = nt): the byte kernel streams the whole grid once per pass.
+#ifndef GOL_U8_STORE_CPOL
+#define GOL_U8_STORE_CPOL 0
+#endif
+#ifndef GOL_U8_LOAD_NT
+#define GOL_U8_LOAD_NT 0
+#endif
+
 template <int W_, int XL_>
 struct U8IO {
   static constexpr int W = W_, XL = XL_;
@@ -293,8 +302,15 @@ struct U8IO {
 #pragma unroll
     for (int i = 0; i < W; ++i) {
       const uint4* p = reinterpret_cast<const uint4*>(row + 32 * int64_t(off[i]));
+#if GOL_U8_LOAD_NT
+      const U32x4* v = reinterpret_cast<const U32x4*>(p);
+      const U32x4 v0 = __builtin_nontemporal_load(v), v1 = __builtin_nontemporal_load(v + 1);
+      r.q[2 * i] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+      r.q[2 * i + 1] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+#else
       r.q[2 * i] = p[0];
       r.q[2 * i + 1] = p[1];
+#endif
     }
     return r;
   }
@@ -329,8 +345,8 @@ struct U8IO {
   __device__ static __forceinline__ void store_buf(BufRsrc row, int voff, uint32_t w) {
     const U32x4 a = {spread(w, 0), spread(w, 1), spread(w, 2), spread(w, 3)};
     const U32x4 b = {spread(w, 4), spread(w, 5), spread(w, 6), spread(w, 7)};
-    __builtin_amdgcn_raw_buffer_store_b128(a, row, voff, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(b, row, voff + 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(a, row, voff, 0, GOL_U8_STORE_CPOL);
+    __builtin_amdgcn_raw_buffer_store_b128(b, row, voff + 16, 0, GOL_U8_STORE_CPOL);
   }
 };
 
