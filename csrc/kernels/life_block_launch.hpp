@@ -182,6 +182,14 @@ void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const Lif
         break;
       }
       [[fallthrough]];
+    case 32:
+      if constexpr (!IO::kBits) {
+        if (T == 32) {
+          launch_T<32, IO>(p, out_rows, tune, s);
+          break;
+        }
+      }
+      [[fallthrough]];
     default: fail("life_block: unsupported temporal block size " + std::to_string(T));
   }
 }

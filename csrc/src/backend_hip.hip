@@ -359,17 +359,23 @@ class HipBackend final : public Backend {
   //
   // The byte layout is HBM-bound on large tiles (every T-generation pass
   // reads and writes the whole byte grid once: ~500 us per pass at 32768^2,
-  // any T), so there T = 24 (210 VGPRs, 2 waves/SIMD) cuts the traffic by a
-  // third: 32768^2 31.3 -> 21.3 us per generation, 65536^2 128 -> 86,
-  // 32768 x 16384 16.0 -> 11.4, 32768 x 8192 8.1 -> 6.6.  On tiles with fewer
-  // than one 4T-row segment per SIMD it loses (8192^2 2.83 -> 3.03,
-  // 32768 x 4096 3.89 -> 4.42; profiles/r02/u8_t24*.jsonl), so those stay at 16.
+  // any T), so there it runs T = 32 (245 VGPRs) or 24 (210), still 2 waves
+  // per SIMD: 32768^2 31.3 (T = 16) -> 21.4 (24) -> 17.7 (32) us per
+  // generation, 65536^2 128 -> 83 -> 64, 32768 x 16384 16.0 -> 11.4 -> 10.4,
+  // 32768 x 8192 8.1 -> 6.6 -> 6.3.  The deepest T whose 4T-row segments
+  // give every SIMD one is taken; below that T = 16 (8192^2: 2.83 vs 3.03 at
+  // 24; 32768 x 4096: 3.7-3.9 vs 4.4 at 24 and 4.9 at 32;
+  // profiles/r02/u8_t24*.jsonl, u8_t32.jsonl).
   KernelChoice choose_kernel(Layout l, int64_t rows, int64_t cols, int tmax_req) const override {
     KernelChoice k{tmax_req > 0 ? tmax_req : preferred_tmax(l), false};
     if (l == Layout::U8 && tmax_req <= 0 && !tune_.u8_lds) {
-      constexpr int64_t kT = 24;
       const int64_t strips = ceil_div(cols + 32 * 16, 62 * 32);
-      k.tmax = strips * (rows / (4 * kT)) >= int64_t(4) * cus_ ? int(kT) : 16;
+      k.tmax = 16;
+      for (int64_t kT : {32, 24})
+        if (strips * (rows / (4 * kT)) >= int64_t(4) * cus_) {
+          k.tmax = int(kT);
+          break;
+        }
     }
     const bool one_word = l == Layout::U8 || tune_.wpl_bits < 2;
     if (tune_.xlane == hipk::kXlaneAdd && one_word) {

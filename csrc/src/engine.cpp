@@ -11,9 +11,9 @@
 namespace gol {
 
 namespace {
-// Temporal block sizes built for every backend; 24 for the byte layout only
-// (HBM-bound there: one grid read + write per pass, docs/PERFORMANCE.md).
-constexpr int kTSizes[] = {24, 16, 12, 8, 4, 2, 1};
+// Temporal block sizes built for every backend; 32 and 24 for the byte layout
+// only (HBM-bound there: one grid read + write per pass, docs/PERFORMANCE.md).
+constexpr int kTSizes[] = {32, 24, 16, 12, 8, 4, 2, 1};
 
 int64_t min_tile_rows(const Decomposition& d) { return d.H / d.Py; }
 int64_t min_tile_cols(const Decomposition& d) { return (d.W / d.col_unit / d.Px) * d.col_unit; }
@@ -36,7 +36,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // made for the smallest tile of the decomposition, not this rank's.
   const Backend::KernelChoice kc =
       be_->choose_kernel(cfg_.layout, min_tile_rows(dec_), std::max<int64_t>(1, min_tile_cols(dec_)), cfg_.tmax);
-  tmax_ = std::min(kc.tmax, cfg_.layout == Layout::U8 ? 24 : 16);
+  tmax_ = std::min(kc.tmax, cfg_.layout == Layout::U8 ? 32 : 16);
   // Epoch depth: a deeper halo means fewer latency-bound exchanges (or local
   // periodic fills: two ~5 us launches each) but ~D redundant rows per epoch.
   // With the grouped kernel the per-rank tile costs the same from 8T to 24T
