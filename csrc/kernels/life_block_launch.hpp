@@ -165,6 +165,23 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
     hipLaunchKernelGGL((life_block_kernel<T, IO, false>), grid, block, 0, s, p);
 }
 
+// Deep byte-layout passes (T = 24, 32): instantiated in translation units of
+// their own (life_block_u8_w1_*_t24 / _t32.hip, `extern template` in the
+// variant TU), so the build compiles them in parallel.
+template <int T, class IO>
+void launch_deep(const LifeBlockParams& p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
+  launch_T<T, IO>(p, out_rows, tune, s);
+}
+#define GOL_U8_DEEP(KW, T_, XL_)                                                                   \
+  namespace gol {                                                                                  \
+  namespace hipk {                                                                                 \
+  namespace lb {                                                                                   \
+  KW template void launch_deep<T_, U8IO<1, XL_>>(const LifeBlockParams&, int64_t, const LifeTuning&, \
+                                                 hipStream_t);                                     \
+  }                                                                                                \
+  }                                                                                                \
+  }
+
 // Host entry point of one compiled variant (instantiated once per
 // translation unit, life_block_*.hip).
 template <class IO>
@@ -178,14 +195,14 @@ void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const Lif
     case 16: launch_T<16, IO>(p, out_rows, tune, s); break;
     case 24:  // byte layout only: HBM-bound, so a deeper pass pays (one read + write per launch)
       if constexpr (!IO::kBits) {
-        launch_T<24, IO>(p, out_rows, tune, s);
+        launch_deep<24, IO>(p, out_rows, tune, s);
         break;
       }
       [[fallthrough]];
     case 32:
       if constexpr (!IO::kBits) {
         if (T == 32) {
-          launch_T<32, IO>(p, out_rows, tune, s);
+          launch_deep<32, IO>(p, out_rows, tune, s);
           break;
         }
       }

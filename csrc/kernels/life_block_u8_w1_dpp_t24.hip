@@ -1,0 +1,5 @@
+// T = 24 byte-layout passes of the U8IO<1, kXlaneDpp> variant
+// (life_block_launch.hpp launch_deep), in a translation unit of their own.
+#include "life_block_launch.hpp"
+
+GOL_U8_DEEP(, 24, kXlaneDpp)
