@@ -38,7 +38,8 @@ class LifeConfig:
     sim_freq: int = 3
     layout: str = "auto"        # auto | bits | u8
     decomp: str = "auto"        # auto | PxQ
-    tmax: int = 0               # generations per kernel launch (0 = the backend's choice: 12 adder / 16 DPP)
+    tmax: int = 0               # generations per kernel launch (0 = the backend's choice: bits 12 adder /
+                                # 16 DPP; u8 32 / 24 / 16 by tile size)
     epoch: int = 0              # generations per halo exchange (0 = 8*tmax, 16*tmax with several ranks)
     poll_gens: int = 0          # generations between termination polls (0 = 256, 512 with several ranks)
     overlap: str = "auto"       # auto | on | off | edges: overlap the row halo exchange with compute
