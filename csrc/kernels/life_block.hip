@@ -113,7 +113,10 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   // left halo must hold the 2T cells its one-sided light cone consumes (wrap
   // mode reads the wrapped owned words instead).
   if (x == kXlaneAuto) x = kXlaneAdd;  // the engine decided through allow_drift
-  if (x == kXlaneAdd && !(a.allow_drift && (p.wrap_w > 0 || 32 * g.hw >= 2 * a.T))) x = kXlaneDpp;
+  // The one-sided window also consumes 2T cells of its wave's single halo
+  // word per pass, so passes deeper than 16 (the byte layout's T = 24 / 32)
+  // run the DPP window.
+  if (x == kXlaneAdd && !(a.allow_drift && a.T <= 16 && (p.wrap_w > 0 || 32 * g.hw >= 2 * a.T))) x = kXlaneDpp;
   if (x == kXlaneAdd) {
     (g.layout == Layout::U8 ? launch_u8_w1_add : launch_bits_w1_add)(p, rows, a.T, tune, stream);
     return a.T;

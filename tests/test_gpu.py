@@ -82,6 +82,33 @@ def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
     assert (life_step(g, gens, engine="hip", layout="u8", tmax=tmax) == want).all()
 
 
+@pytest.mark.parametrize("tmax", [24, 32])
+@pytest.mark.parametrize("xlane", [0, 2, 3])
+def test_deep_byte_passes_vs_torch(gpu, monkeypatch, tmax, xlane):
+    """T = 24 / 32 byte-layout passes (life_block_u8_w1_*_t24/_t32.hip, the
+    HBM-bound layout's deep passes) in every byte variant and schedule,
+    against the fp32 conv oracle, and the exact Generations count."""
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    for group in ("8", "4", "0"):
+        monkeypatch.setenv("GOL_GROUP", group)
+        for W, H in [(32 * 200, 900), (1999, 777)]:
+            g = random_grid(W, H, W + H + tmax)
+            gens = 2 * tmax + 7
+            want = life_step_torch(g, gens, device="cuda")
+            sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=tmax), engine="hip")
+            assert sim.describe()["tmax"] == tmax
+            sim.load(g)
+            sim.advance(gens)
+            assert (sim.tile() == want).all(), (group, W, H)
+    grid = np.zeros((1024, 512), dtype=np.uint8)
+    W, H, seed, density = CONVERGING[5]
+    grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(grid)
+    out, rep = simulate(grid, 1000, engine="hip", layout="u8", tmax=tmax)
+    assert rep.generations == rgens
+    assert (out == ref).all()
+
+
 @pytest.mark.parametrize("group", ["0", "4", "8", "-1"])
 @pytest.mark.parametrize("tmax", [4, 8, 12, 16])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
