@@ -110,10 +110,11 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
         const double cch =
             m4 ? plan_chain<T, 4>(ch, out_rows, simds, group_waves_per_simd<T, IO, 4>(), tune.target_waves, IO::XL)
                : plan_chain<T, 8>(ch, out_rows, simds, group_waves_per_simd<T, IO, 8>(), tune.target_waves, IO::XL);
-        // Opt-in: +2 % on the 8-GPU rank tile, -1 to -3 % on larger tiles and
-        // -12 % on 8192^2, where the folded last strip it gives up is worth
-        // more; choosing it per launch by the model measured slower than
-        // either (profiles/r02/chain_*.jsonl).
+        // tune.chain is set per launch by the backend (HipBackend's launch-
+        // shape autotuning, or GOL_CHAIN=1 forced): +2 % on the 8-GPU rank
+        // tile, -1 to -3 % on larger tiles and -12 % on 8192^2, where the
+        // folded last strip it gives up is worth more; choosing it by the
+        // makespan model measured slower than either (profiles/r02/chain/).
         if (cch > 0) {
           constexpr int64_t kSlot = int64_t(T - 1) * 2 * IO::W * 64;
           const int64_t slots = int64_t(ch.ncolw) * ch.nseg;
