@@ -20,8 +20,25 @@ Strong scaling: the grid is fixed, N GPUs split it into 1 x N row strips,
 one process per GPU, halos and flag reductions over RCCL/xGMI.
 
     python bench.py                                   # 1 GPU
+    python bench.py --gpus 8                          # launches 8 rank processes itself
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
+
+`--gpus N` is the reference's `mpiexec -n P` (README.md:56, src/game_mpi.c:2):
+without a launcher environment (no WORLD_SIZE) bench.py starts N rank
+processes through torch.distributed.run before it touches torch or the GPU,
+relays rank 0's JSON line and exits with the launcher's status.  Under a
+launcher, WORLD_SIZE must equal --gpus (else it exits non-zero).  Each rank
+needs a GPU of its own; --share-gpus lets ranks share devices (RCCL then runs
+them as separate "nodes" over its socket transport: a correctness rehearsal
+of the multi-rank path on a one-GPU box, not a performance number).
+
+After the timed steps (outside the timed region) the same engine runs one
+more step with per-phase device timing (kernels / halos / fills / flag
+reductions, --no-phase-step to skip), and then --verify G generations
+that are checked bit for bit against an fp32 PyTorch conv2d oracle and the
+byte-per-cell layout, started from the engine's state at that point:
+`verified` in the JSON line says whether the credited schedule is exact.
 
 Data: synthetic - counter-based RNG random init at density 0.5 (the same
 distribution as generate.sh's $((RANDOM % 2))), generated on the device.
@@ -31,6 +48,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -60,8 +79,37 @@ def _claim_stdout() -> int:
     return real
 
 
-def main() -> int:
-    out_fd = _claim_stdout()
+def _free_port() -> int:
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _launch_ranks(ngpus: int, argv: list[str], out_fd: int) -> int:
+    """`mpiexec -n N` for bench.py: N rank processes on this node, one per
+    GPU, through torch.distributed.run.  Nothing here touches torch or the
+    GPU; rank 0's JSON line is relayed to stdout, everything else to stderr."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ngpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    log(f"bench.py: launching {ngpus} rank processes: {' '.join(cmd)}")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE)
+    assert proc.stdout is not None
+    lines = 0
+    for raw in proc.stdout:
+        if raw.lstrip().startswith(b"{") and b'"metric"' in raw:
+            os.write(out_fd, raw)
+            lines += 1
+        else:
+            sys.stderr.buffer.write(raw)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc == 0 and lines != 1:
+        log(f"bench.py: the rank processes printed {lines} result lines, expected 1")
+        return 1
+    return rc
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="timed steps (one step = --gens-per-step generations)")
@@ -75,7 +123,8 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=0, help="grid height if not square (experiments only)")
     ap.add_argument("--layout", default="bits", choices=["bits", "u8"])
     ap.add_argument("--engine", default="hip", choices=["hip", "cpu"])
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"],
+                    help="halo transport between rank processes (auto: rccl on GPU, torch/gloo on CPU)")
     ap.add_argument("--decomp", default="auto")
     ap.add_argument("--tmax", type=int, default=0)
     ap.add_argument("--epoch", type=int, default=0)
@@ -88,17 +137,56 @@ def main() -> int:
                     help="one GPU: run the multi-rank row-strip schedule (epoch depth, early-boundary overlap, "
                          "RCCL send/recv + all-reduce) against a 1-rank RCCL communicator that exchanges with "
                          "itself; use with --height H/N to rehearse one rank of an N-GPU run")
-    a = ap.parse_args()
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="let ranks share GPUs (rehearsal of the multi-rank path on fewer GPUs than ranks)")
+    ap.add_argument("--verify", type=int, default=240,
+                    help="after the timed steps, run G more generations and check them against the fp32 "
+                         "PyTorch conv2d oracle and the u8 layout (0: skip)")
+    ap.add_argument("--no-phase-step", action="store_true",
+                    help="skip the extra per-phase-timed step after the timed ones")
+    return ap.parse_args(argv)
 
+
+def main() -> int:
+    out_fd = _claim_stdout()
+    a = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if a.gpus > 1:
+            return _launch_ranks(a.gpus, sys.argv[1:], out_fd)
+    elif int(env_world) != a.gpus:
+        log(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_world} ranks; refusing to "
+            "report a number for a different GPU count")
+        return 2
+
+    from gol_amd.parallel.dist import env_rank  # noqa: PLC0415
+
+    rank, world, local = env_rank()
+    on_gpu = a.engine == "hip"
+    shared = False
+    if on_gpu and world > 1:
+        import torch  # noqa: PLC0415
+
+        ndev = torch.cuda.device_count()  # does not initialise the GPU
+        if ndev < world:
+            if not a.share_gpus:
+                log(f"bench.py: {world} ranks but {ndev} GPU(s) visible; every rank needs a GPU of its own "
+                    "(--share-gpus for a shared-device rehearsal)")
+                return 2
+            # RCCL refuses two ranks of one communicator on one device when
+            # they share a host hash; distinct host ids make every rank its
+            # own "node" (socket transport over loopback).
+            shared = True
+            os.environ["NCCL_HOSTID"] = f"gol-bench-rank{rank}"
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        local = local % max(1, ndev)
+
+    import numpy as np  # noqa: PLC0415
     import torch  # noqa: PLC0415
 
     from gol_amd import LifeConfig, Simulation, make_backend, native  # noqa: PLC0415
-    from gol_amd.parallel.dist import allreduce_max_float, env_rank  # noqa: PLC0415
+    from gol_amd.parallel.dist import allreduce_max_float  # noqa: PLC0415
 
-    rank, world, local = env_rank()
-    if world != a.gpus:
-        log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    on_gpu = a.engine == "hip"
     if on_gpu:
         if not torch.cuda.is_available():
             raise SystemExit("bench.py: no GPU visible (use --engine cpu for a CPU dry run)")
@@ -108,7 +196,7 @@ def main() -> int:
     if world > 1:
         from gol_amd.parallel.dist import init_process_group, make_transport  # noqa: PLC0415
 
-        dist = init_process_group("nccl" if on_gpu else "gloo")
+        dist = init_process_group("nccl" if on_gpu and not shared else "gloo")
         transport = make_transport(a.comm, backend, local)
     elif a.rehearse_rccl and on_gpu:
         C = native()
@@ -119,7 +207,8 @@ def main() -> int:
     S = a.size
     Hg = a.height or S
     gps = max(1, a.gens_per_step)
-    total = a.prewarm + (a.warmup + a.steps * a.repeats) * gps
+    extra = (0 if a.no_phase_step else gps) + max(0, a.verify)
+    total = a.prewarm + (a.warmup + a.steps * a.repeats) * gps + extra
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
                      poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs, timing_barriers=False,
                      self_exchange=bool(a.rehearse_rccl and world == 1),
@@ -159,6 +248,54 @@ def main() -> int:
     gens = max(1, executed)
     value = float(S) * float(Hg) * gens / dt
     stops = sorted({r.stop_reason for r in rs})
+
+    # One more step with per-phase device timing (outside the timed region:
+    # the event pairs around every operation add a little launch overhead).
+    phases = None
+    if not a.no_phase_step:
+        sync()
+        eng.phase_timing = True
+        r = step()
+        eng.phase_timing = False
+        sync()
+        phases = {k: allreduce_max_float(float(getattr(r, k))) for k in
+                  ("loop_ms", "compute_ms", "halo_ms", "fill_ms", "allreduce_ms")}
+        phases["generations"] = int(r.executed)
+        phases["rank"] = "max over ranks"
+
+    # Correctness gate at the credited configuration: the same engine (same
+    # kernel choice, epoch, wrap + fold, autotuned chain picks, drift state)
+    # continues from its current state; the oracle restarts from a snapshot.
+    verify = None
+    verified = None
+    if a.verify > 0:
+        from gol_amd.ops.life_ops import life_step_torch  # noqa: PLC0415
+        from gol_amd.parallel.dist import gather_grid  # noqa: PLC0415
+
+        t_v = time.perf_counter()
+        g_snap = sim.generation
+        snap = gather_grid(sim)
+        rv = eng.run_until(g_snap + a.verify)
+        done = sim.generation - g_snap
+        final = gather_grid(sim)
+        ok_torch = ok_u8 = True
+        if rank == 0:
+            dev = "cuda" if on_gpu else "cpu"
+            want = life_step_torch(snap, done, device=dev)
+            ok_torch = bool(np.array_equal(final, want))
+            u8 = Simulation(LifeConfig(S, Hg, gen_limit=done, layout="u8", check_similarity=False),
+                            transport=native().self_transport(), backend=backend)
+            u8.load(snap)
+            u8.advance(done)
+            ok_u8 = bool(np.array_equal(u8.tile(), want))
+            del u8
+        verified = bool(ok_torch and ok_u8)
+        verify = {"generations": int(done), "from_generation": int(g_snap), "stop_reason": rv.stop_reason,
+                  "vs_torch_fp32_conv2d": ok_torch, "vs_u8_layout": ok_u8,
+                  "seconds": round(time.perf_counter() - t_v, 2)}
+        if dist is not None:
+            dist.barrier()
+
     desc = sim.describe()
     if rank == 0:
         rec = {
@@ -171,6 +308,7 @@ def main() -> int:
             "ms_per_step": dt * 1e3 / max(1, a.steps),
             "higher_is_better": True,
             "scaling": "strong",
+            "verified": verified,
             "vs_baseline": value / BASELINE_VALUE,
             "dtype": "u1 bit-packed cells (exact boolean B3/S23; reference stores u8 chars)"
                      if a.layout == "bits" else "u8 byte-per-cell (exact)",
@@ -179,8 +317,7 @@ def main() -> int:
                 "model": f"Game of Life B3/S23 torus {S}x{Hg}",
                 "global_batch": 1,
                 "seq_len": S * Hg,
-                "parallelism": f"{desc['decomp']} row/col tiles, "
-                               f"{'rccl' if world > 1 else 'rccl-self (rehearsal)' if a.rehearse_rccl else 'single'} halos",
+                "parallelism": f"{desc['decomp']} row/col tiles, {desc['transport'] if world > 1 else 'rccl-self (rehearsal)' if a.rehearse_rccl else 'single'} halos",
                 "grid": f"{S}x{Hg}",
                 "layout": a.layout,
                 "engine": backend.name(),
@@ -198,7 +335,13 @@ def main() -> int:
                 "kernel_launches_per_step": rs[-1].kernel_launches if rs else 0,
                 "halo_bytes_per_step": rs[-1].halo_bytes if rs else 0,
                 "overlapped_halo_exchange": bool(rs and rs[-1].overlapped),
+                "overlap_mode": desc["overlap_mode"],
+                "overlap_trial_ms_per_epoch": {"plain": desc["overlap_trial_ms_plain"],
+                                               "early_boundary": desc["overlap_trial_ms_early"]},
                 "graph_epochs": sum(r.graph_launches for r in rs),
+                "phase_ms_one_step": phases,
+                "verify": verify,
+                "shared_gpus": shared,
                 "baseline": "8.9e8 cell-updates/s (best reference run in BASELINE.md: MPI, 4 ranks, 2048^2, CPU)",
             },
         }
@@ -206,7 +349,7 @@ def main() -> int:
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return 1 if verified is False else 0
 
 
 if __name__ == "__main__":

@@ -75,6 +75,22 @@ class Backend {
   virtual void* stream_mark(void* /*from*/) { return nullptr; }
   virtual void stream_wait(void* /*on*/, void* /*mark*/) {}
 
+  // Phase timing: timing_mark() records a timestamp on
+  // `stream` (nullptr = the compute stream); timing_ms(a, b) is the time
+  // between two marks of one stream (blocks until b has completed);
+  // timing_release() recycles a mark.  Device backends use timing events,
+  // synchronous backends the host clock (their operations complete in
+  // program order).
+  virtual void* timing_mark(void* stream) = 0;
+  virtual double timing_ms(void* a, void* b) = 0;
+  virtual void timing_release(void* mark) = 0;
+  // Makes this backend's device current for the calling thread (rank
+  // threads of single-process multi-GPU runs call it first).
+  virtual void bind_thread() {}
+  // Lets this backend's device read memory of `device` directly (peer
+  // access); throws if the hardware cannot.  No-op for host backends.
+  virtual void enable_peer(int /*device*/) {}
+
   // Kernels.  run_block returns the drift of the stored frame in cells
   // (BlockArgs::allow_drift): the output's column x holds the cell the input
   // frame had at x - drift.

@@ -47,7 +47,13 @@ struct EngineConfig {
   //      the flag all-reduce included, runs on the comm stream;
   //    2 edges: the edge strips are recomputed in scratch tiles while the
   //      interior runs (round 1; eight small launches per epoch);
-  //   -1 auto / 0 off: everything on the compute stream.
+  //    0 off: everything on the compute stream;
+  //   -1 auto: where the early-boundary schedule applies (row strips with
+  //      an interior), the first epochs alternate the plain and the
+  //      early-boundary schedule, every rank times them with events, the
+  //      per-epoch medians are MAX-reduced over ranks, and all ranks keep the
+  //      faster one (GOL_OVERLAP_AUTO=plain|early forces the outcome after
+  //      the trial, for tests); elsewhere as off.
   int overlap = -1;
   // Check each termination poll one poll window later, so the host never
   // drains the device queue (stops are absorbing, so running past is exact).
@@ -86,6 +92,13 @@ struct RunResult {
   bool overlapped = false;       // epochs ran with the overlapped halo exchange
   int64_t graph_launches = 0;    // epochs replayed from a captured HIP graph
   int64_t halo_bytes = 0;        // bytes this rank sent in halo exchanges
+  // Per-phase device time of this run (Engine::set_phase_timing; SURVEY
+  // 5.1/5.5): temporal-block kernels, halo exchanges (pack / send / recv /
+  // unpack), periodic halo fills, termination-flag reductions (all-reduce +
+  // copy to the host).  Phases on different streams may overlap, so the sum
+  // can exceed loop_ms; the rest of loop_ms is host gaps and idle device.
+  bool phase_timed = false;
+  double compute_ms = 0, halo_ms = 0, fill_ms = 0, allreduce_ms = 0;
 };
 
 // The reference's "Generations:" value of a run over (start_gen, limit] whose
@@ -111,6 +124,16 @@ class Engine {
   int epoch_depth() const { return D_; }
   int tmax() const { return tmax_; }
   bool overlap() const { return overlap_ || early_; }
+  // "off" | "on" | "edges" | "auto:trial" | "auto:plain" | "auto:early".
+  std::string overlap_mode() const;
+  // Median epoch time (ms, MAX over ranks) of the plain and the
+  // early-boundary schedule measured by the auto trial (-1: not measured).
+  double trial_ms_plain() const { return auto_ms_[0]; }
+  double trial_ms_early() const { return auto_ms_[1]; }
+  // Sample per-phase device times into RunResult (event pairs around every
+  // kernel, exchange, fill and reduction; adds a little launch overhead).
+  void set_phase_timing(bool on) { phase_timing_ = on; }
+  bool phase_timing() const { return phase_timing_; }
   bool graphs() const { return use_graphs_; }
   int64_t generation() const { return gen_; }
   void set_generation(int64_t g) { gen_ = g; }
@@ -177,6 +200,17 @@ class Engine {
   void epoch_overlapped(int64_t d);
   void run_epoch(int64_t d);
   void release_graphs();
+  // Overlap auto trial (EngineConfig::overlap == -1): picks the schedule of
+  // the next full epoch, records its start, and decides once enough epochs
+  // of both schedules have been timed (at the same epoch on every rank).
+  void auto_choose(bool full_epoch);
+  void auto_mark();
+  void auto_decide();
+  // Phase timing: a mark on `stream` (nullptr when off or capturing), and
+  // the span [a, now] of `phase` on that stream.
+  void* phase_begin(void* stream);
+  void phase_end(int phase, void* a, void* stream);
+  void collect_phases(RunResult& res);
 
   EngineConfig cfg_;
   Backend* be_;
@@ -218,6 +252,29 @@ class Engine {
   bool poll_side_ = false;   // termination polls reduce on the comm stream (Transport::side_reduce)
   int64_t drift_ = 0;
   int64_t graph_drift_[2] = {0, 0};
+  // Overlap auto trial.
+  bool auto_overlap_ = false;       // trial still running
+  bool auto_decided_ = false;
+  int auto_sched_ = 0;              // schedule of the current epoch: 0 plain, 1 early
+  int64_t auto_full_epochs_ = 0;    // full epochs seen so far
+  void* auto_open_ = nullptr;       // start mark of the current epoch
+  int auto_open_sched_ = -1;        // its schedule (-1: not a trial epoch)
+  struct AutoSpan {
+    int sched;
+    void* a;
+    void* b;
+  };
+  std::vector<AutoSpan> auto_spans_;
+  int auto_counts_[2] = {0, 0};
+  double auto_ms_[2] = {-1, -1};
+  // Phase timing.
+  bool phase_timing_ = false;
+  struct PhaseSpan {
+    int phase;
+    void* a;
+    void* b;
+  };
+  std::vector<PhaseSpan> phase_spans_;
 };
 
 }  // namespace gol

@@ -84,6 +84,7 @@ class ThreadHub {
   struct Msg {
     const void* buf;
     size_t bytes;
+    int device = -1;  // sender's device (-1: host memory)
     bool consumed = false;
   };
   std::mutex mu;
@@ -120,6 +121,7 @@ class ThreadTransport final : public Transport {
   int delay_us_ = 0;
   int64_t garble_at_ = 0, received_ = 0;
   uint64_t rng_ = 0;
+  std::vector<int> peers_enabled_;  // devices this rank's device may read directly
   void fault_delay();
 };
 

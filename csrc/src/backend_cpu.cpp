@@ -8,6 +8,7 @@
 // the kernels' v_bitop3 truth tables).  run_block sweeps per-thread row bands
 // with a 3-row window per level, like the GPU kernel's register schedule.
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -112,6 +113,16 @@ class CpuBackend final : public Backend {
   void* event_record() override { return nullptr; }
   void event_wait(void*) override {}
   void event_destroy(void*) override {}
+  // Every operation completes before it returns: a mark is the host clock.
+  void* timing_mark(void*) override {
+    return new std::chrono::steady_clock::time_point(std::chrono::steady_clock::now());
+  }
+  double timing_ms(void* a, void* b) override {
+    const auto* ta = static_cast<std::chrono::steady_clock::time_point*>(a);
+    const auto* tb = static_cast<std::chrono::steady_clock::time_point*>(b);
+    return std::chrono::duration<double, std::milli>(*tb - *ta).count();
+  }
+  void timing_release(void* m) override { delete static_cast<std::chrono::steady_clock::time_point*>(m); }
 
   int run_block(const BlockArgs& a) override;
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override;

@@ -20,15 +20,8 @@
 
 #include "../kernels/life_kernels.hpp"
 #include "gol/backend.hpp"
+#include "gol/hip_util.hpp"
 #include "gol/trace.hpp"
-
-#define HIP_CHECK(expr)                                                                     \
-  do {                                                                                      \
-    hipError_t e_ = (expr);                                                                 \
-    if (e_ != hipSuccess)                                                                   \
-      ::gol::fail(std::string("HIP error in ") + __FILE__ + ":" + std::to_string(__LINE__) + \
-                  " (" #expr "): " + hipGetErrorString(e_));                                \
-  } while (0)
 
 namespace gol {
 namespace {
@@ -44,6 +37,13 @@ int env_int(const char* name, int dflt) {
   return dflt;
 }
 
+// GOL_CHECK_DEVICE=1: every entry point asserts that its device is current,
+// and every buffer the backend allocates or a launch touches is checked to
+// live on that device (hipPointerGetAttributes).
+#define GOL_ON_DEVICE()              \
+  DeviceScope device_scope_(dev_);   \
+  if (check_dev_) assert_current(__func__)
+
 class HipBackend final : public Backend {
  public:
   explicit HipBackend(int device) : dev_(device) {
@@ -51,7 +51,8 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGetDeviceCount(&n));
     GOL_REQUIRE(n > 0, "no HIP device available");
     GOL_REQUIRE(device >= 0 && device < n, "HIP device index out of range");
-    HIP_CHECK(hipSetDevice(dev_));
+    check_dev_ = env_int("GOL_CHECK_DEVICE", 0) != 0;
+    GOL_ON_DEVICE();
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
@@ -81,12 +82,14 @@ class HipBackend final : public Backend {
       void*& buf = chain_[which & 1];
       size_t& cap = chain_bytes_[which & 1];
       if (n > cap) {
+        GOL_ON_DEVICE();
         HIP_CHECK(hipStreamSynchronize(stream_));  // earlier launches may still use it
         if (buf) HIP_CHECK(hipFree(buf));
         HIP_CHECK(hipMalloc(&buf, n));
         if (which == 0) HIP_CHECK(hipMemsetAsync(buf, 0, n, stream_));
         cap = n;
       }
+      if (check_dev_) check_ptr(buf, which == 0 ? "chain flags" : "chain slots");
       return static_cast<uint32_t*>(buf);
     };
     if (const char* t = std::getenv("GOL_WG_TRACE")) {
@@ -104,16 +107,18 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&tune_.err), err_host_, 0));
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
+        GOL_ON_DEVICE();
         HIP_CHECK(hipStreamSynchronize(stream_));  // earlier kernels may still use it
         if (scratch_) HIP_CHECK(hipFree(scratch_));
         HIP_CHECK(hipMalloc(&scratch_, n));
         scratch_bytes_ = n;
       }
+      if (check_dev_) check_ptr(scratch_, "scratch");
       return scratch_;
     };
   }
   ~HipBackend() override {
-    hipSetDevice(dev_);
+    DeviceScope device_scope(dev_);
     if (stream_) hipStreamSynchronize(stream_);
     if (comm_) hipStreamSynchronize(comm_);
     if (stage_) hipFree(stage_);
@@ -125,6 +130,7 @@ class HipBackend final : public Backend {
       hipEventDestroy(p.e1);
     }
     for (hipEvent_t e : free_events_) hipEventDestroy(e);
+    for (hipEvent_t e : timing_pool_) hipEventDestroy(e);
     if (err_host_) hipHostFree(err_host_);
     for (auto& e : marks_)
       if (e) hipEventDestroy(e);
@@ -144,79 +150,139 @@ class HipBackend final : public Backend {
   void* stream() const override { return stream_; }
 
   void* alloc(size_t bytes) override {
-    HIP_CHECK(hipSetDevice(dev_));
+    GOL_ON_DEVICE();
     void* p = nullptr;
     HIP_CHECK(hipMalloc(&p, bytes ? bytes : 1));
     HIP_CHECK(hipMemsetAsync(p, 0, bytes ? bytes : 1, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    if (check_dev_) check_ptr(p, "alloc");
     return p;
   }
   void release(void* p) override {
     if (!p) return;
-    hipSetDevice(dev_);
+    DeviceScope device_scope(dev_);
     hipStreamSynchronize(stream_);
     hipFree(p);
   }
   void* alloc_host(size_t bytes) override {
+    GOL_ON_DEVICE();
     void* p = nullptr;
     HIP_CHECK(hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault));
     return p;
   }
   void release_host(void* p) override {
+    DeviceScope device_scope(dev_);
     if (p) hipHostFree(p);
   }
   void memset_async(void* p, int v, size_t bytes) override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipMemsetAsync(p, v, bytes, stream_));
   }
   void copy_h2d(void* d, const void* s, size_t n) override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
   void copy_d2h(void* d, const void* s, size_t n) override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
   void copy_d2h_async(void* d, const void* s, size_t n) override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
   }
   void copy_d2h_async_on(void* d, const void* s, size_t n, void* stream) override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream ? static_cast<hipStream_t>(stream) : stream_));
   }
   void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
                      int64_t rows) override {
     if (rows <= 0 || width <= 0) return;
+    GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpy2DAsync(dst, size_t(dpitch), src, size_t(spitch), size_t(width), size_t(rows),
                                hipMemcpyDefault, stream_));
   }
-  void synchronize() override { HIP_CHECK(hipStreamSynchronize(stream_)); }
+  void synchronize() override {
+    GOL_ON_DEVICE();
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
   void synchronize_stream(void* s) override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipStreamSynchronize(s ? static_cast<hipStream_t>(s) : stream_));
   }
-  void* event_record() override {
-    hipEvent_t e;
-    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIP_CHECK(hipEventRecord(e, stream_));
-    return e;
-  }
+  void* event_record() override { return event_record_on(nullptr); }
   void* event_record_on(void* stream) override {
+    GOL_ON_DEVICE();
     hipEvent_t e;
     HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(e, stream ? static_cast<hipStream_t>(stream) : stream_));
     return e;
   }
-  void event_wait(void* ev) override { HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(ev))); }
-  void event_destroy(void* ev) override { hipEventDestroy(static_cast<hipEvent_t>(ev)); }
+  void event_wait(void* ev) override {
+    GOL_ON_DEVICE();
+    HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(ev)));
+  }
+  void event_destroy(void* ev) override {
+    DeviceScope device_scope(dev_);
+    hipEventDestroy(static_cast<hipEvent_t>(ev));
+  }
   bool event_query(void* ev) override {
+    GOL_ON_DEVICE();
     const hipError_t e = hipEventQuery(static_cast<hipEvent_t>(ev));
     if (e == hipErrorNotReady) return false;
     HIP_CHECK(e);
     return true;
   }
+  // Phase timing: timing-enabled events from a pool.
+  void* timing_mark(void* stream) override {
+    GOL_ON_DEVICE();
+    hipEvent_t e;
+    if (timing_pool_.empty()) {
+      HIP_CHECK(hipEventCreate(&e));
+    } else {
+      e = timing_pool_.back();
+      timing_pool_.pop_back();
+    }
+    HIP_CHECK(hipEventRecord(e, stream ? static_cast<hipStream_t>(stream) : stream_));
+    return e;
+  }
+  double timing_ms(void* a, void* b) override {
+    GOL_ON_DEVICE();
+    HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(b)));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, static_cast<hipEvent_t>(a), static_cast<hipEvent_t>(b)));
+    return double(ms);
+  }
+  void timing_release(void* m) override {
+    if (m) timing_pool_.push_back(static_cast<hipEvent_t>(m));
+  }
+  void bind_thread() override {
+    HIP_CHECK(hipSetDevice(dev_));
+    if (check_dev_) assert_current(__func__);
+  }
+  // Direct reads of another device's buffers (ThreadTransport across GPUs).
+  void enable_peer(int peer) override {
+    if (peer == dev_ || peer < 0) return;
+    GOL_ON_DEVICE();
+    int can = 0;
+    HIP_CHECK(hipDeviceCanAccessPeer(&can, dev_, peer));
+    GOL_REQUIRE(can, "device " + std::to_string(dev_) + " cannot access device " + std::to_string(peer) +
+                         " (no peer access): the thread transport cannot copy between them; use --comm rccl");
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) {
+      (void)hipGetLastError();
+      return;
+    }
+    HIP_CHECK(e);
+  }
   bool supports_graphs() const override { return tune_.split == 0; }  // split allocates scratch lazily
   void capture_begin() override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   }
   void* capture_end() override {
+    GOL_ON_DEVICE();
     hipGraph_t g = nullptr;
     HIP_CHECK(hipStreamEndCapture(stream_, &g));
     hipGraphExec_t exec = nullptr;
@@ -224,11 +290,16 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGraphDestroy(g));
     return exec;
   }
-  void graph_launch(void* g) override { HIP_CHECK(hipGraphLaunch(static_cast<hipGraphExec_t>(g), stream_)); }
+  void graph_launch(void* g) override {
+    GOL_ON_DEVICE();
+    HIP_CHECK(hipGraphLaunch(static_cast<hipGraphExec_t>(g), stream_));
+  }
   void graph_destroy(void* g) override {
+    DeviceScope device_scope(dev_);
     if (g) hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
   }
   void i64_async(int64_t* dev, int64_t v, bool add) override {
+    GOL_ON_DEVICE();
     hipk::launch_i64(dev, v, add, stream_);
     HIP_CHECK(hipGetLastError());
   }
@@ -236,22 +307,37 @@ class HipBackend final : public Backend {
   // made every epoch ~0.9 ms slower in the one-GPU RCCL rehearsal
   // (profiles/r02/rehearsal_overlap.jsonl).
   void* comm_stream() override {
-    if (!comm_) HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+    if (!comm_) {
+      GOL_ON_DEVICE();
+      HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+      if (check_dev_) {
+        int d = -1;
+        HIP_CHECK(hipStreamGetDevice(comm_, &d));
+        GOL_REQUIRE(d == dev_, "GOL_CHECK_DEVICE: comm stream created on device " + std::to_string(d));
+      }
+    }
     return comm_;
   }
   // Marks come from a small ring of reusable timing-free events: a mark is
   // only waited on by the next few operations of an epoch.
   void* stream_mark(void* from) override {
+    GOL_ON_DEVICE();
     hipEvent_t& e = marks_[mark_next_++ % marks_.size()];
     if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(e, from ? static_cast<hipStream_t>(from) : stream_));
     return e;
   }
   void stream_wait(void* on, void* mark) override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipStreamWaitEvent(on ? static_cast<hipStream_t>(on) : stream_, static_cast<hipEvent_t>(mark), 0));
   }
 
   int run_block(const BlockArgs& a) override {
+    GOL_ON_DEVICE();
+    if (check_dev_) {
+      check_ptr(a.in, "run_block input");
+      check_ptr(a.out, "run_block output");
+    }
     if (chain_mode_) {  // chained groups: own stream only, never inside a graph capture
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       tune_.chain_ok = (!a.stream || a.stream == stream_) && hipStreamIsCapturing(stream_, &cs) == hipSuccess &&
@@ -391,6 +477,7 @@ class HipBackend final : public Backend {
   }
   bool wraps_columns(Layout l) const override { return tune_.wrap && !(l == Layout::U8 && tune_.u8_lds); }
   void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override {
+    GOL_ON_DEVICE();
     hipk::launch_rotate_cols(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), g, shift, stream_);
     HIP_CHECK(hipGetLastError());
   }
@@ -436,6 +523,7 @@ class HipBackend final : public Backend {
     }
   }
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override {
+    GOL_ON_DEVICE();
     auto* p = static_cast<uint8_t*>(buf);
     if (!(cols && rows && hipk::launch_fill_all(p, g, stream_))) {
       if (cols) hipk::launch_fill_cols(p, g, stream_);
@@ -444,15 +532,18 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGetLastError());
   }
   void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n, void* stream) override {
+    GOL_ON_DEVICE();
     hipk::launch_fill_cols_rows(static_cast<uint8_t*>(buf), g, r0, n, stream ? static_cast<hipStream_t>(stream) : stream_);
     HIP_CHECK(hipGetLastError());
   }
   void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {
+    GOL_ON_DEVICE();
     HIP_CHECK(hipMemsetAsync(flag, 0, 4, stream_));
     hipk::launch_alive(static_cast<const uint8_t*>(buf), g, flag, nullptr, stream_);
     HIP_CHECK(hipGetLastError());
   }
   int64_t alive_count(const void* buf, const TileGeom& g) override {
+    GOL_ON_DEVICE();
     unsigned long long* d = nullptr;
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d), 8, stream_));
     HIP_CHECK(hipMemsetAsync(d, 0, 8, stream_));
@@ -468,6 +559,7 @@ class HipBackend final : public Backend {
   // Host <-> tile transfers go through a bounded device staging buffer so a
   // 32768^2 (1 GiB) or larger grid never needs a second full-size copy.
   void load_owned(void* buf, const TileGeom& g, const uint8_t* cells, int64_t ld) override {
+    GOL_ON_DEVICE();
     const int64_t chunk = rows_per_chunk(g);
     uint8_t* stage = static_cast<uint8_t*>(stage_buf(chunk * g.W));
     for (int64_t r = 0; r < g.H; r += chunk) {
@@ -480,6 +572,7 @@ class HipBackend final : public Backend {
     }
   }
   void store_owned(const void* buf, const TileGeom& g, uint8_t* cells, int64_t ld, bool ascii) override {
+    GOL_ON_DEVICE();
     const int64_t chunk = rows_per_chunk(g);
     uint8_t* stage = static_cast<uint8_t*>(stage_buf(chunk * g.W));
     for (int64_t r = 0; r < g.H; r += chunk) {
@@ -493,6 +586,7 @@ class HipBackend final : public Backend {
   }
   void init_random(void* buf, const TileGeom& g, uint64_t seed, double density, int64_t grow0,
                    int64_t gcol0) override {
+    GOL_ON_DEVICE();
     hipk::launch_init_random(static_cast<uint8_t*>(buf), g, seed, density_thresh(density), grow0, gcol0,
                              stream_);
     HIP_CHECK(hipGetLastError());
@@ -512,10 +606,26 @@ class HipBackend final : public Backend {
       HIP_CHECK(hipMalloc(&stage_, size_t(bytes)));
       stage_bytes_ = bytes;
     }
+    if (check_dev_) check_ptr(stage_, "staging buffer");
     return stage_;
+  }
+  void assert_current(const char* where) const {
+    int d = -1;
+    HIP_CHECK(hipGetDevice(&d));
+    GOL_REQUIRE(d == dev_, std::string("GOL_CHECK_DEVICE: ") + where + " runs on device " + std::to_string(d) +
+                               ", backend owns device " + std::to_string(dev_));
+  }
+  void check_ptr(const void* p, const char* what) const {
+    if (!p) return;
+    hipPointerAttribute_t at{};
+    HIP_CHECK(hipPointerGetAttributes(&at, p));
+    GOL_REQUIRE(at.device == dev_, std::string("GOL_CHECK_DEVICE: ") + what + " lives on device " +
+                                       std::to_string(at.device) + ", backend owns device " + std::to_string(dev_));
   }
 
   int dev_;
+  bool check_dev_ = false;  // GOL_CHECK_DEVICE
+  std::vector<hipEvent_t> timing_pool_;  // timing_mark() events
   hipStream_t stream_ = nullptr;
   std::string arch_;
   int cus_ = 256;

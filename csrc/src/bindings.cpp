@@ -125,7 +125,8 @@ PYBIND11_MODULE(_gol, m) {
       .def("is_device", &Backend::is_device)
       .def("device", &Backend::device)
       .def("stream", [](const Backend& b) { return reinterpret_cast<std::uintptr_t>(b.stream()); })
-      .def("synchronize", &Backend::synchronize, py::call_guard<py::gil_scoped_release>());
+      .def("synchronize", &Backend::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("bind_thread", &Backend::bind_thread);
   m.def("cpu_backend",
         [](int threads, int drift) { return std::shared_ptr<Backend>(make_cpu_backend(threads, drift)); },
         py::arg("threads") = 0, py::arg("drift") = -1);
@@ -215,6 +216,11 @@ PYBIND11_MODULE(_gol, m) {
       .def_readonly("overlapped", &RunResult::overlapped)
       .def_readonly("graph_launches", &RunResult::graph_launches)
       .def_readonly("halo_bytes", &RunResult::halo_bytes)
+      .def_readonly("phase_timed", &RunResult::phase_timed)
+      .def_readonly("compute_ms", &RunResult::compute_ms)
+      .def_readonly("halo_ms", &RunResult::halo_ms)
+      .def_readonly("fill_ms", &RunResult::fill_ms)
+      .def_readonly("allreduce_ms", &RunResult::allreduce_ms)
       .def("as_dict", [](const RunResult& r) {
         py::dict d;
         d["generations"] = r.generations;
@@ -229,6 +235,11 @@ PYBIND11_MODULE(_gol, m) {
         d["overlapped"] = r.overlapped;
         d["graph_launches"] = r.graph_launches;
         d["halo_bytes"] = r.halo_bytes;
+        d["phase_timed"] = r.phase_timed;
+        d["compute_ms"] = r.compute_ms;
+        d["halo_ms"] = r.halo_ms;
+        d["fill_ms"] = r.fill_ms;
+        d["allreduce_ms"] = r.allreduce_ms;
         return d;
       });
 
@@ -245,6 +256,10 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("epoch_depth", &Engine::epoch_depth)
       .def_property_readonly("tmax", &Engine::tmax)
       .def("overlap", &Engine::overlap)
+      .def("overlap_mode", &Engine::overlap_mode)
+      .def_property_readonly("trial_ms_plain", &Engine::trial_ms_plain)
+      .def_property_readonly("trial_ms_early", &Engine::trial_ms_early)
+      .def_property("phase_timing", &Engine::phase_timing, &Engine::set_phase_timing)
       .def("graphs", &Engine::graphs)
       .def_property("generation", &Engine::generation, &Engine::set_generation)
       .def_property_readonly("drift", &Engine::drift)

@@ -1,6 +1,8 @@
 #include "gol/checkpoint.hpp"
 
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <cerrno>
 #include <cstdio>
@@ -58,20 +60,50 @@ int64_t need_int(const std::string& js, const std::string& key, const std::strin
 
 }  // namespace
 
-std::string checkpoint_grid_path(const std::string& dir) { return dir + "/grid.txt"; }
+std::string checkpoint_grid_path(const std::string& dir) { return dir + "/" + checkpoint_load(dir).grid; }
 
-void checkpoint_begin(const std::string& dir, int64_t W, int64_t H) {
-  mkdirs(dir);
-  create_text_file(checkpoint_grid_path(dir), W, H);
+namespace {
+
+bool file_exists(const std::string& path) {
+  struct stat st;
+  return ::stat(path.c_str(), &st) == 0;
 }
 
-void checkpoint_commit(const std::string& dir, const CheckpointMeta& m) {
+void fsync_path(const std::string& path, bool directory) {
+  const int fd = ::open(path.c_str(), directory ? (O_RDONLY | O_DIRECTORY) : O_RDONLY);
+  if (fd < 0) fail("checkpoint: cannot open '" + path + "' to sync it: " + std::strerror(errno));
+  const int rc = ::fsync(fd);
+  const int err = errno;
+  ::close(fd);
+  if (rc != 0 && !(directory && (err == EINVAL || err == EROFS)))
+    fail("checkpoint: fsync of '" + path + "' failed: " + std::strerror(err));
+}
+
+}  // namespace
+
+std::string checkpoint_begin(const std::string& dir, int64_t W, int64_t H, int64_t generation) {
+  mkdirs(dir);
+  std::string committed;
+  if (file_exists(dir + "/meta.json")) committed = checkpoint_load(dir).grid;
+  std::string name = "grid-" + std::to_string(generation) + ".txt";
+  if (name == committed) name = "grid-" + std::to_string(generation) + "b.txt";
+  const std::string path = dir + "/" + name;
+  create_text_file(path, W, H);
+  return path;
+}
+
+void checkpoint_commit(const std::string& dir, const std::string& grid_path, CheckpointMeta m) {
+  const size_t slash = grid_path.find_last_of('/');
+  m.grid = slash == std::string::npos ? grid_path : grid_path.substr(slash + 1);
+  std::string previous;
+  if (file_exists(dir + "/meta.json")) previous = checkpoint_load(dir).grid;
+  fsync_path(grid_path, false);  // the tiles are on disk before meta.json names them
   std::ostringstream o;
   o << "{\n \"format\": \"" << kCheckpointFormat << "\",\n \"width\": " << m.W << ",\n \"height\": " << m.H
     << ",\n \"generation\": " << m.generation << ",\n \"sim_phase\": " << m.sim_phase
     << ",\n \"gen_limit\": " << m.gen_limit << ",\n \"check_similarity\": "
     << (m.check_similarity ? "true" : "false") << ",\n \"sim_freq\": " << m.sim_freq << ",\n \"layout\": \""
-    << m.layout << "\"\n}";
+    << m.layout << "\",\n \"grid\": \"" << m.grid << "\"\n}";
   const std::string tmp = dir + "/meta.json.tmp", fin = dir + "/meta.json";
   {
     std::ofstream f(tmp, std::ios::trunc);
@@ -79,8 +111,12 @@ void checkpoint_commit(const std::string& dir, const CheckpointMeta& m) {
     f << o.str();
     if (!f.flush()) fail("cannot write checkpoint metadata '" + tmp + "'");
   }
+  fsync_path(tmp, false);
   if (std::rename(tmp.c_str(), fin.c_str()) != 0)
     fail("cannot publish checkpoint metadata '" + fin + "': " + std::strerror(errno));
+  fsync_path(dir, true);
+  // The committed checkpoint no longer needs the previous grid.
+  if (!previous.empty() && previous != m.grid) std::remove((dir + "/" + previous).c_str());
 }
 
 CheckpointMeta checkpoint_load(const std::string& dir) {
@@ -104,6 +140,12 @@ CheckpointMeta checkpoint_load(const std::string& dir) {
   m.check_similarity = cs == "true";
   const std::string lay = json_field(js, "layout");
   if (!lay.empty()) m.layout = lay;
+  const std::string grid = json_field(js, "grid");
+  if (!grid.empty()) {
+    GOL_REQUIRE(grid.find('/') == std::string::npos && grid != "." && grid != "..",
+                "checkpoint '" + dir + "': bad grid file name '" + grid + "'");
+    m.grid = grid;
+  }
   GOL_REQUIRE(m.W > 0 && m.H > 0 && m.sim_freq > 0 && m.generation >= 0,
               "checkpoint '" + dir + "': inconsistent metadata");
   return m;

@@ -15,6 +15,15 @@ namespace {
 // only (HBM-bound there: one grid read + write per pass, docs/PERFORMANCE.md).
 constexpr int kTSizes[] = {32, 24, 16, 12, 8, 4, 2, 1};
 
+// Phases of RunResult's device-time split.
+enum Phase { kCompute = 0, kHalo = 1, kFill = 2, kReduce = 3, kPhases = 4 };
+constexpr size_t kMaxPhaseSpans = size_t(1) << 16;  // per run; later spans go unmeasured
+
+// Overlap auto trial: warm-up epochs (first launches autotune the chained
+// groups), then kAutoTrials timed epochs of each schedule, alternating.
+constexpr int64_t kAutoWarm = 2;
+constexpr int kAutoTrials = 4;
+
 int64_t min_tile_rows(const Decomposition& d) { return d.H / d.Py; }
 int64_t min_tile_cols(const Decomposition& d) { return (d.W / d.col_unit / d.Px) * d.col_unit; }
 }  // namespace
@@ -84,7 +93,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
   const bool interior = min_tile_rows(dec_) >= 2 * int64_t(D_) + 1;  // on every rank
   overlap_ = row_exchange && cfg_.overlap == 2 && interior;
-  early_ = row_exchange && dec_.Px == 1 && cfg_.overlap == 1 && interior;
+  const bool early_ok = row_exchange && dec_.Px == 1 && interior;
+  early_ = early_ok && cfg_.overlap == 1;
   // With the early-boundary schedule every transport operation runs on the
   // comm stream (one stream per communicator, in issue order), so the flag
   // all-reduce of a poll runs beside the compute stream.  Not by default: in
@@ -105,6 +115,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
   if (use_graphs_) early_ = comm_route_ = false;  // captured epochs stay on one stream
+  // Overlap auto: measure both schedules on the real ranks (see auto_choose).
+  // The one-GPU RCCL rehearsal measured the early-boundary schedule slower
+  // (profiles/r02/rehearsal_overlap.jsonl), but it has no xGMI latency in it;
+  // on a multi-GPU node the decision is taken from the node itself.
+  auto_overlap_ = cfg_.overlap == -1 && early_ok && !use_graphs_;
   // Side polls: with a transport whose flag reduction has its own
   // communicator (RCCL), a poll's all-reduce and D2H copy run on the comm
   // stream after a mark on the compute stream, which never waits for them:
@@ -114,8 +129,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // hop cost ~10 us per poll, more than the 1-rank reduction it hides
   // (profiles/r02/side_poll_ab.jsonl); with 8 ranks the reduction is longer.
   const char* side = std::getenv("GOL_SIDE_POLL");
-  poll_side_ = tr_->side_reduce() && be_->is_device() && !early_ && !comm_route_ && !use_graphs_ && side &&
-               std::atoi(side) != 0;
+  poll_side_ = tr_->side_reduce() && be_->is_device() && !early_ && !comm_route_ && !use_graphs_ &&
+               !auto_overlap_ && side && std::atoi(side) != 0;
   gen_ = cfg_.start_gen;
 }
 
@@ -128,6 +143,15 @@ void Engine::release_graphs() {
 
 Engine::~Engine() {
   release_graphs();
+  for (auto& sp : auto_spans_) {
+    be_->timing_release(sp.a);
+    be_->timing_release(sp.b);
+  }
+  if (auto_open_) be_->timing_release(auto_open_);
+  for (auto& sp : phase_spans_) {
+    be_->timing_release(sp.a);
+    be_->timing_release(sp.b);
+  }
   if (gen_dev_) be_->release(gen_dev_);
   for (auto& b : buf_)
     if (b) be_->release(b);
@@ -197,9 +221,14 @@ void Engine::exchange_columns(void* buf) {
   auto nb = dec_.neighbors(rank_);
   const int64_t H = g_.H, pitch = g_.pitch;
   if (dec_.Px == 1) {
-    if (cols_filled_) be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/false);
+    if (cols_filled_) {
+      void* t = phase_begin(nullptr);
+      be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/false);
+      phase_end(kFill, t, nullptr);
+    }
     return;
   }
+  void* t = phase_begin(nullptr);
   const int64_t halo = 32 * int64_t(g_.hw);
   const int64_t span = g_.span_bytes(halo);
   const int64_t r0 = g_.row0();
@@ -215,6 +244,7 @@ void Engine::exchange_columns(void* buf) {
   halo_bytes_ += 2 * span * H;
   be_->copy_2d_async(base + g_.offset(r0, 0), pitch, colbuf_[2], span, span, H);
   be_->copy_2d_async(base + g_.offset(r0, g_.cell0() + g_.W), pitch, colbuf_[3], span, span, H);
+  phase_end(kHalo, t, nullptr);
 }
 
 // Two-phase halo exchange (columns, then full-width rows so the corner
@@ -228,7 +258,9 @@ void Engine::halo_exchange() {
   auto nb = dec_.neighbors(rank_);
   const int64_t H = g_.H, pitch = g_.pitch;
   if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange) {  // one rank: both periodic fills, one launch
+    void* t = phase_begin(nullptr);
     be_->fill_periodic(buf, g_, /*cols=*/cols_filled_, /*rows=*/true);
+    phase_end(kFill, t, nullptr);
     ++exchanges_;
     return;
   }
@@ -236,7 +268,9 @@ void Engine::halo_exchange() {
   exchange_columns(buf);
   // Phase B: north/south halo rows over the full padded width.
   if (dec_.Py == 1 && !cfg_.self_exchange) {
+    void* t = phase_begin(nullptr);
     be_->fill_periodic(buf, g_, /*cols=*/false, /*rows=*/true);
+    phase_end(kFill, t, nullptr);
   } else {
     const int64_t Dv = g_.Dv;
     const size_t bytes = size_t(Dv * pitch);
@@ -247,7 +281,9 @@ void Engine::halo_exchange() {
         {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
     };
     comm_after_compute();
+    void* t = phase_begin(rccl_stream());
     tr_->exchange(ops, rccl_stream());
+    phase_end(kHalo, t, rccl_stream());
     compute_after_comm();
     halo_bytes_ += 2 * int64_t(bytes);
   }
@@ -288,7 +324,9 @@ void Engine::epoch_overlapped(int64_t d) {
       {true, nb[kSouth], bot + D * pitch, bytes},       // my bottom rows -> south's top-edge halo
       {false, nb[kNorth], top, bytes},                  // north's bottom rows -> my top-edge halo
   };
+  void* t = phase_begin(comm);
   tr_->exchange(ops, comm ? comm : be_->stream());
+  phase_end(kHalo, t, comm);
   halo_bytes_ += 2 * int64_t(bytes);
   void* rows_done = be_->stream_mark(comm);
   ++exchanges_;
@@ -330,14 +368,16 @@ void Engine::run_epoch(int64_t d) {
     epoch_overlapped(d);
     return;
   }
+  const bool sent_early = rows_pending_;
   if (rows_pending_) {
     // The previous epoch sent this buffer's boundary rows early.
     if (rows_arrived_) be_->stream_wait(nullptr, rows_arrived_);
     rows_pending_ = false;
     rows_arrived_ = nullptr;
-  } else {
-    halo_exchange();
   }
+  // The previous epoch ends here (its early rows have arrived).
+  if (auto_overlap_) auto_mark();
+  if (!sent_early) halo_exchange();
   int64_t a = 0;
   while (d > 0) {
     const int T = pick_T(d);
@@ -395,8 +435,10 @@ void Engine::last_block_early(int T) {
   // Boundary strips [Dv, Dv + D) and [Dv + H - D, Dv + H), one launch.
   const int drift = launch(in, out, g_, T, Dv, Dv + D, gen_, comm, H - D, /*prio_boost=*/true);
   if (cols_filled_) {
+    void* t = phase_begin(comm);
     be_->fill_cols_rows(out, g_, Dv, D, comm);
     be_->fill_cols_rows(out, g_, Dv + H - D, D, comm);
+    phase_end(kFill, t, comm);
   }
   auto nb = dec_.neighbors(rank_);
   const size_t bytes = size_t(Dv * pitch);
@@ -406,14 +448,20 @@ void Engine::last_block_early(int T) {
       {true, nb[kSouth], base + H * pitch, bytes},
       {false, nb[kNorth], base, bytes},
   };
+  void* tx = phase_begin(comm);
   tr_->exchange(ops, comm ? comm : be_->stream());
+  phase_end(kHalo, tx, comm);
   rows_arrived_ = comm ? be_->stream_mark(comm) : nullptr;
   rows_pending_ = true;
   halo_bytes_ += 2 * int64_t(bytes);
   ++exchanges_;
   ++early_sends_;
   launch(in, out, g_, T, Dv + D, Dv + H - D, gen_);  // interior, concurrent with the above
-  if (cols_filled_) be_->fill_cols_rows(out, g_, Dv + D, H - 2 * D);
+  if (cols_filled_) {
+    void* t = phase_begin(nullptr);
+    be_->fill_cols_rows(out, g_, Dv + D, H - 2 * D);
+    phase_end(kFill, t, nullptr);
+  }
   add_drift(drift);
   cur_ ^= 1;
   gen_ += T;
@@ -444,7 +492,9 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   a.stream = stream;
   a.dual_offset = dual_offset;
   a.prio_boost = prio_boost;
+  void* t = phase_begin(stream);
   const int drift = be_->run_block(a);
+  phase_end(kCompute, t, stream);
   ++launches_;
   return drift;
 }
@@ -473,9 +523,11 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
     // Flags of (from, to] are complete at the compute stream's current mark.
     void* side = be_->comm_stream();
     be_->stream_wait(side, be_->stream_mark(nullptr));
+    void* t = phase_begin(side);
     // The one-rank RCCL rehearsal reduces too, through its 1-rank communicator.
     if (tr_->size() > 1 || cfg_.self_exchange) tr_->allreduce_max_u32(dev, size_t(n), side);
     be_->copy_d2h_async_on(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t), side);
+    phase_end(kReduce, t, side);
     p.ev = be_->event_record_on(side);
     ++polls_;
     return p;
@@ -484,8 +536,10 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   // compute stream's critical path, in issue order with the halo exchanges.
   void* comm = (comm_route_ || early_) ? be_->comm_stream() : nullptr;
   comm_after_compute();
+  void* t = phase_begin(comm);
   if (tr_->size() > 1) tr_->allreduce_max_u32(dev, size_t(n), rccl_stream());
   be_->copy_d2h_async_on(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t), comm);
+  phase_end(kReduce, t, comm);
   p.ev = be_->event_record_on(comm);
   ++polls_;
   return p;
@@ -626,6 +680,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
       ++graph_runs_;
     } else {
       if (use_graphs_) be_->i64_async(gen_dev_, d, /*add=*/true);  // keep the offset in step
+      if (auto_overlap_) auto_choose(d == D_ && send_next_);
       run_epoch(d);
     }
     ++epoch;
@@ -651,6 +706,10 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   if (poll_side_) be_->synchronize_stream(be_->comm_stream());
   be_->synchronize();
   be_->check_device_errors();
+  if (auto_open_) {  // an auto-trial epoch span does not continue into the next run
+    be_->timing_release(auto_open_);
+    auto_open_ = nullptr;
+  }
   if (cfg_.timing_barriers) {
     settle_pending(false);
     tr_->barrier();
@@ -665,6 +724,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.graph_launches = graph_runs_ - g0;
   res.halo_bytes = halo_bytes_ - hb0;
   res.generations = limit;
+  collect_phases(res);
   if (found >= 0) {
     res.first_unchanged = found;
     be_->alive_any(buf_[cur_], g_, alive_dev_);
@@ -678,6 +738,113 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
                                            cfg_.sim_freq, cfg_.sim_phase, &res.stop_reason);
   }
   return res;
+}
+
+// ---- overlap auto trial ---------------------------------------------------
+// The schedule of each full epoch is a function of the epoch count only, so
+// every rank runs the same sequence, reaches the decision at the same epoch
+// and issues the decision's all-reduce at the same point of its operation
+// stream (RCCL matches operations by issue order).
+void Engine::auto_choose(bool full_epoch) {
+  int sched = 0;
+  int trial = -1;
+  if (full_epoch) {
+    const int64_t i = auto_full_epochs_++;
+    if (i >= kAutoWarm) {
+      sched = ((i - kAutoWarm) % 2 == 0) ? 1 : 0;
+      trial = sched;
+    }
+  }
+  early_ = comm_route_ = sched == 1;
+  auto_sched_ = trial;
+}
+
+void Engine::auto_mark() {
+  if (auto_open_) {
+    void* end = be_->timing_mark(nullptr);
+    if (auto_open_sched_ >= 0) {
+      auto_spans_.push_back({auto_open_sched_, auto_open_, end});
+      ++auto_counts_[auto_open_sched_];
+    } else {
+      be_->timing_release(auto_open_);
+      be_->timing_release(end);
+    }
+    auto_open_ = nullptr;
+  }
+  if (auto_counts_[0] >= kAutoTrials && auto_counts_[1] >= kAutoTrials) {
+    auto_decide();
+    return;
+  }
+  auto_open_ = be_->timing_mark(nullptr);
+  auto_open_sched_ = auto_sched_;
+}
+
+void Engine::auto_decide() {
+  std::vector<double> ms[2];
+  for (auto& sp : auto_spans_) {
+    ms[sp.sched].push_back(be_->timing_ms(sp.a, sp.b));
+    be_->timing_release(sp.a);
+    be_->timing_release(sp.b);
+  }
+  auto_spans_.clear();
+  uint32_t v[2];
+  for (int k = 0; k < 2; ++k) {
+    std::sort(ms[k].begin(), ms[k].end());
+    const double med = ms[k][ms[k].size() / 2];
+    v[k] = uint32_t(std::min(4.0e9, std::max(0.0, med * 1e4)));  // 0.1 us units
+  }
+  // Slowest rank decides: every rank ends up with the same MAX values.
+  uint32_t* dev = alive_dev_ + 4;
+  be_->copy_h2d(dev, v, sizeof(v));
+  if (tr_->size() > 1) tr_->allreduce_max_u32(dev, 2, be_->stream());
+  be_->copy_d2h(v, dev, sizeof(v));
+  auto_ms_[0] = v[0] * 1e-4;
+  auto_ms_[1] = v[1] * 1e-4;
+  bool early = double(v[1]) < 0.98 * double(v[0]);
+  if (const char* f = std::getenv("GOL_OVERLAP_AUTO")) {
+    if (std::strcmp(f, "early") == 0) early = true;
+    if (std::strcmp(f, "plain") == 0) early = false;
+  }
+  early_ = comm_route_ = early;
+  auto_overlap_ = false;
+  auto_decided_ = true;
+}
+
+std::string Engine::overlap_mode() const {
+  if (overlap_) return "edges";
+  if (cfg_.overlap == 1) return early_ ? "on" : "off";
+  if (cfg_.overlap == -1) {
+    if (auto_overlap_) return "auto:trial";
+    if (auto_decided_) return early_ ? "auto:early" : "auto:plain";
+  }
+  return "off";
+}
+
+// ---- phase timing -----------------------------------------------------------
+void* Engine::phase_begin(void* stream) {
+  if (!phase_timing_ || capturing_ || phase_spans_.size() >= kMaxPhaseSpans) return nullptr;
+  return be_->timing_mark(stream);
+}
+
+void Engine::phase_end(int phase, void* a, void* stream) {
+  if (!a) return;
+  phase_spans_.push_back({phase, a, be_->timing_mark(stream)});
+}
+
+void Engine::collect_phases(RunResult& res) {
+  if (!phase_timing_) return;
+  double ms[kPhases] = {0, 0, 0, 0};
+  for (auto& sp : phase_spans_) {
+    ms[sp.phase] += be_->timing_ms(sp.a, sp.b);
+    be_->timing_release(sp.a);
+    be_->timing_release(sp.b);
+  }
+  phase_spans_.clear();
+  res.phase_timed = true;
+  res.compute_ms = ms[kCompute];
+  res.halo_ms = ms[kHalo];
+  res.fill_ms = ms[kFill];
+  res.allreduce_ms = ms[kReduce];
 }
 
 }  // namespace gol

@@ -49,6 +49,7 @@ void ThreadTransport::exchange(const std::vector<P2POp>& ops, void* stream) {
       auto m = std::make_shared<ThreadHub::Msg>();
       m->buf = op.buf;
       m->bytes = op.bytes;
+      m->device = backend_->is_device() ? backend_->device() : -1;
       hub_->queues[{rank_, op.peer}].push_back(m);
       sent.push_back(m);
     }
@@ -68,6 +69,15 @@ void ThreadTransport::exchange(const std::vector<P2POp>& ops, void* stream) {
                                           std::to_string(m->bytes) + " vs " +
                                           std::to_string(op.bytes) + ")");
     fault_delay();
+    // Ranks on different GPUs of one process: the receiver's device copies
+    // straight out of the sender's buffer over xGMI, which needs peer access
+    // (enable_peer throws where the hardware has none).
+    const int mine = backend_->is_device() ? backend_->device() : -1;
+    if (m->device >= 0 && mine >= 0 && m->device != mine &&
+        std::find(peers_enabled_.begin(), peers_enabled_.end(), m->device) == peers_enabled_.end()) {
+      backend_->enable_peer(m->device);
+      peers_enabled_.push_back(m->device);
+    }
     backend_->copy_2d_async(op.buf, int64_t(op.bytes), m->buf, int64_t(op.bytes), int64_t(op.bytes), 1);
     backend_->synchronize();
     if (garble_at_ > 0 && ++received_ == garble_at_ && op.bytes > 0) {

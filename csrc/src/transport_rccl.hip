@@ -16,9 +16,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "gol/common.hpp"
+#include "gol/hip_util.hpp"
 #include "gol/transport.hpp"
 
 #define NCCL_CHECK(expr)                                                                      \
@@ -36,19 +38,46 @@ namespace {
 // hostname, library path) to stdout when the library initialises.  Stdout
 // belongs to the program: the reference's "Generations:" lines, bench.py's
 // one JSON line.  Library initialisation runs with fd 1 pointed at stderr.
-struct StdoutToStderr {
-  int saved = -1;
+// The P transports of an in-process run are built on P threads at once
+// (ncclCommInitRank blocks until every rank has joined), so the redirect is
+// process-wide and reference-counted: the first scope saves fd 1, the last
+// one restores it, whatever the order the threads leave in.
+class StdoutToStderr {
+ public:
   StdoutToStderr() {
-    std::fflush(stdout);
-    saved = dup(1);
-    if (saved >= 0) dup2(2, 1);
+    std::lock_guard<std::mutex> lk(mu());
+    if (depth()++ == 0) {
+      std::fflush(stdout);
+      saved() = dup(1);
+      if (saved() >= 0) dup2(2, 1);
+    }
   }
   ~StdoutToStderr() {
-    std::fflush(stdout);
-    if (saved >= 0) {
-      dup2(saved, 1);
-      close(saved);
+    std::lock_guard<std::mutex> lk(mu());
+    if (--depth() == 0) {
+      std::fflush(stdout);
+      if (saved() >= 0) {
+        dup2(saved(), 1);
+        close(saved());
+        saved() = -1;
+      }
     }
+  }
+  StdoutToStderr(const StdoutToStderr&) = delete;
+  StdoutToStderr& operator=(const StdoutToStderr&) = delete;
+
+ private:
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
+  }
+  static int& depth() {
+    static int d = 0;
+    return d;
+  }
+  static int& saved() {
+    static int fd = -1;
+    return fd;
   }
 };
 
@@ -59,7 +88,7 @@ class RcclTransport final : public Transport {
     GOL_REQUIRE(uid.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size");
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
-    if (hipSetDevice(dev_) != hipSuccess) fail("hipSetDevice failed for RCCL transport");
+    DeviceScope on(dev_);
     {
       StdoutToStderr quiet;
       NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
@@ -70,12 +99,12 @@ class RcclTransport final : public Transport {
       const char* side = std::getenv("GOL_SIDE_POLL");
       if (side && std::atoi(side) != 0) NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
     }
-    if (hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking) != hipSuccess)
-      fail("hipStreamCreate failed");
-    if (hipMalloc(&barrier_buf_, 64) != hipSuccess) fail("hipMalloc failed");
+    HIP_CHECK(hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking));
+    HIP_CHECK(hipMalloc(&barrier_buf_, 64));
+    HIP_CHECK(hipMemset(barrier_buf_, 0, 64));
   }
   ~RcclTransport() override {
-    hipSetDevice(dev_);
+    DeviceScope on(dev_);
     if (barrier_buf_) hipFree(barrier_buf_);
     if (barrier_stream_) hipStreamDestroy(barrier_stream_);
     if (flags_comm_) ncclCommDestroy(flags_comm_);
@@ -86,6 +115,7 @@ class RcclTransport final : public Transport {
   const char* name() const override { return "rccl"; }
 
   void exchange(const std::vector<P2POp>& ops, void* stream) override {
+    DeviceScope on(dev_);
     auto s = static_cast<hipStream_t>(stream);
     NCCL_CHECK(ncclGroupStart());
     for (const auto& op : ops) {
@@ -97,11 +127,13 @@ class RcclTransport final : public Transport {
     NCCL_CHECK(ncclGroupEnd());
   }
   void allreduce_max_u32(uint32_t* buf, size_t n, void* stream) override {
+    DeviceScope on(dev_);
     NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, flags_comm_ ? flags_comm_ : comm_,
                              static_cast<hipStream_t>(stream)));
   }
   bool side_reduce() const override { return flags_comm_ != nullptr; }
   void barrier() override {
+    DeviceScope on(dev_);
     NCCL_CHECK(ncclAllReduce(barrier_buf_, barrier_buf_, 1, ncclUint32, ncclMax, comm_, barrier_stream_));
     if (hipStreamSynchronize(barrier_stream_) != hipSuccess) fail("RCCL barrier failed");
   }

@@ -39,7 +39,7 @@ struct Options {
   std::string engine = "auto";  // auto | hip | cpu | ref
   std::string layout = "auto";  // auto | bits | u8
   std::string decomp = "auto";
-  std::string comm = "thread";  // thread | rccl (in-process ranks)
+  std::string comm = "auto";  // auto | thread | rccl (in-process ranks)
   std::string output;  // default: the matching reference build's file (see default_output)
   std::string style = "serial";  // serial | mpi | async | collective | openmp | cuda
   std::string metrics;
@@ -51,6 +51,7 @@ struct Options {
   double density = 0.5;
   int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0, overlap = -1, graphs = 0;
   bool show = false;
+  bool phase_timing = false;  // per-phase device times in --metrics-json
   int64_t checkpoint_every = 0;     // generations between checkpoints (0: none)
   int64_t start_gen = 0;            // resume: generation of the loaded grid
   int sim_phase = 0;                // resume: similarity counter at start_gen
@@ -72,18 +73,23 @@ struct Options {
                "                              --style: ./game_output.out, ./mpi_output.out, ...)\n"
                "  --gpus N                    run on N GPUs in this process (one rank each)\n"
                "  --ranks N                   in-process ranks (subdomains; share devices)\n"
-               "  --comm thread|rccl          in-process halo transport\n"
+               "  --comm auto|thread|rccl     in-process halo transport (auto: rccl when every rank\n"
+               "                              has a GPU of its own, else thread)\n"
                "  --decomp auto|PxQ           process grid (Px columns x Py rows)\n"
                "  --tmax T --epoch D --poll N temporal block, halo depth, poll interval\n"
-               "  --overlap auto|on|off|edges overlap the row halo exchange with compute (early\n"
-               "                              boundary rows; edges = recomputed edge strips)\n"
+               "  --overlap auto|on|off|edges on = early boundary rows sent while the interior\n"
+               "                              computes; edges = recomputed edge strips; off = no\n"
+               "                              overlap; auto = time plain and early epochs on the\n"
+               "                              ranks and keep the faster (row strips only)\n"
                "  --graphs auto|on|off        replay full epochs as captured HIP graphs\n"
                "  --threads N                 host threads for the cpu engine\n"
                "  --style serial|mpi|async|collective|openmp|cuda\n"
                "                              stdout format and output name of that reference build\n"
-               "  --metrics-json PATH         write run metrics as JSON\n"
+               "  --metrics-json PATH         write run metrics as JSON (with per-phase device times)\n"
+               "  --phase-timing              time kernels / halos / fills / reductions (implied\n"
+               "                              by --metrics-json)\n"
                "  --checkpoint-every K        write a checkpoint every K generations ...\n"
-               "  --checkpoint-dir DIR        ... into DIR (grid.txt + meta.json)\n"
+               "  --checkpoint-dir DIR        ... into DIR (grid-<gen>.txt + meta.json; crash-safe)\n"
                "  --resume DIR                continue from a checkpoint: same final grid and\n"
                "                              Generations line as the uninterrupted run\n"
                "  --show                      print the final grid with VT100 escapes\n");
@@ -127,6 +133,7 @@ Options parse(int argc, char** argv) {
       o.graphs = v == "on" ? 1 : v == "off" ? 0 : -1;
     }
     else if (a == "--show") o.show = true;
+    else if (a == "--phase-timing") o.phase_timing = true;
     else if (a == "--random") {
       std::string v = next();
       o.random = true;
@@ -152,10 +159,14 @@ Options parse(int argc, char** argv) {
     o.H = m.H;
     o.input = checkpoint_grid_path(o.resume);
     if (!o.gens_set) o.gens = m.gen_limit;
-    if (!o.sim_set) {
-      o.similarity = m.check_similarity;
-      o.sim_freq = m.sim_freq;
-    }
+    // The checkpoint's similarity phase counts modulo its own frequency; a
+    // different one would match neither the original run nor a fresh run
+    // at the new frequency.
+    if (o.sim_set && o.similarity && o.sim_freq != m.sim_freq)
+      throw Error("--resume: checkpoint was taken with --sim-freq " + std::to_string(m.sim_freq) +
+                  "; resuming with --sim-freq " + std::to_string(o.sim_freq) + " would shift the similarity checks");
+    if (!o.sim_set) o.similarity = m.check_similarity;
+    o.sim_freq = m.sim_freq;
     o.start_gen = m.generation;
     o.sim_phase = m.sim_phase;
     if (o.layout == "auto" && (m.layout == "bits" || m.layout == "u8")) o.layout = m.layout;
@@ -163,6 +174,7 @@ Options parse(int argc, char** argv) {
   if (o.W <= 0) o.W = 30;
   if (o.H <= 0) o.H = 30;
   if (o.gpus > 0) o.ranks = o.gpus;
+  if (!o.metrics.empty()) o.phase_timing = true;
   static const char* kStyles[] = {"serial", "mpi", "async", "collective", "openmp", "cuda"};
   if (std::find(std::begin(kStyles), std::end(kStyles), o.style) == std::end(kStyles)) usage(2);
   // Output file of the matching reference build: src/game.c:27,
@@ -254,21 +266,43 @@ int run(const Options& o) {
     std::vector<std::unique_ptr<Transport>> transports(P);
     std::vector<std::unique_ptr<Engine>> engines(P);
     auto hub = std::make_shared<ThreadHub>(P);
+    // One process, P rank threads.  RCCL needs every rank on a GPU of its
+    // own (it refuses duplicate devices in one communicator); ranks that
+    // share devices, and CPU ranks, use the thread transport.
+    std::string comm = o.comm;
+    if (comm == "auto") comm = (engine == "hip" && P > 1 && P <= ndev) ? "rccl" : "thread";
+    if (comm == "rccl" && P > 1) {
+      GOL_REQUIRE(engine == "hip", "--comm rccl needs --engine hip");
+      GOL_REQUIRE(P <= ndev, "--comm rccl needs one GPU per rank (--gpus N, not --ranks)");
+    }
     std::vector<uint8_t> uid;
-    if (o.comm == "rccl" && P > 1) uid = rccl_unique_id();
+    if (comm == "rccl" && P > 1) uid = rccl_unique_id();
     for (int r = 0; r < P; ++r)
       backends[r] = engine == "hip" ? make_hip_backend(r % ndev) : make_cpu_backend(o.threads > 0 ? o.threads : 0);
     if (P == 1) {
       transports[0] = std::make_unique<SelfTransport>();
-    } else if (o.comm == "rccl") {
+    } else if (comm == "rccl") {
       std::vector<std::thread> th;
+      std::vector<std::string> errs(P);
       for (int r = 0; r < P; ++r)
-        th.emplace_back([&, r] { transports[r] = make_rccl_transport(uid, r, P, r % ndev); });
+        th.emplace_back([&, r] {
+          try {
+            backends[r]->bind_thread();
+            transports[r] = make_rccl_transport(uid, r, P, r % ndev);
+          } catch (const std::exception& e) {
+            errs[r] = e.what();
+          }
+        });
       for (auto& t : th) t.join();
+      for (auto& e : errs)
+        if (!e.empty()) throw Error(e);
     } else {
       for (int r = 0; r < P; ++r) transports[r] = std::make_unique<ThreadTransport>(hub, r, backends[r].get());
     }
-    for (int r = 0; r < P; ++r) engines[r] = std::make_unique<Engine>(cfg, backends[r].get(), transports[r].get());
+    for (int r = 0; r < P; ++r) {
+      engines[r] = std::make_unique<Engine>(cfg, backends[r].get(), transports[r].get());
+      engines[r]->set_phase_timing(o.phase_timing);
+    }
 
     auto par = [&](const std::function<void(int)>& fn) {
       std::vector<std::thread> th;
@@ -276,6 +310,7 @@ int run(const Options& o) {
       for (int r = 0; r < P; ++r)
         th.emplace_back([&, r] {
           try {
+            backends[r]->bind_thread();  // a new thread starts on device 0
             fn(r);
           } catch (const std::exception& e) {
             errs[r] = e.what();
@@ -303,6 +338,7 @@ int run(const Options& o) {
     std::vector<RunResult> results(P);
     RunResult total;
     const int64_t limit = o.gens;
+    int64_t checkpoints_written = 0;
     for (;;) {
       const int64_t gen = engines[0]->generation();
       const int64_t target = o.checkpoint_every > 0 ? std::min(limit, gen + o.checkpoint_every) : limit;
@@ -314,6 +350,17 @@ int run(const Options& o) {
       total.exchanges += results[0].exchanges;
       total.polls += results[0].polls;
       total.kernel_launches += results[0].kernel_launches;
+      // Per-phase device times: the slowest rank's, like loop_ms.
+      for (auto& rr : results) {
+        total.phase_timed = total.phase_timed || rr.phase_timed;
+      }
+      const RunResult* slow = &results[0];
+      for (auto& rr : results)
+        if (rr.loop_ms > slow->loop_ms) slow = &rr;
+      total.compute_ms += slow->compute_ms;
+      total.halo_ms += slow->halo_ms;
+      total.fill_ms += slow->fill_ms;
+      total.allreduce_ms += slow->allreduce_ms;
       const RunResult& last = results[0];
       if (last.first_unchanged >= 0 || engines[0]->generation() >= limit) {
         total.first_unchanged = last.first_unchanged;
@@ -324,12 +371,12 @@ int run(const Options& o) {
       }
       if (!o.checkpoint_dir.empty()) {
         const int64_t g = engines[0]->generation();
-        checkpoint_begin(o.checkpoint_dir, o.W, o.H);
+        const std::string grid_path = checkpoint_begin(o.checkpoint_dir, o.W, o.H, g);
         par([&](int r) {
           Engine& e = *engines[r];
           std::vector<uint8_t> tile(size_t(e.rows().size() * e.cols().size()));
           e.store_cells(tile.data(), e.cols().size(), false);
-          write_text_tile(checkpoint_grid_path(o.checkpoint_dir), o.W, o.H, e.rows(), e.cols(), tile.data(),
+          write_text_tile(grid_path, o.W, o.H, e.rows(), e.cols(), tile.data(),
                           e.cols().size());
         });
         CheckpointMeta m;
@@ -341,7 +388,11 @@ int run(const Options& o) {
         m.check_similarity = o.similarity;
         m.sim_freq = o.sim_freq;
         m.layout = layout_name(layout);
-        checkpoint_commit(o.checkpoint_dir, m);
+        // Fault injection (tests): die after the N-th checkpoint's tiles are
+        // written, before it is committed.
+        if (const char* c = std::getenv("GOL_FAULT_CHECKPOINT_CRASH"))
+          if (++checkpoints_written == std::atoll(c)) std::_Exit(86);
+        checkpoint_commit(o.checkpoint_dir, grid_path, m);
       }
     }
     res = total;
@@ -375,7 +426,13 @@ int run(const Options& o) {
         << ", \"write_ms\": " << write_ms << ", \"cell_updates_per_s\": " << cups
         << ", \"epoch\": " << engines[0]->epoch_depth() << ", \"tmax\": " << engines[0]->tmax()
         << ", \"exchanges\": " << res.exchanges << ", \"polls\": " << res.polls
-        << ", \"kernel_launches\": " << res.kernel_launches << "}\n";
+        << ", \"kernel_launches\": " << res.kernel_launches << ", \"comm\": \"" << (P > 1 ? comm : "self")
+        << "\", \"overlap_mode\": \"" << engines[0]->overlap_mode()
+        << "\", \"overlap_trial_ms_plain\": " << engines[0]->trial_ms_plain()
+        << ", \"overlap_trial_ms_early\": " << engines[0]->trial_ms_early()
+        << ", \"phase_timed\": " << (res.phase_timed ? "true" : "false") << ", \"compute_ms\": " << res.compute_ms
+        << ", \"halo_ms\": " << res.halo_ms << ", \"fill_ms\": " << res.fill_ms
+        << ", \"allreduce_ms\": " << res.allreduce_ms << "}\n";
     }
   }
 

@@ -27,7 +27,7 @@ def parse_args(argv=None):
     p.add_argument("--engine", default="auto", choices=["auto", "hip", "cpu", "ref"])
     p.add_argument("--layout", default="auto", choices=["auto", "bits", "u8"])
     p.add_argument("--gens", type=int, default=1000, help="GEN_LIMIT")
-    p.add_argument("--sim-freq", type=int, default=3, help="SIMILARITY_FREQUENCY")
+    p.add_argument("--sim-freq", type=int, default=None, help="SIMILARITY_FREQUENCY (default 3)")
     p.add_argument("--no-similarity", action="store_true")
     p.add_argument("--random", default=None, help="SEED[:DENSITY] random init instead of a file")
     p.add_argument("--output", default=None,
@@ -40,17 +40,26 @@ def parse_args(argv=None):
     p.add_argument("--poll", "--poll-every", dest="poll", type=int, default=0,
                    help="generations between termination polls")
     p.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "edges"],
-                   help="overlap the row halo exchange with compute: early boundary rows (auto/on), "
-                        "recomputed edge strips (edges), or off")
+                   help="on = early boundary rows sent while the interior computes; edges = recomputed "
+                        "edge strips; off = no overlap; auto = time plain and early epochs on the ranks "
+                        "and keep the faster one (row strips only)")
     p.add_argument("--graphs", default="off", choices=["auto", "on", "off"],
                    help="replay full epochs as captured HIP graphs")
     p.add_argument("--threads", type=int, default=0)
     p.add_argument("--style", default="serial", choices=["serial", "mpi", "async", "collective", "openmp", "cuda"])
-    p.add_argument("--metrics-json", default=None)
+    p.add_argument("--metrics-json", default=None,
+                   help="write run metrics as JSON (with per-phase device times)")
+    p.add_argument("--phase-timing", action="store_true",
+                   help="time kernels / halos / fills / reductions (implied by --metrics-json)")
+    p.add_argument("--show", action="store_true",
+                   help="print the final grid with VT100 escapes (src/game.c:42-58)")
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--resume", default=None, help="checkpoint directory to resume from")
     a = p.parse_args(argv)
+    a.sim_freq_given = a.sim_freq is not None
+    if a.sim_freq is None:
+        a.sim_freq = 3
     if a.output is None:  # src/game.c:27, src/game_mpi.c:29, ... src/game_cuda.cu:37
         a.output = f"./{'game' if a.style == 'serial' else a.style}_output.out"
     if a.width <= 0:
@@ -84,6 +93,11 @@ def main(argv=None) -> int:
         if a.output != "none":
             write_grid(a.output, out)
         sys.stdout.write(stdout_lines(a.style, gens, ms, read_ms, (time.perf_counter() - t1) * 1e3))
+        if a.show:
+            from .utils.io import show_text  # noqa: PLC0415
+
+            sys.stdout.write(show_text(out))
+            sys.stdout.flush()
         return 0
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,8 +123,12 @@ def main(argv=None) -> int:
 
         cfg, grid_path = load_checkpoint(a.resume, layout=a.layout, decomp=a.decomp, tmax=a.tmax,
                                          epoch=a.epoch, poll_gens=a.poll, gen_limit=a.gens)
+        if a.sim_freq_given and not a.no_similarity and a.sim_freq != cfg.sim_freq:
+            raise SystemExit(f"--resume: checkpoint was taken with --sim-freq {cfg.sim_freq}; resuming with "
+                             f"--sim-freq {a.sim_freq} would shift the similarity checks")
         src = str(grid_path)
     sim = Simulation(cfg, transport=transport, backend=backend)
+    sim.phase_timing = bool(a.phase_timing or a.metrics_json)
     t0 = time.perf_counter()
     if a.random is not None and not a.resume:
         sim.init_random(seed, density)
@@ -127,6 +145,11 @@ def main(argv=None) -> int:
         rep = sim.run()
 
     write_ms = 0.0
+    tiles = None
+    if a.show:  # every rank's tile, gathered on rank 0 (the viewer prints the whole grid)
+        from .parallel.dist import gather_grid  # noqa: PLC0415
+
+        tiles = gather_grid(sim) if world > 1 else sim.tile()
     if a.output != "none":
         t1 = time.perf_counter()
         if rank == 0:
@@ -144,6 +167,11 @@ def main(argv=None) -> int:
         rec.update(sim.describe())
         rec.update({"read_ms": read_ms, "write_ms": write_ms, "width": a.width, "height": a.height})
         write_json(a.metrics_json, rec)
+        if tiles is not None:
+            from .utils.io import show_text  # noqa: PLC0415
+
+            sys.stdout.write(show_text(tiles))
+            sys.stdout.flush()
     return 0
 
 

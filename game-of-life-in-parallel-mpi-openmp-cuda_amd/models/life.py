@@ -109,6 +109,12 @@ class RunReport:
     overlapped: bool = False
     graph_launches: int = 0
     halo_bytes: int = 0
+    # Per-phase device time (Simulation.phase_timing).
+    phase_timed: bool = False
+    compute_ms: float = 0.0
+    halo_ms: float = 0.0
+    fill_ms: float = 0.0
+    allreduce_ms: float = 0.0
 
     @property
     def cell_updates_per_s(self) -> float:
@@ -168,6 +174,15 @@ class Simulation:
     def epoch_depth(self) -> int:
         return self._eng.epoch_depth
 
+    @property
+    def phase_timing(self) -> bool:
+        """Per-phase device timing of the following runs (RunReport.*_ms)."""
+        return bool(self._eng.phase_timing)
+
+    @phase_timing.setter
+    def phase_timing(self, on: bool) -> None:
+        self._eng.phase_timing = bool(on)
+
     def describe(self) -> dict[str, Any]:
         d = self._eng.decomp
         g = self._eng.geom
@@ -176,7 +191,9 @@ class Simulation:
                 "rank": self.rank, "ranks": d.nranks(), "tile_rows": g.H, "tile_cols": g.W,
                 "halo_rows": g.Dv, "halo_words": g.hw, "tmax": self._eng.tmax,
                 "epoch": self._eng.epoch_depth, "pitch": g.pitch, "overlap": self._eng.overlap(),
-                "graphs": self._eng.graphs(),
+                "graphs": self._eng.graphs(), "overlap_mode": self._eng.overlap_mode(),
+                "overlap_trial_ms_plain": self._eng.trial_ms_plain,
+                "overlap_trial_ms_early": self._eng.trial_ms_early,
                 "kernel": "adder window (drifting frame)" if self._eng.drifting else "symmetric window"}
 
     # -- state -----------------------------------------------------------
@@ -212,7 +229,9 @@ class Simulation:
                         loop_ms=r.loop_ms, first_unchanged=r.first_unchanged, extinct=r.extinct,
                         exchanges=r.exchanges, polls=r.polls, kernel_launches=r.kernel_launches,
                         cells=self.config.width * self.config.height, overlapped=r.overlapped,
-                        graph_launches=r.graph_launches, halo_bytes=r.halo_bytes)
+                        graph_launches=r.graph_launches, halo_bytes=r.halo_bytes, phase_timed=r.phase_timed,
+                        compute_ms=r.compute_ms, halo_ms=r.halo_ms, fill_ms=r.fill_ms,
+                        allreduce_ms=r.allreduce_ms)
         self.last_report = rep
         return rep
 

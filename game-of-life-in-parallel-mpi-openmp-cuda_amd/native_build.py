@@ -70,21 +70,36 @@ def _compile_cmd(src: Path, obj: Path) -> list[str]:
             extra = ["-mllvm", f"-amdgpu-sched-strategy={os.environ.get('GOL_SCHED_STRATEGY', 'max-ilp')}"]
         return [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                 "-Wall", "-Wno-unused-result", "-munsafe-fp-atomics", *inc, f"-I{ROCM / 'include'}",
-                *extra, "-c", str(src), "-o", str(obj)]
+                *extra, "-MMD", "-MF", str(obj.with_suffix(".d")), "-c", str(src), "-o", str(obj)]
     extra = []
     if src.name == "bindings.cpp":
         import pybind11  # noqa: PLC0415
         extra = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
                  "-fvisibility=hidden"]
     return ["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread", *inc, *extra,
-            "-c", str(src), "-o", str(obj)]
+            "-MMD", "-MF", str(obj.with_suffix(".d")), "-c", str(src), "-o", str(obj)]
+
+
+def _deps(obj: Path) -> list[Path] | None:
+    """Headers the object was built from (the compiler's -MMD file), or None."""
+    d = obj.with_suffix(".d")
+    if not d.exists():
+        return None
+    text = d.read_text().replace("\\\n", " ")
+    _, _, rest = text.partition(":")
+    return [Path(t) for t in rest.split() if t.endswith((".hpp", ".h", ".hip", ".inc"))]
 
 
 def _needs(obj: Path, src: Path, hdr_mtime: float) -> bool:
     if not obj.exists():
         return True
     om = obj.stat().st_mtime
-    return om < src.stat().st_mtime or om < hdr_mtime
+    if om < src.stat().st_mtime:
+        return True
+    deps = _deps(obj)
+    if deps is None:  # no dependency record: any header change rebuilds
+        return om < hdr_mtime
+    return any((not p.exists()) or om < p.stat().st_mtime for p in deps if str(p).startswith(str(CSRC)))
 
 
 def _run(cmd: list[str], verbose: bool) -> None:

@@ -178,3 +178,34 @@ def allreduce_max_float(x: float) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_grid(sim, group=None):
+    """Whole grid assembled on every rank from the ranks' tiles (the
+    reference's rank-0 gather, src/game_mpi.c:429-458, as one all_gather of
+    padded tiles over the process group: RCCL on GPU, gloo on CPU).  Used
+    for verification and the --show viewer, not on the hot path."""
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+
+    tile = np.ascontiguousarray(sim.tile(), dtype=np.uint8)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return tile
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    world = dist.get_world_size(group)
+    (r0, r1), (c0, c1) = sim.rows, sim.cols
+    ext = torch.tensor([r0, r1, c0, c1], dtype=torch.int64, device=dev)
+    exts = [torch.zeros_like(ext) for _ in range(world)]
+    dist.all_gather(exts, ext, group=group)
+    exts = [tuple(int(v) for v in e.cpu()) for e in exts]
+    mh = max(e[1] - e[0] for e in exts)
+    mw = max(e[3] - e[2] for e in exts)
+    pad = torch.zeros((mh, mw), dtype=torch.uint8, device=dev)
+    pad[: r1 - r0, : c1 - c0] = torch.from_numpy(tile).to(dev)
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    H, W = sim.config.height, sim.config.width
+    out = np.zeros((H, W), dtype=np.uint8)
+    for (a, b, c, d), t in zip(exts, parts):
+        out[a:b, c:d] = t[: b - a, : d - c].cpu().numpy()
+    return out

@@ -30,9 +30,11 @@ class InProcessGroup:
         self.hub = C.ThreadHub(self.nranks)
         devs = list(devices) if devices else [0]
         self.sims: list[Simulation] = []
+        self.backends = []
         for r in range(self.nranks):
             be = make_backend(engine, devs[r % len(devs)], threads_per_rank)
             tr = C.thread_transport(self.hub, r, be)
+            self.backends.append(be)
             self.sims.append(Simulation(config, transport=tr, backend=be))
 
     def parallel(self, fn: Callable[[Simulation], object]) -> list:
@@ -41,6 +43,9 @@ class InProcessGroup:
 
         def work(r):
             try:
+                # A new thread starts on device 0: bind this rank's GPU first
+                # (every backend entry point also switches to its device).
+                self.backends[r].bind_thread()
                 out[r] = fn(self.sims[r])
             except BaseException as e:  # noqa: BLE001
                 errs[r] = e

@@ -5,12 +5,17 @@ input format, so ``./a.out N N game_output.out`` resumes from the last
 generation - losing the generation counter and the similarity-counter phase
 (src/game.c:171).  Here a checkpoint is
 
-* ``grid.txt``  - the text grid, written by every rank at its subarray
-  offsets (same path as the output writer, so it stays a valid input), and
-* ``meta.json`` - generation number, similarity phase and run config,
+* ``grid-<gen>[b].txt`` - the text grid, written by every rank at its
+  subarray offsets (same path as the output writer, so it stays a valid
+  input), and
+* ``meta.json`` - generation number, similarity phase, run config and the
+  name of its grid file,
 
 so a resumed run reproduces an uninterrupted one exactly (same final grid,
-same "Generations" line).
+same "Generations" line).  A new checkpoint writes a grid file the committed
+one does not use, fsyncs it, then replaces meta.json atomically and only
+then deletes the old grid: a crash at any point leaves one complete
+checkpoint (csrc/include/gol/checkpoint.hpp, same format).
 """
 from __future__ import annotations
 
@@ -23,6 +28,25 @@ from ..models.life import LifeConfig, RunReport, Simulation
 from .termination import reported_generations, sim_phase_at
 
 
+def committed_grid(directory) -> Optional[str]:
+    """Grid file name of the committed checkpoint in ``directory`` (None: none)."""
+    meta = Path(directory) / "meta.json"
+    if not meta.exists():
+        return None
+    return json.loads(meta.read_text()).get("grid", "grid.txt")
+
+
+def _fsync(path: Path, directory: bool = False) -> None:
+    fd = os.open(str(path), os.O_RDONLY | (os.O_DIRECTORY if directory else 0))
+    try:
+        os.fsync(fd)
+    except OSError:
+        if not directory:
+            raise
+    finally:
+        os.close(fd)
+
+
 def save_checkpoint(sim: Simulation, directory: str, is_root: bool = True, barrier=None) -> Path:
     d = Path(directory)
     if is_root:
@@ -31,14 +55,20 @@ def save_checkpoint(sim: Simulation, directory: str, is_root: bool = True, barri
         barrier()
     cfg = sim.config
     gen = sim.generation
+    # Every rank picks the same fresh name (nobody commits before the last
+    # barrier below), never the committed checkpoint's file.
+    previous = committed_grid(d)
+    name = f"grid-{gen}.txt"
+    if name == previous:
+        name = f"grid-{gen}b.txt"
     meta = {
         "format": "gol-mi355x-checkpoint-v1",
         "width": cfg.width, "height": cfg.height, "generation": gen,
         "sim_phase": sim_phase_at(gen, cfg.start_gen, cfg.sim_phase, cfg.sim_freq),
         "gen_limit": cfg.gen_limit, "check_similarity": cfg.check_similarity,
-        "sim_freq": cfg.sim_freq, "layout": cfg.resolved_layout(),
+        "sim_freq": cfg.sim_freq, "layout": cfg.resolved_layout(), "grid": name,
     }
-    grid = d / "grid.txt"
+    grid = d / name
     if is_root:
         from .io import create_text_file  # noqa: PLC0415
         create_text_file(str(grid), cfg.width, cfg.height)
@@ -48,9 +78,18 @@ def save_checkpoint(sim: Simulation, directory: str, is_root: bool = True, barri
     if barrier:
         barrier()
     if is_root:
+        if os.environ.get("GOL_FAULT_CHECKPOINT_CRASH_PY") == str(gen):  # fault injection (tests)
+            os._exit(86)
+        _fsync(grid)
         tmp = d / "meta.json.tmp"
         tmp.write_text(json.dumps(meta, indent=1))
+        _fsync(tmp)
         os.replace(tmp, d / "meta.json")
+        _fsync(d, directory=True)
+        if previous and previous != name and (d / previous).exists():
+            (d / previous).unlink()
+    if barrier:
+        barrier()
     return d
 
 
@@ -63,7 +102,7 @@ def load_checkpoint(directory: str, **overrides) -> tuple[LifeConfig, Path]:
                      sim_phase=meta["sim_phase"])
     for k, v in overrides.items():
         setattr(cfg, k, v)
-    return cfg, d / "grid.txt"
+    return cfg, d / meta.get("grid", "grid.txt")
 
 
 def run_with_checkpoints(sim: Simulation, every: int, directory: Optional[str], is_root: bool = True,

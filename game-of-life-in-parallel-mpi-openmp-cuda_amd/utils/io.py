@@ -50,3 +50,18 @@ def parse_text(text: str, width: int, height: int) -> np.ndarray:
 def format_text(grid: np.ndarray) -> str:
     g = np.asarray(grid)
     return "".join("".join("1" if v else "0" for v in row) + "\n" for row in g)
+
+
+def show_text(grid: np.ndarray) -> str:
+    """The reference's VT100 viewer (src/game.c:42-58): cursor home, then per
+    row two reverse-video spaces for every live cell and two plain spaces for
+    every dead one, and a next-line escape.  (The MPI copy tests truthiness,
+    so it shows every cell as live, quirk Q3; here a cell is live if it is
+    1 or '1'.)"""
+    g = np.asarray(grid)
+    live = (g == 1) | (g == ord("1"))
+    out = ["\033[H"]
+    for row in live:
+        out.append("".join("\033[07m  \033[m" if v else "  " for v in row))
+        out.append("\033[E")
+    return "".join(out)

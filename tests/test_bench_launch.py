@@ -1,0 +1,167 @@
+"""bench.py's launch contract, per-phase timing and the overlap auto trial on
+the CPU (gloo / thread transports).
+
+* ``bench.py --gpus N`` with no launcher starts N rank processes itself
+  (the reference's ``mpiexec -n P``, README.md:56) and reports n_gpus = N;
+  a launcher whose WORLD_SIZE differs from --gpus is refused.
+* Per-phase device times are present and account for the
+  generation loop.
+* ``overlap=auto`` alternates the plain and early-boundary schedules, decides
+  at the same epoch on every rank, and is exact in both outcomes and across
+  the switch.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from gol_amd import LifeConfig, Simulation, random_grid, reference_run
+from gol_amd.parallel import InProcessGroup
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(REPO) + os.pathsep + env.get("PYTHONPATH", "")
+    env["GOL_HOST_THREADS"] = "2"
+    env["OMP_NUM_THREADS"] = "1"
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(REPO / "bench.py"), *map(str, args)], cwd=REPO, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+SMALL = ["--engine", "cpu", "--size", 256, "--steps", 3, "--warmup", 1, "--gens-per-step", 100, "--prewarm", 16,
+         "--verify", 40]
+
+
+@pytest.mark.parametrize("gpus", [1, 4])
+def test_bench_gpus_n_launches_n_ranks_itself(native, gpus):
+    r = _bench(["--gpus", gpus, *SMALL])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == gpus and rec["steps"] == 3 and rec["warmup"] == 1
+    cfg = rec["config"]
+    assert cfg["generations_timed"] == 300 and cfg["step_stop_reasons"] == ["limit"]
+    assert cfg["parallelism"].startswith("1x1" if gpus == 1 else f"1x{gpus}")
+    assert rec["verified"] is True
+    assert cfg["verify"]["vs_torch_fp32_conv2d"] and cfg["verify"]["vs_u8_layout"]
+    assert cfg["verify"]["generations"] == 40
+    ph = cfg["phase_ms_one_step"]
+    assert ph["generations"] == 100 and ph["compute_ms"] > 0 and ph["allreduce_ms"] >= 0
+    if gpus > 1:
+        assert ph["halo_ms"] > 0 and cfg["halo_bytes_per_step"] > 0
+
+
+def test_bench_refuses_a_launcher_with_another_world_size(native):
+    r = _bench(["--gpus", 4, *SMALL], env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert r.stdout.strip() == ""
+    assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_phase_times_account_for_the_loop(native):
+    g = random_grid(512, 384, 3)
+    sim = Simulation(LifeConfig(512, 384, gen_limit=300, tmax=8, epoch=32), engine="cpu")
+    sim.load(g)
+    assert sim.advance(50).phase_timed is False
+    sim.phase_timing = True
+    rep = sim.advance(250)
+    assert rep.phase_timed
+    total = rep.compute_ms + rep.halo_ms + rep.fill_ms + rep.allreduce_ms
+    assert rep.compute_ms > 0 and rep.fill_ms > 0
+    # Synchronous backend: the phases tile the loop (host bookkeeping aside).
+    assert 0.6 * rep.loop_ms <= total <= 1.01 * rep.loop_ms, (total, rep.loop_ms)
+
+
+def test_phase_times_with_ranks(native):
+    W, H = 256, 512
+    g = random_grid(W, H, 5)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=200, decomp="2x2", tmax=8, epoch=16), 4, engine="cpu")
+    grp.load(g)
+    for s in grp.sims:
+        s.phase_timing = True
+    reps = grp.run()  # with termination polls: flag all-reduces
+    for r in reps:
+        assert r.phase_timed and r.compute_ms > 0 and r.halo_ms > 0 and r.allreduce_ms > 0
+        assert r.compute_ms + r.halo_ms + r.fill_ms + r.allreduce_ms <= 1.01 * r.loop_ms
+    want, gens, _ = reference_run(g, 200)
+    assert all(r.generations == gens for r in reps)
+    assert (grp.gather() == want).all()
+
+
+@pytest.mark.parametrize("pick", ["plain", "early", ""])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_overlap_auto_trial_is_exact(native, monkeypatch, pick, layout):
+    """Trial epochs alternate the schedules (early-boundary sends included),
+    then every rank keeps the decided one; forced either way (and measured)
+    the final grid and Generations equal the serial loop's."""
+    monkeypatch.setenv("GOL_OVERLAP_AUTO", pick)
+    W, H, gens = 256, 3 * 200, 700
+    g = random_grid(W, H, 7)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x3", layout=layout, tmax=8, epoch=32,
+                                    check_similarity=False), 3, engine="cpu")
+    grp.load(g)
+    reps = grp.advance(gens)
+    modes = {s.describe()["overlap_mode"] for s in grp.sims}
+    assert len(modes) == 1
+    mode = modes.pop()
+    if pick:
+        assert mode == f"auto:{pick}"
+    else:
+        assert mode in ("auto:plain", "auto:early")
+    d = grp.sims[0].describe()
+    assert d["overlap_trial_ms_plain"] > 0 and d["overlap_trial_ms_early"] > 0
+    assert all(r.overlapped for r in reps)  # the trial ran early-boundary epochs
+    want, _, _ = reference_run(g, gens, check_similarity=False)
+    assert (grp.gather() == want).all()
+
+
+def test_overlap_auto_with_termination(native, monkeypatch):
+    """A run that stops at a fixed point during the trial keeps the exact
+    Generations line, and the next run continues the trial."""
+    monkeypatch.setenv("GOL_OVERLAP_AUTO", "early")
+    W, H = 32, 96
+    g = random_grid(W, H, 95, 0.1)
+    ref, rgens, _ = reference_run(g)
+    assert rgens < 1000
+    grp = InProcessGroup(LifeConfig(W, H, decomp="1x3", tmax=2, epoch=4, poll_gens=8), 3, engine="cpu")
+    grp.load(g)
+    reps = grp.run()
+    assert all(r.generations == rgens for r in reps)
+    assert (grp.gather() == ref).all()
+
+
+def test_overlap_auto_is_off_without_row_exchange(native):
+    sim = Simulation(LifeConfig(256, 256, gen_limit=100), engine="cpu")
+    sim.load(random_grid(256, 256, 1))
+    sim.run()
+    assert sim.describe()["overlap_mode"] == "off"
+
+
+def test_python_cli_show_prints_the_vt100_view(native, tmp_path):
+    from gol_amd.utils import io
+
+    g = np.array([[0, 1, 0], [1, 1, 0]], dtype=np.uint8)
+    want = "\033[H" + "  \033[07m  \033[m  " + "\033[E" + "\033[07m  \033[m\033[07m  \033[m  " + "\033[E"
+    assert io.show_text(g) == want
+    assert io.show_text(np.where(g == 1, ord("1"), ord("0")).astype(np.uint8)) == want
+    grid = random_grid(8, 6, 2)
+    inp = tmp_path / "in.txt"
+    io.write_grid(str(inp), grid)
+    env = dict(os.environ, PYTHONPATH=str(REPO))
+    r = subprocess.run([sys.executable, "-m", "gol_amd", "8", "6", str(inp), "--engine", "cpu", "--gens", "5",
+                        "--output", "none", "--show"], cwd=tmp_path, env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    ref, gens, _ = reference_run(grid, 5)
+    assert r.stdout.startswith(f"Finished.\n\nGenerations:\t{gens}\n")
+    assert r.stdout.endswith(io.show_text(ref))

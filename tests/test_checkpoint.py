@@ -5,6 +5,7 @@ import json
 import os
 import subprocess
 import sys
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -83,7 +84,7 @@ def test_checkpoint_grid_is_a_valid_reference_input(native, tmp_path):
     sim.load(g)
     sim.advance(13)
     d = save_checkpoint(sim, str(tmp_path / "ck"))
-    text = (d / "grid.txt").read_text()
+    text = (d / json.loads((d / "meta.json").read_text())["grid"]).read_text()
     assert text == io.format_text(np.asarray(sim.tile()))
 
 
@@ -147,3 +148,77 @@ def test_native_resume_rejects_a_missing_or_foreign_checkpoint(gol_bin, tmp_path
     (tmp_path / "bad" / "meta.json").write_text('{"format": "something-else"}')
     r = subprocess.run([str(gol_bin), "--resume", str(tmp_path / "bad")], capture_output=True, text=True)
     assert r.returncode != 0 and "format" in r.stderr
+
+
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_native_checkpoint_crash_before_commit_keeps_previous(gol_bin, tmp_path, ranks):
+    """A kill after the second checkpoint's tiles are written but before it is
+    committed (GOL_FAULT_CHECKPOINT_CRASH=2) must leave the first checkpoint
+    complete: meta.json still names its grid file, which still holds the
+    grid of that generation, and resuming from it is exact."""
+    W, H, seed = 64, 48, 5
+    g = random_grid(W, H, seed)
+    inp = tmp_path / "in.txt"
+    io.write_grid(str(inp), g)
+    ck = tmp_path / "ck"
+    env = dict(os.environ, GOL_FAULT_CHECKPOINT_CRASH="2")
+    r = subprocess.run([str(gol_bin), str(W), str(H), str(inp), "--engine", "cpu", "--ranks", str(ranks), "--gens",
+                        "100", "--checkpoint-every", "20", "--checkpoint-dir", str(ck), "--output", "none"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 86, r.stderr
+    meta = json.loads((ck / "meta.json").read_text())
+    assert meta["generation"] == 20 and meta["grid"] == "grid-20.txt"
+    want20, _, _ = reference_run(g, 20, check_similarity=False)
+    assert (io.read_grid(str(ck / meta["grid"]), W, H) == want20).all()
+    assert (ck / "grid-40.txt").exists()  # the uncommitted attempt, never named by meta.json
+    ref, rgens, _ = reference_run(g, 100)
+    res = _bin(gol_bin, ["--resume", ck, "--engine", "cpu", "--output", tmp_path / "res.out"], tmp_path)
+    assert _gens(res) == rgens
+    assert (io.read_grid(str(tmp_path / "res.out"), W, H) == ref).all()
+
+
+def test_native_checkpoint_removes_superseded_grid(gol_bin, tmp_path):
+    W, H = 64, 32
+    ck = tmp_path / "ck"
+    _bin(gol_bin, [W, H, "--random", "3", "--engine", "cpu", "--gens", 60, "--no-similarity",
+                   "--checkpoint-every", 20, "--checkpoint-dir", ck, "--output", "none"], tmp_path)
+    meta = json.loads((ck / "meta.json").read_text())
+    assert meta["generation"] == 40
+    assert sorted(p.name for p in ck.iterdir()) == ["grid-40.txt", "meta.json"]
+
+
+def test_python_checkpoint_crash_before_commit_keeps_previous(native, tmp_path):
+    """Python writer: a process killed between the tile writes and the commit
+    of its second checkpoint leaves the first one loadable and exact."""
+    code = f"""
+import sys
+sys.path.insert(0, {str(Path(__file__).resolve().parents[1])!r})
+from gol_amd import LifeConfig, Simulation, random_grid
+from gol_amd.utils.checkpoint import save_checkpoint
+g = random_grid(40, 30, 9)
+sim = Simulation(LifeConfig(40, 30, check_similarity=False), engine="cpu")
+sim.load(g)
+sim.advance(10)
+save_checkpoint(sim, {str(tmp_path / "ck")!r})
+sim.advance(10)
+save_checkpoint(sim, {str(tmp_path / "ck")!r})
+"""
+    env = dict(os.environ, GOL_FAULT_CHECKPOINT_CRASH_PY="20")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 86, r.stderr
+    cfg, grid = load_checkpoint(str(tmp_path / "ck"))
+    assert cfg.start_gen == 10 and grid.name == "grid-10.txt"
+    want, _, _ = reference_run(random_grid(40, 30, 9), 10, check_similarity=False)
+    assert (io.read_grid(str(grid), 40, 30) == want).all()
+
+
+def test_checkpoint_same_generation_twice_uses_alternate_file(native, tmp_path):
+    g = random_grid(40, 30, 2)
+    sim = Simulation(LifeConfig(40, 30), engine="cpu")
+    sim.load(g)
+    sim.advance(5)
+    save_checkpoint(sim, str(tmp_path / "ck"))
+    save_checkpoint(sim, str(tmp_path / "ck"))
+    meta = json.loads((tmp_path / "ck" / "meta.json").read_text())
+    assert meta["grid"] == "grid-5b.txt"
+    assert sorted(p.name for p in (tmp_path / "ck").iterdir()) == ["grid-5b.txt", "meta.json"]

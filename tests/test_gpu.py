@@ -647,3 +647,25 @@ def test_fused_periodic_fill_matches_cpu_buffer(gpu, monkeypatch, W, H, epoch):
     (a, dva, hwa), (b, dvb, hwb) = bufs
     assert (dva, hwa) == (dvb, hwb) and dva > 0 and hwa > 0
     assert np.array_equal(a, b)
+
+
+def test_inprocess_ranks_keep_device_affinity(gpu, monkeypatch, tmp_path):
+    """Single-process multi-rank run from fresh Python threads with
+    GOL_CHECK_DEVICE=1: every backend entry point asserts its device is
+    current and that its staging / chain / scratch buffers and the launch
+    operands live on it.  Drives load_text, the autotuned chained-group
+    launches, halo exchanges and store_cells (gather)."""
+    from gol_amd.utils import io
+
+    monkeypatch.setenv("GOL_CHECK_DEVICE", "1")
+    monkeypatch.setenv("GOL_CHAIN", "-1")
+    W, H, gens = 32 * 64, 4 * 640, 300
+    p = tmp_path / "in.txt"
+    io.generate(str(p), W, H, seed=9)
+    g = io.read_grid(str(p), W, H)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x4", epoch=96), 4, engine="hip",
+                         devices=[0, 0, 0, 0])
+    grp.parallel(lambda s: s.load_text(str(p)))
+    reps = grp.advance(gens)
+    assert all(r.executed == gens for r in reps)
+    assert (grp.gather() == life_step_torch(g, gens, device="cuda")).all()

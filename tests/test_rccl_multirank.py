@@ -1,0 +1,88 @@
+"""Multi-rank RCCL on the one-GPU box (SURVEY 4.3 tier T4).
+
+RCCL refuses two ranks of one communicator on the same device only when they
+share a host hash; with a distinct NCCL_HOSTID per rank the ranks become
+separate "nodes" that talk over RCCL's socket transport.  So N real rank
+processes share GPU 0 and run the native RcclTransport - grouped
+ncclSend/ncclRecv halos, ncclAllReduce(MAX) termination flags, the overlap
+auto trial's MAX-reduced timings - exactly as on a multi-GPU node, only with
+a slower wire.  Every case is checked against the fp32 conv2d oracle and the
+exact serial loop (tests/mp_rccl_worker.py).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(REPO) + os.pathsep + env.get("PYTHONPATH", "")
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def _ndev() -> int:
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def _torchrun(nproc, args, timeout=240):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", *args]
+    return subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("nproc,cases", [
+    (2, "1x2:bits:auto,1x2:u8:on,2x1:bits:off,1x2:bits:edges"),
+    (4, "1x4:bits:auto,2x2:bits:off,2x2:u8:auto,1x4:u8:off"),
+])
+def test_rccl_ranks_sharing_one_gpu(gpu, nproc, cases):
+    r = _torchrun(nproc, [str(REPO / "tests" / "mp_rccl_worker.py"), cases])
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert f"MULTIRANK PASS world={nproc}" in r.stdout, r.stderr[-4000:]
+
+
+def test_bench_launches_its_own_ranks_on_gpu(gpu):
+    """bench.py --gpus 2 with no launcher: it starts 2 rank processes itself
+    (RCCL halos, shared GPU rehearsal), relays one JSON line with n_gpus 2,
+    and the verification gate passes."""
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--share-gpus", "--size", "2048",
+           "--steps", "2", "--warmup", "1", "--gens-per-step", "200", "--prewarm", "2400", "--verify", "100"]
+    r = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["verified"] is True
+    cfg = rec["config"]
+    assert cfg["shared_gpus"] is (_ndev() < 2) and cfg["generations_timed"] == 400
+    assert "rccl" in cfg["parallelism"] and cfg["halo_bytes_per_step"] > 0
+    assert cfg["overlap_mode"] in ("auto:plain", "auto:early")
+    ph = cfg["phase_ms_one_step"]
+    assert ph["compute_ms"] > 0 and ph["halo_ms"] > 0 and ph["allreduce_ms"] > 0
+
+
+def test_bench_refuses_more_ranks_than_gpus_without_share(gpu):
+    if _ndev() >= 2:
+        pytest.skip("every rank has a GPU of its own here")
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--size", "2048", "--steps", "1",
+           "--warmup", "0", "--gens-per-step", "50", "--prewarm", "0", "--verify", "0"]
+    r = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0
+    assert r.stdout.strip() == ""
