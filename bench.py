@@ -36,7 +36,8 @@ of the multi-rank path on a one-GPU box, not a performance number).
 After the timed steps (outside the timed region) the same engine runs one
 more step with per-phase device timing (kernels / halos / fills / flag
 reductions, --no-phase-step to skip), and then --verify G generations
-that are checked bit for bit against an fp32 PyTorch conv2d oracle and the
+that are checked bit for bit against an fp32 PyTorch oracle (rolled-copy
+neighbour sums, ops/life_ops.py life_step_torch_roll) and the
 byte-per-cell layout, started from the engine's state at that point:
 `verified` in the JSON line says whether the credited schedule is exact.
 
@@ -141,7 +142,7 @@ def parse_args(argv=None):
                     help="let ranks share GPUs (rehearsal of the multi-rank path on fewer GPUs than ranks)")
     ap.add_argument("--verify", type=int, default=240,
                     help="after the timed steps, run G more generations and check them against the fp32 "
-                         "PyTorch conv2d oracle and the u8 layout (0: skip)")
+                         "PyTorch oracle and the u8 layout (0: skip)")
     ap.add_argument("--no-phase-step", action="store_true",
                     help="skip the extra per-phase-timed step after the timed ones")
     return ap.parse_args(argv)
@@ -269,7 +270,7 @@ def main() -> int:
     verify = None
     verified = None
     if a.verify > 0:
-        from gol_amd.ops.life_ops import life_step_torch  # noqa: PLC0415
+        from gol_amd.ops.life_ops import life_step_torch_roll  # noqa: PLC0415
         from gol_amd.parallel.dist import gather_grid  # noqa: PLC0415
 
         t_v = time.perf_counter()
@@ -281,7 +282,7 @@ def main() -> int:
         ok_torch = ok_u8 = True
         if rank == 0:
             dev = "cuda" if on_gpu else "cpu"
-            want = life_step_torch(snap, done, device=dev)
+            want = life_step_torch_roll(snap, done, device=dev)
             ok_torch = bool(np.array_equal(final, want))
             u8 = Simulation(LifeConfig(S, Hg, gen_limit=done, layout="u8", check_similarity=False),
                             transport=native().self_transport(), backend=backend)
@@ -291,7 +292,7 @@ def main() -> int:
             del u8
         verified = bool(ok_torch and ok_u8)
         verify = {"generations": int(done), "from_generation": int(g_snap), "stop_reason": rv.stop_reason,
-                  "vs_torch_fp32_conv2d": ok_torch, "vs_u8_layout": ok_u8,
+                  "vs_torch_fp32_oracle": ok_torch, "vs_u8_layout": ok_u8,
                   "seconds": round(time.perf_counter() - t_v, 2)}
         if dist is not None:
             dist.barrier()

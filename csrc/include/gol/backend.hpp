@@ -120,6 +120,10 @@ class Backend {
   virtual KernelChoice choose_kernel(Layout l, int64_t /*rows*/, int64_t /*cols*/, int tmax_req) const {
     return {tmax_req > 0 ? tmax_req : preferred_tmax(l), drifts(l)};
   }
+  // Fewest output rows a run_block of T generations accepts (the pipelined
+  // deep byte pass plans whole wave-pair groups); the engine keeps every
+  // block at least this tall or uses a smaller T.
+  virtual int64_t min_block_rows(Layout /*l*/, int /*T*/) const { return 1; }
   // Periodic self-fill of halo regions of a single tile (any tile size):
   // columns (left/right halo words of owned rows) and/or rows (full padded
   // rows of the top/bottom halo, which also fills the corners).

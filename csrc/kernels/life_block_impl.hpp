@@ -104,14 +104,22 @@ __device__ __forceinline__ uint32_t left_in_carry(uint32_t first, uint32_t last)
 
 // Words produced per wave, and which lane words are the wave's halo: the
 // symmetric windows need one halo word per side; the one-sided adder window
-// (kXlaneAdd) reads nothing to its right, so only lane 0 is a halo.
-template <int XL, int W>
+// (kXlaneAdd) reads nothing to its right, so only lane 0 is a halo.  A pass
+// deeper than 32 generations consumes more than one 32-cell word of its
+// light cone per side: the T = 48 byte pass (U8IO<1, XL, 2>) keeps H = 2
+// halo lanes per side (60 output words per wave).
+template <int XL, int W, int H = 1>
 constexpr int wave_out_words() {
-  return XL == kXlaneAdd ? 64 * W - 1 : 64 * W - 2;
+  return XL == kXlaneAdd ? 64 * W - H : 64 * W - 2 * H;
 }
-template <int XL, int W>
+template <int XL, int W, int H = 1>
 __device__ __forceinline__ bool wave_halo(int lane, int i) {
-  return (lane == 0 && i == 0) || (XL != kXlaneAdd && lane == 63 && i == W - 1);
+  if constexpr (H == 1) {
+    return (lane == 0 && i == 0) || (XL != kXlaneAdd && lane == 63 && i == W - 1);
+  } else {
+    static_assert(W == 1, "wide wave halos: one word per lane");
+    return lane < H || (XL != kXlaneAdd && lane >= 64 - H);
+  }
 }
 
 // Column map of one lane (all life_block kernels).
@@ -140,8 +148,8 @@ struct LaneCols {
 template <class IO>
 __device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int kcol, int lane, int sub_lanes = 64,
                                                   int nsub = 1) {
-  constexpr int W = IO::W, XL = IO::XL;
-  constexpr int kWaveOut = wave_out_words<XL, W>();
+  constexpr int W = IO::W, XL = IO::XL, H = IO::kHalo;
+  constexpr int kWaveOut = wave_out_words<XL, W, H>();
   LaneCols<IO> c;
   int j = lane;
   c.sub = 0;
@@ -149,14 +157,14 @@ __device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int 
     c.sub = lane / sub_lanes;
     j = lane - c.sub * sub_lanes;
   }
-  const int lc0 = kcol * kWaveOut - 1 + W * j;
+  const int lc0 = kcol * kWaveOut - H + W * j;
   if (p.wrap_w == 0) {
     c.store_col = lc0;
 #pragma unroll
     for (int i = 0; i < W; ++i) {
       const int cc = lc0 + i;
       c.ok[i] = cc >= 0 && cc < p.Wp;
-      c.own[i] = c.ok[i] && !wave_halo<XL, W>(lane, i);
+      c.own[i] = c.ok[i] && !wave_halo<XL, W, H>(lane, i);
       c.fmask[i] = (c.own[i] && cc >= p.own_w0 && cc < p.own_w1) ? (cc == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
       c.off[i] = min(max(cc, 0), p.Wp - 1);
     }
@@ -168,7 +176,8 @@ __device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int 
 #pragma unroll
   for (int i = 0; i < W; ++i) {
     const int lc = lc0 + i;
-    const bool halo = sub_lanes < 64 ? (j == 0 || (XL != kXlaneAdd && j == sub_lanes - 1)) : wave_halo<XL, W>(lane, i);
+    const bool halo =
+        sub_lanes < 64 ? (j == 0 || (XL != kXlaneAdd && j == sub_lanes - 1)) : wave_halo<XL, W, H>(lane, i);
     c.ok[i] = true;
     c.own[i] = live && !halo && lc >= 0 && lc < ww;
     c.fmask[i] = c.own[i] ? (lc == ww - 1 ? p.last_mask : ~0u) : 0u;
@@ -254,6 +263,7 @@ __device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, 
 template <int W_, int XL_>
 struct BitsIO {
   static constexpr int W = W_, XL = XL_;
+  static constexpr int kHalo = 1;  // halo lanes per wave side
   static constexpr bool kBits = true;
   struct Raw {
     uint32_t w[W];
@@ -290,9 +300,10 @@ struct BitsIO {
 #define GOL_U8_LOAD_NT 0
 #endif
 
-template <int W_, int XL_>
+template <int W_, int XL_, int HALO_ = 1>
 struct U8IO {
   static constexpr int W = W_, XL = XL_;
+  static constexpr int kHalo = HALO_;  // halo lanes per wave side (2: passes deeper than 32)
   static constexpr bool kBits = false;
   struct Raw {
     uint4 q[2 * W];

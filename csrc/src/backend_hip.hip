@@ -75,6 +75,7 @@ class HipBackend final : public Backend {
     tune_.wrap = env_int("GOL_WRAP", 1) != 0;
     tune_.fold = env_int("GOL_FOLD", 1) != 0;
     chain_mode_ = env_int("GOL_CHAIN", -1);
+    u8_pipe_ = env_int("GOL_U8_PIPE", 1) != 0;
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
     tune_log_ = env_int("GOL_TUNE_LOG", 0) != 0;
     tune_.chain_seq = &chain_seq_;
@@ -452,6 +453,11 @@ class HipBackend final : public Backend {
   // give every SIMD one is taken; below that T = 16 (8192^2: 2.83 vs 3.03 at
   // 24; 32768 x 4096: 3.7-3.9 vs 4.4 at 24 and 4.9 at 32;
   // profiles/r02/u8_t24*.jsonl, u8_t32.jsonl).
+  //
+  // Deeper still, T = 48 runs as level-pipelined wave pairs (24 + 24
+  // levels, four pairs per workgroup, 2 waves per SIMD): taken when the tile
+  // gives every CU a workgroup of four pairs of at least 2T + 2 rows plus the
+  // group's T - 1 boundary rows (GOL_U8_PIPE=0: off).
   KernelChoice choose_kernel(Layout l, int64_t rows, int64_t cols, int tmax_req) const override {
     KernelChoice k{tmax_req > 0 ? tmax_req : preferred_tmax(l), false};
     if (l == Layout::U8 && tmax_req <= 0 && !tune_.u8_lds) {
@@ -462,6 +468,12 @@ class HipBackend final : public Backend {
           k.tmax = int(kT);
           break;
         }
+      if (u8_pipe_)
+        for (int64_t kT : {48})
+          if (strips * (rows / (4 * (2 * kT + 2) + kT - 1)) >= int64_t(cus_)) {
+            k.tmax = int(kT);
+            break;
+          }
     }
     const bool one_word = l == Layout::U8 || tune_.wpl_bits < 2;
     if (tune_.xlane == hipk::kXlaneAdd && one_word) {
@@ -474,6 +486,9 @@ class HipBackend final : public Backend {
       if (strips * (rows / (2 * kT)) >= int64_t(16) * cus_) k = {int(kT), true};
     }
     return k;
+  }
+  int64_t min_block_rows(Layout l, int T) const override {
+    return l == Layout::U8 && T > 32 ? int64_t(4) * (2 * T + 2) + T - 1 : 1;
   }
   bool wraps_columns(Layout l) const override { return tune_.wrap && !(l == Layout::U8 && tune_.u8_lds); }
   void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override {
@@ -636,6 +651,7 @@ class HipBackend final : public Backend {
   void* chain_[2] = {nullptr, nullptr};  // chained groups: flags, slots (LifeTuning::chain_mem)
   size_t chain_bytes_[2] = {0, 0};
   uint32_t chain_seq_ = 0;
+  bool u8_pipe_ = true;  // GOL_U8_PIPE: T = 48 / 64 byte passes
   int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, 2 timing probe, -1 autotuned per launch shape
   bool tune_log_ = false;
   std::map<TuneKey, TuneStats> tuned_;

@@ -11,9 +11,10 @@
 namespace gol {
 
 namespace {
-// Temporal block sizes built for every backend; 32 and 24 for the byte layout
-// only (HBM-bound there: one grid read + write per pass, docs/PERFORMANCE.md).
-constexpr int kTSizes[] = {32, 24, 16, 12, 8, 4, 2, 1};
+// Temporal block sizes built for every backend; 48, 32 and 24 for the byte
+// layout only (HBM-bound there: one grid read + write per pass,
+// docs/PERFORMANCE.md; 48 as level-pipelined wave pairs).
+constexpr int kTSizes[] = {48, 32, 24, 16, 12, 8, 4, 2, 1};
 
 // Phases of RunResult's device-time split.
 enum Phase { kCompute = 0, kHalo = 1, kFill = 2, kReduce = 3, kPhases = 4 };
@@ -45,7 +46,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // made for the smallest tile of the decomposition, not this rank's.
   const Backend::KernelChoice kc =
       be_->choose_kernel(cfg_.layout, min_tile_rows(dec_), std::max<int64_t>(1, min_tile_cols(dec_)), cfg_.tmax);
-  tmax_ = std::min(kc.tmax, cfg_.layout == Layout::U8 ? 32 : 16);
+  tmax_ = std::min(kc.tmax, cfg_.layout == Layout::U8 ? 48 : 16);
   // Epoch depth: a deeper halo means fewer latency-bound exchanges (or local
   // periodic fills: two ~5 us launches each) but ~D redundant rows per epoch.
   // With the grouped kernel the per-rank tile costs the same from 8T to 24T
@@ -62,6 +63,16 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   }
   D_ = std::max(1, D);
   tmax_ = std::min(tmax_, D_);
+  // The smallest block of any schedule: the owned rows (a trapezoid's last
+  // block) and, where the row exchange may overlap compute, D rows (an edge
+  // strip, the early-boundary strips) and the interior (H - 2D).  A deep pass
+  // that cannot plan that few rows steps down to the next T.
+  {
+    const int64_t h = min_tile_rows(dec_);
+    int64_t min_rows = h;
+    if (row_exchange && h >= 2 * int64_t(D_) + 1) min_rows = std::min({h, int64_t(D_), h - 2 * int64_t(D_)});
+    while (tmax_ > 1 && be_->min_block_rows(cfg_.layout, tmax_) > min_rows) tmax_ = pick_T(tmax_ - 1);
+  }
   // A drifting kernel (one-sided window, Backend::drifts) consumes 2 cells of
   // left halo per generation and none on the right; it needs the tile to be
   // the whole torus width so that the drift is a relabeling of columns.

@@ -33,7 +33,8 @@ HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/t
              "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp"]
 LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "bits_w1_add", "u8_w1_dpp",
                  "u8_w1_carry", "u8_w1_add",
-                 *[f"u8_w1_{x}_t{t}" for x in ("dpp", "carry", "add") for t in (24, 32)]]  # deep byte passes
+                 *[f"u8_w1_{x}_t{t}" for x in ("dpp", "carry", "add") for t in (24, 32)],  # deep byte passes
+                 "u8_w1_dpp_t48"]  # pipelined wave pairs (life_pipe_impl.hpp)
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
             *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
             "kernels/tile_ops.hip"]
@@ -120,7 +121,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     todo = [s for s in srcs if force or _needs(objs[s], CSRC / s, hdr)]
     # Longest compiles first (deep byte passes, then the kernel variants), so
     # the pool does not end on one long translation unit.
-    todo.sort(key=lambda s: 0 if ("_t24" in s or "_t32" in s) else 1 if "life_block_" in s else 2)
+    todo.sort(key=lambda s: 0 if any(f"_t{t}" in s for t in (24, 32, 48, 64)) else 1 if "life_block_" in s else 2)
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]

@@ -51,6 +51,22 @@ def life_step_torch(grid, gens: int = 1, device: str = "cpu"):
     return t[0, 0].to(torch.uint8).cpu().numpy()
 
 
+def life_step_torch_roll(grid, gens: int = 1, device: str = "cpu"):
+    """fp32 PyTorch reference of B3/S23 on a torus from elementwise ops only
+    (separable neighbour sums of rolled copies, no convolution library): the
+    verification oracle for whole-benchmark grids, where a first conv2d call
+    spends a minute in kernel selection on a fresh box."""
+    import torch  # noqa: PLC0415
+
+    t = torch.as_tensor(np.asarray(grid) != 0, dtype=torch.float32, device=device)
+    for _ in range(gens):
+        h = t + torch.roll(t, 1, 1) + torch.roll(t, -1, 1)
+        n = h + torch.roll(h, 1, 0) + torch.roll(h, -1, 0) - t
+        t = ((n == 3) | ((n == 2) & (t == 1))).to(torch.float32)
+        del h, n
+    return t.to(torch.uint8).cpu().numpy()
+
+
 def random_grid(width: int, height: int, seed: int = 1, density: float = 0.5) -> np.ndarray:
     """Host copy of the engine's counter-based RNG grid (same as init_random)."""
     return native().random_grid(int(width), int(height), int(seed), float(density))

@@ -53,7 +53,7 @@ def test_bench_gpus_n_launches_n_ranks_itself(native, gpus):
     assert cfg["generations_timed"] == 300 and cfg["step_stop_reasons"] == ["limit"]
     assert cfg["parallelism"].startswith("1x1" if gpus == 1 else f"1x{gpus}")
     assert rec["verified"] is True
-    assert cfg["verify"]["vs_torch_fp32_conv2d"] and cfg["verify"]["vs_u8_layout"]
+    assert cfg["verify"]["vs_torch_fp32_oracle"] and cfg["verify"]["vs_u8_layout"]
     assert cfg["verify"]["generations"] == 40
     ph = cfg["phase_ms_one_step"]
     assert ph["generations"] == 100 and ph["compute_ms"] > 0 and ph["allreduce_ms"] >= 0
@@ -165,3 +165,36 @@ def test_python_cli_show_prints_the_vt100_view(native, tmp_path):
     ref, gens, _ = reference_run(grid, 5)
     assert r.stdout.startswith(f"Finished.\n\nGenerations:\t{gens}\n")
     assert r.stdout.endswith(io.show_text(ref))
+
+
+def test_native_cli_metrics_carry_phases_and_comm(gol_bin, tmp_path):
+    """bin/gol --metrics-json: per-phase device times (implied phase timing),
+    the resolved in-process transport (auto -> thread for CPU ranks) and the
+    overlap mode."""
+    m = tmp_path / "m.json"
+    r = subprocess.run([str(gol_bin), "256", "600", "--random", "3", "--engine", "cpu", "--ranks", "3",
+                        "--decomp", "1x3", "--gens", "500", "--tmax", "8", "--epoch", "32", "--output", "none",
+                        "--metrics-json", str(m)], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rec = json.loads(m.read_text())
+    assert rec["comm"] == "thread" and rec["ranks"] == 3
+    assert rec["phase_timed"] is True and rec["compute_ms"] > 0 and rec["halo_ms"] > 0
+    assert rec["compute_ms"] + rec["halo_ms"] + rec["fill_ms"] + rec["allreduce_ms"] <= 1.01 * rec["loop_ms"]
+    assert rec["overlap_mode"] in ("auto:plain", "auto:early")
+
+
+def test_native_cli_rccl_needs_a_gpu_per_rank(gol_bin, tmp_path):
+    r = subprocess.run([str(gol_bin), "64", "64", "--random", "1", "--engine", "cpu", "--ranks", "2", "--comm", "rccl",
+                        "--output", "none"], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "rccl" in r.stderr
+
+
+def test_native_cli_resume_rejects_another_sim_freq(gol_bin, tmp_path):
+    ck = tmp_path / "ck"
+    r = subprocess.run([str(gol_bin), "64", "64", "--random", "1", "--engine", "cpu", "--gens", "40",
+                        "--checkpoint-every", "10", "--checkpoint-dir", str(ck), "--output", "none"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(gol_bin), "--resume", str(ck), "--engine", "cpu", "--sim-freq", "5", "--output", "none"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "--sim-freq" in r.stderr

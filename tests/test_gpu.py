@@ -669,3 +669,39 @@ def test_inprocess_ranks_keep_device_affinity(gpu, monkeypatch, tmp_path):
     reps = grp.advance(gens)
     assert all(r.executed == gens for r in reps)
     assert (grp.gather() == life_step_torch(g, gens, device="cuda")).all()
+
+
+@pytest.mark.parametrize("W,H", [(32 * 200, 1500), (1999, 1300), (32 * 300, 5000)])
+def test_pipelined_byte_pass_t48_vs_torch(gpu, W, H):
+    """T = 48 byte-layout passes as level-pipelined wave pairs (24 + 24
+    levels, life_block_u8_w1_dpp_t48.hip) against the fp32 conv oracle."""
+    g = random_grid(W, H, W + H)
+    gens = 2 * 48 + 11
+    want = life_step_torch(g, gens, device="cuda")
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=48), engine="hip")
+    assert sim.describe()["tmax"] == 48
+    sim.load(g)
+    sim.advance(gens)
+    assert (sim.tile() == want).all()
+
+
+def test_pipelined_byte_pass_t48_termination_and_ranks(gpu):
+    """The T = 48 pass with lazy termination (exact Generations), and in a
+    1x2 multi-subdomain run whose early-boundary strips are dual launches."""
+    grid = np.zeros((1600, 512), dtype=np.uint8)
+    W, H, seed, density = CONVERGING[5]
+    grid[700:700 + H, 200:200 + W] = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(grid)
+    out, rep = simulate(grid, 1000, engine="hip", layout="u8", tmax=48)
+    assert rep.generations == rgens
+    assert (out == ref).all()
+    W, H, gens = 32 * 40 + 5, 2 * 1500, 600
+    g = random_grid(W, H, 3)
+    want = life_step_torch(g, gens, device="cuda")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x2", layout="u8", tmax=48, epoch=480,
+                                    overlap="on"), 2, engine="hip", devices=[0])
+    assert grp.sims[0].describe()["tmax"] == 48
+    grp.load(g)
+    reps = grp.advance(gens)
+    assert all(r.overlapped for r in reps)
+    assert (grp.gather() == want).all()

@@ -63,7 +63,7 @@ def test_bench_launches_its_own_ranks_on_gpu(gpu):
     (RCCL halos, shared GPU rehearsal), relays one JSON line with n_gpus 2,
     and the verification gate passes."""
     cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--share-gpus", "--size", "2048",
-           "--steps", "2", "--warmup", "1", "--gens-per-step", "200", "--prewarm", "2400", "--verify", "100"]
+           "--steps", "2", "--warmup", "1", "--gens-per-step", "200", "--prewarm", "4000", "--verify", "100"]
     r = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
