@@ -102,6 +102,10 @@ class Backend {
   // column reads within the owned words): the engine then skips the periodic
   // column fills of whole-width tiles.
   virtual bool wraps_columns(Layout) const { return false; }
+  // Whether run_block also honours BlockArgs::wrap_rows for this layout (a
+  // single-rank whole-torus tile read modulo its owned rows at T = 1): the
+  // engine then runs one-generation epochs with no periodic fill at all.
+  virtual bool wraps_rows(Layout) const { return false; }
   // Owned rows of src rotated left by `shift` cells (0 < shift < W) into dst:
   // dst cell x = src cell (x + shift) mod W.  Halos of dst are not written.
   virtual void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) = 0;

@@ -249,6 +249,7 @@ class Engine {
   int64_t exchanges_ = 0, polls_ = 0, launches_ = 0;
   bool drift_ok_ = false;   // whole-width tile of 32-cell words on a drifting backend
   bool cols_filled_ = true; // column halos kept valid by fills (false: the backend wraps column reads)
+  bool rows_wrapped_ = false; // single-rank torus read modulo its rows (no fills at all)
   bool poll_side_ = false;   // termination polls reduce on the comm stream (Transport::side_reduce)
   int64_t drift_ = 0;
   int64_t graph_drift_[2] = {0, 0};

@@ -86,6 +86,10 @@ struct BlockArgs {
   // Run the launch's waves at the highest issue priority (s_setprio 3): the
   // small boundary launch that runs beside the interior of the same block.
   bool prio_boost = false;
+  // The tile is the whole torus (one rank): a backend that wraps row reads
+  // too (Backend::wraps_rows) reads rows modulo the owned rows, so the engine
+  // neither fills nor exchanges halo rows.
+  bool wrap_rows = false;
   // The tile is the whole torus width (Px == 1, W % 32 == 0): a backend may
   // wrap column reads within the owned words instead of reading halo columns,
   // which it then neither reads nor writes.

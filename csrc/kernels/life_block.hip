@@ -100,11 +100,11 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {
     BlockArgs b = a;
     b.dual_offset = 0;
-    launch_life_step_lds(b, tune.lds_rows, stream);
+    launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
     if (a.dual_offset) {
       b.row_lo += a.dual_offset;
       b.row_hi += a.dual_offset;
-      launch_life_step_lds(b, tune.lds_rows, stream);
+      launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
     }
     return 0;
   }

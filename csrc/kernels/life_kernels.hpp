@@ -136,7 +136,7 @@ GOL_LIFE_VARIANT(launch_bits_w1_add);
 GOL_LIFE_VARIANT(launch_u8_w1_add);
 
 // Single-generation LDS-tiled byte-layout kernel (life_step_lds.hip).
-void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream);
+void launch_life_step_lds(const BlockArgs& a, int lds_rows, bool wrap, hipStream_t stream);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

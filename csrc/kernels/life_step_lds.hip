@@ -18,6 +18,11 @@
 //     ((S ^ k) + 0x7f7f7f7f) & 0x80808080 (bytes of S ^ k are <= 15).
 //   * The changed flag (next != current over owned cells) is reduced with
 //     __ballot and one plain store per wave.
+//   * Torus wrap in the loads (single rank, width % 32 == 0): staging
+//     chunks and halo rows are read modulo the owned columns and rows, so the
+//     tile has no halo columns, the engine runs one-generation epochs with no
+//     periodic fill launches at all (each was ~5 us per epoch, a sixth of a
+//     generation at 8192^2), and every generation is exactly one launch.
 // It is HBM-bound (1 B read + 1 B write per cell-update); the temporal
 // blocking kernel (life_block_impl.hpp) is the fast path.  This one is kept
 // as the single-step u8 baseline ("8192^2 LDS-tiled u8 kernel")
@@ -55,7 +60,8 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
                                                             uint8_t* __restrict__ out, int64_t pitch,
                                                             int64_t row_lo, int64_t row_hi, int64_t Wc,
                                                             int64_t own_c0, int64_t own_c1,
-                                                            uint32_t* changed, const int64_t* gen_dev) {
+                                                            uint32_t* changed, const int64_t* gen_dev,
+                                                            int64_t wrap_w, int64_t wrap_h, int64_t row0) {
   constexpr int kLdsRows = kTileH + 2;
   constexpr int kRowsPerThread = kTileH / 4;
   __shared__ __attribute__((aligned(16))) uint8_t tile[kLdsRows * kLdsStride];
@@ -75,12 +81,14 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
     const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
     const int64_t gr = r0 - 1 + lr;
     const int64_t gc = c0 - kHaloB + 16 * int64_t(ch);
-    // Unconditional load from a clamped address, zeroed afterwards, so the
-    // loads are not serialised behind branches.
-    const int64_t grc = gr < row_hi + 1 ? gr : row_hi;
-    const int64_t gcc = gc < 0 ? 0 : (gc + 16 <= pitch ? gc : pitch - 16);
+    // Unconditional load from a clamped (or wrapped) address, zeroed
+    // afterwards, so the loads are not serialised behind branches.
+    int64_t grc = gr < row_hi + 1 ? gr : row_hi;
+    int64_t gcc = gc < 0 ? 0 : (gc + 16 <= pitch ? gc : pitch - 16);
+    if (wrap_h) grc = row0 + ((grc - row0) % wrap_h + wrap_h) % wrap_h;  // rows modulo the owned rows
+    if (wrap_w) gcc = (gc % wrap_w + wrap_w) % wrap_w;  // 16-byte chunks modulo the width (% 16 == 0)
+    ok[k] = idx < kChunks && gr < row_hi + 1 && (wrap_w || (gc >= 0 && gc + 16 <= pitch));
     v[k] = *reinterpret_cast<const uint4*>(in + grc * pitch + gcc);
-    ok[k] = idx < kChunks && gr < row_hi + 1 && gc >= 0 && gc + 16 <= pitch;
   }
 #pragma unroll
   for (int k = 0; k < kPerThread; ++k)
@@ -162,7 +170,7 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
 
 }  // namespace
 
-void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream) {
+void launch_life_step_lds(const BlockArgs& a, int lds_rows, bool wrap, hipStream_t stream) {
   const TileGeom& g = a.g;
   GOL_REQUIRE(g.layout == Layout::U8, "life_step_lds: byte layout only");
   GOL_REQUIRE(a.T == 1, "life_step_lds: single-step kernel (T = 1)");
@@ -173,11 +181,18 @@ void launch_life_step_lds(const BlockArgs& a, int lds_rows, hipStream_t stream) 
   uint32_t* changed = a.changed ? a.changed + (a.gen_dev ? a.gen_rel : a.gen_base + 1 - a.flags_base) : nullptr;
   const int64_t* gen_dev = a.changed ? a.gen_dev : nullptr;
   const int th = lds_rows == 32 ? 32 : 64;
+  // Torus wrap: whole-width tile without halo columns (and, with wrap_rows,
+  // the whole torus: owned rows read modulo H).
+  const int64_t wrap_w = wrap && a.full_width && g.hw == 0 && g.W % 16 == 0 ? g.W : 0;
+  const int64_t wrap_h = wrap_w && a.wrap_rows ? g.H : 0;
+  GOL_REQUIRE(!a.wrap_rows || wrap_h, "life_step_lds: row wrap needs a whole-width tile without halo columns");
+  GOL_REQUIRE(wrap_w || g.hw > 0, "life_step_lds: a tile without halo columns needs column wrap");
   GOL_REQUIRE(ceil_div(rows, int64_t(th)) < (int64_t(1) << 31), "life_step_lds: too many rows");
   const dim3 grid(unsigned(ceil_div(g.Wc(), int64_t(kTileW))), unsigned(ceil_div(rows, int64_t(th))));
   auto k = th == 32 ? life_step_lds_kernel<32> : life_step_lds_kernel<64>;
   hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
-                     g.pitch, a.row_lo, a.row_hi, g.Wc(), g.cell0(), g.cell0() + g.W, changed, gen_dev);
+                     g.pitch, a.row_lo, a.row_hi, g.Wc(), g.cell0(), g.cell0() + g.W, changed, gen_dev, wrap_w,
+                     wrap_h, g.row0());
 }
 
 }  // namespace hipk

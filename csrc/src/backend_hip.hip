@@ -490,7 +490,9 @@ class HipBackend final : public Backend {
   int64_t min_block_rows(Layout l, int T) const override {
     return l == Layout::U8 && T > 32 ? int64_t(4) * (2 * T + 2) + T - 1 : 1;
   }
-  bool wraps_columns(Layout l) const override { return tune_.wrap && !(l == Layout::U8 && tune_.u8_lds); }
+  bool wraps_columns(Layout l) const override { return tune_.wrap; }
+  // The single-step LDS kernel reads rows modulo the torus too (T = 1).
+  bool wraps_rows(Layout l) const override { return tune_.wrap && l == Layout::U8 && tune_.u8_lds; }
   void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override {
     GOL_ON_DEVICE();
     hipk::launch_rotate_cols(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), g, shift, stream_);

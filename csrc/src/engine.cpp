@@ -80,6 +80,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // Whole-width tiles on a backend that wraps column reads (lane_cols in the
   // HIP kernels) never read their halo columns: no column fills.
   cols_filled_ = !(dec_.Px == 1 && cfg_.W % 32 == 0 && be_->wraps_columns(cfg_.layout));
+  // A single-rank torus on a backend that also wraps row reads (the T = 1
+  // LDS kernel): one-generation epochs over the owned rows, no fills at all.
+  rows_wrapped_ = !cols_filled_ && dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && tmax_ == 1 &&
+                  be_->wraps_rows(cfg_.layout);
+  if (rows_wrapped_) D_ = 1;
   // Halo columns: none when the kernels wrap (smaller rows to exchange and
   // fill); else D cells per side, 2D on the left for the drifting window.
   int hw = cols_filled_ ? int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32)) : 0;
@@ -268,6 +273,10 @@ void Engine::halo_exchange() {
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
   const int64_t H = g_.H, pitch = g_.pitch;
+  if (rows_wrapped_) {  // the kernels read the torus modulo its rows and columns
+    ++exchanges_;
+    return;
+  }
   if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange) {  // one rank: both periodic fills, one launch
     void* t = phase_begin(nullptr);
     be_->fill_periodic(buf, g_, /*cols=*/cols_filled_, /*rows=*/true);
@@ -500,6 +509,7 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   a.flags_base = flags_base_;
   a.allow_drift = drift_ok_;
   a.full_width = dec_.Px == 1 && cfg_.W % 32 == 0;
+  a.wrap_rows = rows_wrapped_;
   a.stream = stream;
   a.dual_offset = dual_offset;
   a.prio_boost = prio_boost;

@@ -389,10 +389,13 @@ def test_grouped_schedule_is_the_default(gpu):
     assert "group=8" in sim.describe()["backend"]
 
 
-@pytest.mark.parametrize("W,H", [(1, 1), (5, 3), (100, 70), (1023, 65), (1025, 200), (3000, 129)])
+@pytest.mark.parametrize("W,H", [(1, 1), (5, 3), (100, 70), (1023, 65), (1025, 200), (3000, 129), (32, 40),
+                                 (2048, 333), (3072, 97), (8192, 130)])
 @pytest.mark.parametrize("lds_rows", [32, 64])
 def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H, lds_rows):
-    """The LDS-tiled single-step byte kernel (GOL_U8_KERNEL=lds, T = 1)."""
+    """The LDS-tiled single-step byte kernel (GOL_U8_KERNEL=lds, T = 1); widths
+    that are multiples of 32 run the torus-wrap loads (no halo columns, no
+    fills: one launch per generation)."""
     monkeypatch.setenv("GOL_U8_KERNEL", "lds")
     monkeypatch.setenv("GOL_LDS_ROWS", str(lds_rows))
     g = random_grid(W, H, W ^ H)
@@ -400,6 +403,20 @@ def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H, lds_rows):
     assert (life_step(g, 9, engine="hip", layout="u8") == want).all()
     sim = Simulation(LifeConfig(W, H, layout="u8"), engine="hip")
     assert "lds" in sim.describe()["backend"] and sim.describe()["tmax"] == 1
+
+
+@pytest.mark.parametrize("spec,P", [("1x2", 2), ("2x1", 2), ("2x2", 4)])
+def test_u8_lds_kernel_multi_subdomain(gpu, monkeypatch, spec, P):
+    """LDS kernel with row exchanges (column wrap on 1xN strips) and column
+    exchanges (halo columns), several subdomains on one GPU."""
+    monkeypatch.setenv("GOL_U8_KERNEL", "lds")
+    W, H = 32 * 40, 210
+    g = random_grid(W, H, 8)
+    want = life_step_torch(g, 40, device="cuda")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=40, layout="u8", decomp=spec), P, engine="hip", devices=[0])
+    grp.load(g)
+    grp.advance(40)
+    assert (grp.gather() == want).all()
 
 
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
