@@ -89,6 +89,16 @@ struct ChainSaver {
 // earlier, and its wave 0 publishes right after its prologue, before it waits
 // on anything.  Bounded (~0.1 s): giving up raises the launch's error word
 // (Backend::check_device_errors) instead of hanging the GPU.
+//
+// Memory model (cdna_hip_programming.md §6 Guideline 16, "Valid forms"):
+// the producer stores every payload word sc1 (ChainSaver), drains them
+// (s_waitcnt vmcnt(0)) and only then one lane stores the flag with an
+// agent-scope atomic; the consumer polls that word relaxed at agent scope and
+// reads every payload word with an sc1 buffer load to registers (which
+// bypasses this CU's L1), so no agent-scope acquire (L1 invalidate) is
+// needed; the wavefront-scope acquire keeps the compiler from moving the
+// loads above the poll.  (An LDS-DMA copy, global_load_lds, would not
+// qualify: it is not a load to registers.)
 template <int T, int W>
 __device__ __forceinline__ void chain_fetch(const LifeBlockParams& p, int64_t slot_below, int64_t flag_below,
                                             uint32_t* lds_slot, int lane) {
@@ -102,12 +112,21 @@ __device__ __forceinline__ void chain_fetch(const LifeBlockParams& p, int64_t sl
     __builtin_amdgcn_s_sleep(2);
   }
   if (!arrived && p.err && lane == 0) __hip_atomic_store(p.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  // LDS-DMA (global_load_lds, sc1): all rows in flight at once, no VGPRs.
-  const uint32_t* src = p.chain_buf + slot_below;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const BufRsrc src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p.chain_buf + slot_below), short(0),
+                                                        kRows * 64 * 4, kBufFlags);
+  // Eight rows in flight per batch (8 VGPRs), sc1 loads to registers, then LDS.
+  constexpr int kBatch = 8;
 #pragma unroll 1
-  for (int r = 0; r < kRows; ++r)
-    __builtin_amdgcn_global_load_lds(src + r * 64 + lane, lds_slot + r * 64, 4, 0, kCpolSc1);
-  __builtin_amdgcn_s_waitcnt(0);
+  for (int r0 = 0; r0 < kRows; r0 += kBatch) {
+    uint32_t v[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j)
+      v[j] = r0 + j < kRows ? __builtin_amdgcn_raw_buffer_load_b32(src, ((r0 + j) * 64 + lane) * 4, 0, kCpolSc1) : 0u;
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j)
+      if (r0 + j < kRows) lds_slot[(r0 + j) * 64 + lane] = v[j];
+  }
 }
 
 #ifndef GOL_PRIO_BUCKETS

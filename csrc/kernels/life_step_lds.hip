@@ -85,9 +85,14 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
     // afterwards, so the loads are not serialised behind branches.
     int64_t grc = gr < row_hi + 1 ? gr : row_hi;
     int64_t gcc = gc < 0 ? 0 : (gc + 16 <= pitch ? gc : pitch - 16);
-    if (wrap_h) grc = row0 + ((grc - row0) % wrap_h + wrap_h) % wrap_h;  // rows modulo the owned rows
-    if (wrap_w) gcc = (gc % wrap_w + wrap_w) % wrap_w;  // 16-byte chunks modulo the width (% 16 == 0)
-    ok[k] = idx < kChunks && gr < row_hi + 1 && (wrap_w || (gc >= 0 && gc + 16 <= pitch));
+    // Wrap: a staged row or chunk is at most one halo row / chunk outside the
+    // owned range, so one conditional add or subtract (no 64-bit modulo).
+    if (wrap_h) grc = grc < row0 ? grc + wrap_h : grc >= row0 + wrap_h ? grc - wrap_h : grc;  // owned rows
+    // 16-byte chunks (W % 16 == 0); chunks two widths out (narrow tiles) only
+    // neighbour unstored cells: clamped into the row and zeroed.
+    if (wrap_w) gcc = min(gc < 0 ? gc + wrap_w : gc >= wrap_w ? gc - wrap_w : gc, pitch - 16);
+    ok[k] = idx < kChunks && gr < row_hi + 1 &&
+            (wrap_w ? gc >= -wrap_w && gc < 2 * wrap_w : gc >= 0 && gc + 16 <= pitch);
     v[k] = *reinterpret_cast<const uint4*>(in + grc * pitch + gcc);
   }
 #pragma unroll
