@@ -84,6 +84,11 @@ class Backend {
   virtual void* timing_mark(void* stream) = 0;
   virtual double timing_ms(void* a, void* b) = 0;
   virtual void timing_release(void* mark) = 0;
+  // Linked launches (HIP, GOL_LINK): work on the backend's second compute
+  // stream precedes what comes next on its compute stream.  The engine calls
+  // it before enqueueing transport operations on stream() itself.
+  virtual void join_streams() {}
+  virtual int64_t linked_launches() const { return 0; }
   // Makes this backend's device current for the calling thread (rank
   // threads of single-process multi-GPU runs call it first).
   virtual void bind_thread() {}

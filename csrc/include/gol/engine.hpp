@@ -92,6 +92,7 @@ struct RunResult {
   bool overlapped = false;       // epochs ran with the overlapped halo exchange
   int64_t graph_launches = 0;    // epochs replayed from a captured HIP graph
   int64_t halo_bytes = 0;        // bytes this rank sent in halo exchanges
+  int64_t linked_launches = 0;   // launches that overlapped the previous one (GOL_LINK)
   // Per-phase device time of this run (Engine::set_phase_timing; SURVEY
   // 5.1/5.5): temporal-block kernels, halo exchanges (pack / send / recv /
   // unpack), periodic halo fills, termination-flag reductions (all-reduce +

@@ -66,6 +66,9 @@ struct Vec {
 using BufRsrc = __amdgpu_buffer_rsrc_t;
 using U32x4 = uint32_t __attribute__((ext_vector_type(4)));
 constexpr int kBufFlags = 0x00020000;
+// Cache policy aux bits of a buffer access: sc1 = device scope (written
+// through to the device-coherent level; loads bypass this CU's L1).
+constexpr int kCpolSc1 = 16;
 
 // Words of the neighbouring lanes: lane i gets lane i-1's last word (left)
 // and lane i+1's first word (right).  Edge lanes receive don't-care values;
@@ -264,6 +267,7 @@ template <int W_, int XL_>
 struct BitsIO {
   static constexpr int W = W_, XL = XL_;
   static constexpr int kHalo = 1;  // halo lanes per wave side
+  static constexpr bool kLinked = false;  // Sc1IO
   static constexpr bool kBits = true;
   struct Raw {
     uint32_t w[W];
@@ -304,6 +308,7 @@ template <int W_, int XL_, int HALO_ = 1>
 struct U8IO {
   static constexpr int W = W_, XL = XL_;
   static constexpr int kHalo = HALO_;  // halo lanes per wave side (2: passes deeper than 32)
+  static constexpr bool kLinked = false;  // Sc1IO
   static constexpr bool kBits = false;
   struct Raw {
     uint4 q[2 * W];
@@ -358,6 +363,29 @@ struct U8IO {
     const U32x4 b = {spread(w, 4), spread(w, 5), spread(w, 6), spread(w, 7)};
     __builtin_amdgcn_raw_buffer_store_b128(a, row, voff, 0, GOL_U8_STORE_CPOL);
     __builtin_amdgcn_raw_buffer_store_b128(b, row, voff + 16, 0, GOL_U8_STORE_CPOL);
+  }
+};
+
+// Storage layout of a linked launch (LifeBlockParams::link_flag): rows are
+// handed between launches that run at the same time, so every row store is
+// written through (sc1) and every row load is an sc1 load to registers, the
+// form that needs no agent-scope acquire on the consumer
+// (cdna_hip_programming.md §6 Guideline 16, "Valid forms").
+template <class IO>
+struct Sc1IO : IO {
+  using Raw = typename IO::Raw;
+  static constexpr int W = IO::W;
+  static constexpr bool kLinked = true;
+  __device__ static __forceinline__ Raw load_raw(const uint8_t* row, const int (&off)[W]) {
+    static_assert(IO::kBits, "linked launches: bit layout");
+    Raw r;
+    const BufRsrc rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), short(0), 0x7FFFFFFF, kBufFlags);
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, off[i] * 4, 0, kCpolSc1);
+    return r;
+  }
+  __device__ static __forceinline__ void store_buf(BufRsrc row, int voff, uint32_t w) {
+    __builtin_amdgcn_raw_buffer_store_b32(w, row, voff, 0, kCpolSc1);
   }
 };
 

@@ -23,6 +23,69 @@ namespace lb {
 // a segment's S*T level-rows.
 constexpr int kSplitMaxRowsPerT = 8;
 
+// Linked launch of the grouped kernel (LifeBlockParams::link_*): returns
+// false (nothing launched) when the launch cannot be planned that way.  The
+// first launch of a chain goes on stream[0] (the caller's `s`); a launch that
+// reads the previous one's output and fits beside it goes on the other
+// stream, after an event recorded just before the previous launch (so it
+// starts no earlier than that one), and waits for its input rows group by
+// group.
+template <int T, class IO>
+bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const LifeTuning& tune, hipStream_t s) {
+  using LIO = Sc1IO<IO>;
+  constexpr int M = 8;
+  LinkState& L = *tune.link;
+  if (s != L.stream[0]) return false;
+  LifeBlockParams q = p0;
+  q.fold = 1;
+  q.fold_lanes = 64;
+  if (plan_group<T, M>(q, out_rows, simds, group_waves_per_simd<T, LIO, M>(), tune.target_waves, IO::XL) <= 0)
+    return false;
+  const int64_t blocks = int64_t(q.ncolw) * q.nseg;
+  static const int per_cu = occupancy_blocks(life_group_kernel<T, LIO, M>, 64 * M);
+  const int64_t cap = int64_t(std::max(1, tune.cus)) * per_cu;
+  const bool link = L.prev_valid && L.prev_out == q.in && L.prev.ncolw == q.ncolw && L.prev.wrap_w == q.wrap_w &&
+                    L.prev.pitch == q.pitch && L.prev_blocks + blocks <= cap;
+  // Completion words of this launch: the third buffer back, so neither the
+  // previous launch's words (read by this one) nor the ones before it (read by
+  // the previous launch, which may still run) are overwritten.
+  const size_t need = size_t(blocks);
+  if (L.flag_words < need) {
+    if (!tune.chain_mem) return false;
+    for (int i = 0; i < 3; ++i) L.flags[i] = tune.chain_mem(2 + i, need * 4);
+    L.flag_words = need;
+    L.prev_valid = false;
+    if (link) return false;  // the buffers moved under the previous launch: start a new chain
+  }
+  if (++L.seq == 0) L.seq = 1;
+  q.link_flag = L.flags[L.seq % 3];
+  q.link_seq = L.seq;
+  hipStream_t st = L.stream[0];
+  int which = 0;
+  if (link) {
+    which = 1 - L.cur;
+    st = L.stream[which];
+    q.link_prev_flag = L.prev.link_flag;
+    q.link_prev_seq = L.prev.link_seq;
+    q.link_prev_row_lo = L.prev.row_lo;
+    q.link_prev_nseg = L.prev.nseg;
+    q.link_prev_seg_rows = L.prev.seg_rows;
+    q.link_prev_seg_rem = L.prev.seg_rem;
+    (void)hipStreamWaitEvent(st, L.before[L.cur], 0);
+    ++L.linked;
+  } else {
+    link_join(L);
+  }
+  (void)hipEventRecord(L.before[which], st);
+  hipLaunchKernelGGL((life_group_kernel<T, LIO, M>), dim3(unsigned(blocks)), dim3(64 * M), 0, st, q);
+  L.cur = which;
+  L.prev = q;
+  L.prev_out = q.out;
+  L.prev_blocks = blocks;
+  L.prev_valid = true;
+  return true;
+}
+
 template <int T, class IO>
 void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
   constexpr int kWaveOut = wave_out_words<IO::XL, IO::W>();
@@ -47,6 +110,18 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
     }
   }
   const int simds = 4 * std::max(1, tune.cus) / dual;
+  // Linked launches (GOL_LINK): this launch starts while the previous one
+  // still runs, on the other stream, when both fit on the GPU at once (small
+  // tiles, whose launches alone hold 2 waves per SIMD).  Any other launch
+  // first joins the two streams.
+  if (tune.link) {
+    if constexpr (IO::kBits && IO::W == 1 && (T == 8 || T == 12 || T == 16) &&
+                  (IO::XL == kXlaneDpp || IO::XL == kXlaneAdd)) {
+      if (tune.group != 0 && tune.split == 0 && !tune.skew && dual == 1 && launch_linked<T, IO>(p, out_rows, simds, tune, s))
+        return;
+    }
+    link_join(*tune.link);
+  }
   if constexpr (T >= 4) {
     if (tune.group != 0 && (tune.split == 0 || dual == 2) && !tune.skew) {
       // M = 4 or 8 waves per workgroup; auto (-1) takes the cheapest of

@@ -63,9 +63,9 @@ struct LdsSaver {
 // (LifeBlockParams::chain_buf) wave 0 also stores its rows to the group's
 // global slot through `pub`, whose num_records is 0 for every
 // other wave, so their copies are dropped by the range check without a branch
-// in the unrolled prologue.  sc1: written through to the device-coherent level
-// (the reading group may run on another XCD, behind another L2).
-constexpr int kCpolSc1 = 16;
+// in the unrolled prologue.  sc1 (kCpolSc1): written through to the
+// device-coherent level (the reading group may run on another XCD, behind
+// another L2).
 template <int T, int W>
 struct ChainSaver {
   uint32_t* slot;
@@ -127,6 +127,43 @@ __device__ __forceinline__ void chain_fetch(const LifeBlockParams& p, int64_t sl
     for (int j = 0; j < kBatch; ++j)
       if (r0 + j < kRows) lds_slot[(r0 + j) * 64 + lane] = v[j];
   }
+}
+
+// Linked launches (LifeBlockParams::link_prev_flag): wave 0 of a group
+// waits, one flag per lane, until every group of the previous launch whose
+// output rows [r0, r1) this group reads has published, in its own strip and
+// the strips beside it (modulo the strip count in wrap mode, clipped in halo
+// mode).  The previous launch's groups were all dispatched before or beside
+// this one (the backend links two launches only when both fit on the GPU at
+// once), so the wait ends; bounded (~0.1 s) like chain_fetch, it raises the
+// error word 3 instead of hanging.
+__device__ __forceinline__ void link_wait(const LifeBlockParams& p, int kcol, int64_t r0, int64_t r1, int lane) {
+  const int q1 = p.link_prev_seg_rows + 1;
+  const int64_t big = int64_t(p.link_prev_seg_rem) * q1;
+  const auto grp_of = [&](int64_t r) {
+    const int64_t x = max<int64_t>(0, r - p.link_prev_row_lo);
+    const int64_t g = x < big ? x / q1 : p.link_prev_seg_rem + (x - big) / max(1, p.link_prev_seg_rows);
+    return int(min<int64_t>(g, p.link_prev_nseg - 1));
+  };
+  const int g0 = grp_of(r0), g1 = grp_of(r1 - 1);
+  const int ng = g1 - g0 + 1;
+  const int nflags = 3 * ng;
+  for (int base = 0; base < nflags; base += 64) {
+    const int f = base + lane;
+    int k = kcol + f / ng - 1;
+    if (p.wrap_w > 0) k = (k + p.ncolw) % p.ncolw;
+    const bool mine = f < nflags && k >= 0 && k < p.ncolw;
+    const uint32_t* w = p.link_prev_flag + (int64_t(mine ? k : 0) * p.link_prev_nseg + g0 + (mine ? f % ng : 0));
+    bool done = !mine;
+    for (int spin = 0; spin < (1 << 16); ++spin) {
+      if (!done) done = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.link_prev_seq;
+      if (__all(done)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!__all(done) && p.err && lane == 0) __hip_atomic_store(p.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // No load of the previous launch's rows may move above the wait.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 #ifndef GOL_PRIO_BUCKETS
@@ -341,6 +378,10 @@ void life_group_kernel(const LifeBlockParams p) {
     }
   }
 
+  if constexpr (IO::kLinked) {  // wait for the previous launch's rows this group reads
+    if (p.link_prev_flag && m == 0) link_wait(p, kcol, G0 - T, G1 + T, lane);
+    __syncthreads();
+  }
   rd.base = p.in + in0 * pitch;  // input row of step k: in0 + k
   rd.pitch = pitch;
   rd.kmax = last ? kend - 1 : kmain + 1;
@@ -397,6 +438,13 @@ void life_group_kernel(const LifeBlockParams p) {
     }
     uint32_t* ch = p.gen_dev ? p.changed + (*p.gen_dev + p.gen_rel) : p.changed;
     if (lane < T && ((mask >> lane) & 1u)) ch[lane] = 1u;
+  }
+  if constexpr (IO::kLinked) {  // every wave's rows are written through, then one flag
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (p.link_flag && m == 0 && lane == 0)
+      __hip_atomic_store(p.link_flag + (int64_t(kcol) * p.nseg + grp), p.link_seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
   if (p.wg_trace) wg_trace_record(p.wg_trace, M, m, lane, t_start);
 }

@@ -65,6 +65,20 @@ struct LifeBlockParams {
   uint32_t* chain_flag;
   uint32_t chain_seq;
   int64_t chain_end;
+  // Linked launches (LifeTuning::link, life_group_kernel<..., LINK = true>):
+  // this launch may run while the previous grouped launch, whose output is
+  // its input, still runs.  Group (kcol, grp) first waits until every group
+  // of that launch whose output rows it reads (its strip and the two beside
+  // it) has published link_prev_flag[strip * link_prev_nseg + group] ==
+  // link_prev_seq, and after its last store publishes link_flag[kcol * nseg
+  // + grp] = link_seq.  Payload stores and input loads are sc1 (the no-
+  // acquire valid form of cdna_hip_programming.md Guideline 16).
+  uint32_t* link_flag;             // null: not a linked launch
+  uint32_t link_seq;
+  const uint32_t* link_prev_flag;  // null: nothing to wait for
+  uint32_t link_prev_seq;
+  int64_t link_prev_row_lo;
+  int link_prev_nseg, link_prev_seg_rows, link_prev_seg_rem;
 };
 
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
@@ -83,6 +97,34 @@ constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
 //   (HipBackend::choose_kernel: whole-width tiles that fill four waves per
 //   SIMD at T = 12), the DPP window everywhere else.
 enum Xlane : int { kXlaneAuto = -1, kXlaneDpp = 0, kXlaneBpermute = 1, kXlaneCarry = 2, kXlaneAdd = 3 };
+
+// Backend-owned state of linked launches (GOL_LINK; LifeBlockParams::link_*):
+// consecutive grouped launches of an epoch alternate between two streams and
+// overlap, ordered by per-group completion words instead of the stream.
+struct LinkState {
+  hipStream_t stream[2] = {nullptr, nullptr};  // [0] = the backend's compute stream
+  hipEvent_t before[2] = {nullptr, nullptr};   // recorded on stream[i] just before its last launch
+  int cur = 0;                                  // stream of the last launch
+  bool prev_valid = false;                      // the last launch may be linked to
+  const void* prev_out = nullptr;               // its output buffer
+  int64_t prev_blocks = 0;                      // its workgroups
+  LifeBlockParams prev{};                       // its plan and completion words
+  uint32_t* flags[3] = {nullptr, nullptr, nullptr};  // completion words, rotating per launch
+  size_t flag_words = 0;
+  uint32_t seq = 0;
+  int64_t linked = 0;                           // launches that ran linked (diagnostics)
+};
+
+// Everything enqueued on stream[1] precedes what comes next on stream[0];
+// the next launch starts a new chain.
+inline void link_join(LinkState& L) {
+  if (L.cur != 0) {
+    (void)hipEventRecord(L.before[1], L.stream[1]);
+    (void)hipStreamWaitEvent(L.stream[0], L.before[1], 0);
+    L.cur = 0;
+  }
+  L.prev_valid = false;
+}
 
 struct LifeTuning {
   int cus = 256;            // compute units of the device
@@ -106,6 +148,7 @@ struct LifeTuning {
   // ordered like `scratch`: which = 0 the chain flags (zeroed when allocated),
   // 1 the chain slots.
   std::function<uint32_t*(int which, size_t n)> chain_mem;
+  LinkState* link = nullptr;     // linked launches on (null: every launch on the given stream)
   uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
   uint32_t* err = nullptr;       // LifeBlockParams::err
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).

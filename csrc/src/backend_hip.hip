@@ -76,21 +76,33 @@ class HipBackend final : public Backend {
     tune_.fold = env_int("GOL_FOLD", 1) != 0;
     chain_mode_ = env_int("GOL_CHAIN", -1);
     u8_pipe_ = env_int("GOL_U8_PIPE", 1) != 0;
+    // Linked launches: consecutive grouped launches of an epoch overlap on
+    // two streams, ordered by per-group completion words (LifeBlockParams::
+    // link_*): small tiles whose launches alone hold only 2 waves per SIMD.
+    link_on_ = env_int("GOL_LINK", 0) != 0;
+    if (link_on_) {
+      link_.stream[0] = stream_;
+      HIP_CHECK(hipStreamCreateWithFlags(&link_.stream[1], hipStreamNonBlocking));
+      for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
     tune_log_ = env_int("GOL_TUNE_LOG", 0) != 0;
     tune_.chain_seq = &chain_seq_;
+    // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words
+    // (zeroed when allocated: flags and words are compared with sequence numbers).
     tune_.chain_mem = [this](int which, size_t n) -> uint32_t* {
-      void*& buf = chain_[which & 1];
-      size_t& cap = chain_bytes_[which & 1];
+      void*& buf = chain_[which];
+      size_t& cap = chain_bytes_[which];
       if (n > cap) {
         GOL_ON_DEVICE();
         HIP_CHECK(hipStreamSynchronize(stream_));  // earlier launches may still use it
+        if (link_.stream[1]) HIP_CHECK(hipStreamSynchronize(link_.stream[1]));
         if (buf) HIP_CHECK(hipFree(buf));
         HIP_CHECK(hipMalloc(&buf, n));
-        if (which == 0) HIP_CHECK(hipMemsetAsync(buf, 0, n, stream_));
+        if (which != 1) HIP_CHECK(hipMemset(buf, 0, n));
         cap = n;
       }
-      if (check_dev_) check_ptr(buf, which == 0 ? "chain flags" : "chain slots");
+      if (check_dev_) check_ptr(buf, which == 0 ? "chain flags" : which == 1 ? "chain slots" : "link words");
       return static_cast<uint32_t*>(buf);
     };
     if (const char* t = std::getenv("GOL_WG_TRACE")) {
@@ -120,6 +132,7 @@ class HipBackend final : public Backend {
   }
   ~HipBackend() override {
     DeviceScope device_scope(dev_);
+    if (link_.stream[1]) hipStreamSynchronize(link_.stream[1]);
     if (stream_) hipStreamSynchronize(stream_);
     if (comm_) hipStreamSynchronize(comm_);
     if (stage_) hipFree(stage_);
@@ -136,9 +149,21 @@ class HipBackend final : public Backend {
     for (auto& e : marks_)
       if (e) hipEventDestroy(e);
     if (comm_) hipStreamDestroy(comm_);
+    for (auto& e : link_.before)
+      if (e) hipEventDestroy(e);
+    if (link_.stream[1]) hipStreamDestroy(link_.stream[1]);
     if (stream_) hipStreamDestroy(stream_);
   }
 
+  // Linked launches: everything on the second stream precedes what comes
+  // next on the compute stream (every entry point but a linkable run_block).
+  void join_streams() override {
+    if (link_on_) {
+      DeviceScope device_scope(dev_);
+      hipk::link_join(link_);
+    }
+  }
+  int64_t linked_launches() const override { return link_.linked; }
   std::string name() const override {
     hipk::LifeTuning t = tune_;
     t.chain = chain_mode_;
@@ -151,6 +176,7 @@ class HipBackend final : public Backend {
   void* stream() const override { return stream_; }
 
   void* alloc(size_t bytes) override {
+    join_streams();
     GOL_ON_DEVICE();
     void* p = nullptr;
     HIP_CHECK(hipMalloc(&p, bytes ? bytes : 1));
@@ -161,6 +187,7 @@ class HipBackend final : public Backend {
   }
   void release(void* p) override {
     if (!p) return;
+    join_streams();
     DeviceScope device_scope(dev_);
     hipStreamSynchronize(stream_);
     hipFree(p);
@@ -176,24 +203,29 @@ class HipBackend final : public Backend {
     if (p) hipHostFree(p);
   }
   void memset_async(void* p, int v, size_t bytes) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipMemsetAsync(p, v, bytes, stream_));
   }
   void copy_h2d(void* d, const void* s, size_t n) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
   void copy_d2h(void* d, const void* s, size_t n) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
   void copy_d2h_async(void* d, const void* s, size_t n) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
   }
   void copy_d2h_async_on(void* d, const void* s, size_t n, void* stream) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream ? static_cast<hipStream_t>(stream) : stream_));
   }
@@ -205,15 +237,18 @@ class HipBackend final : public Backend {
                                hipMemcpyDefault, stream_));
   }
   void synchronize() override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
   void synchronize_stream(void* s) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipStreamSynchronize(s ? static_cast<hipStream_t>(s) : stream_));
   }
   void* event_record() override { return event_record_on(nullptr); }
   void* event_record_on(void* stream) override {
+    join_streams();
     GOL_ON_DEVICE();
     hipEvent_t e;
     HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -237,6 +272,7 @@ class HipBackend final : public Backend {
   }
   // Phase timing: timing-enabled events from a pool.
   void* timing_mark(void* stream) override {
+    join_streams();
     GOL_ON_DEVICE();
     hipEvent_t e;
     if (timing_pool_.empty()) {
@@ -279,6 +315,7 @@ class HipBackend final : public Backend {
   }
   bool supports_graphs() const override { return tune_.split == 0; }  // split allocates scratch lazily
   void capture_begin() override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   }
@@ -292,6 +329,7 @@ class HipBackend final : public Backend {
     return exec;
   }
   void graph_launch(void* g) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipGraphLaunch(static_cast<hipGraphExec_t>(g), stream_));
   }
@@ -300,6 +338,7 @@ class HipBackend final : public Backend {
     if (g) hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
   }
   void i64_async(int64_t* dev, int64_t v, bool add) override {
+    join_streams();
     GOL_ON_DEVICE();
     hipk::launch_i64(dev, v, add, stream_);
     HIP_CHECK(hipGetLastError());
@@ -322,6 +361,7 @@ class HipBackend final : public Backend {
   // Marks come from a small ring of reusable timing-free events: a mark is
   // only waited on by the next few operations of an epoch.
   void* stream_mark(void* from) override {
+    join_streams();
     GOL_ON_DEVICE();
     hipEvent_t& e = marks_[mark_next_++ % marks_.size()];
     if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -329,6 +369,7 @@ class HipBackend final : public Backend {
     return e;
   }
   void stream_wait(void* on, void* mark) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipStreamWaitEvent(on ? static_cast<hipStream_t>(on) : stream_, static_cast<hipEvent_t>(mark), 0));
   }
@@ -339,16 +380,26 @@ class HipBackend final : public Backend {
       check_ptr(a.in, "run_block input");
       check_ptr(a.out, "run_block output");
     }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(stream_, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+    // A launch may join a linked chain only on the compute stream, outside a
+    // capture, for one row range of the bit layout; anything else first joins.
+    const bool linkable = link_on_ && !a.stream && !capturing && a.dual_offset == 0 && a.g.layout == Layout::Bits;
+    if (!linkable) join_streams();
+    tune_.link = linkable ? &link_ : nullptr;
     if (chain_mode_) {  // chained groups: own stream only, never inside a graph capture
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      tune_.chain_ok = (!a.stream || a.stream == stream_) && hipStreamIsCapturing(stream_, &cs) == hipSuccess &&
-                       cs == hipStreamCaptureStatusNone;
+      tune_.chain_ok = (!a.stream || a.stream == stream_) && !capturing && !linkable;
     }
-    if (trace_at_ >= 0 && launches_ == trace_at_) return run_block_traced(a);
+    if (trace_at_ >= 0 && launches_ == trace_at_) {
+      join_streams();
+      tune_.link = nullptr;
+      return run_block_traced(a);
+    }
     ++launches_;
     hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
     Pending* timed = nullptr;
-    if (chain_mode_ < 0) timed = autotune_chain(a);
+    if (chain_mode_ < 0 && !linkable) timed = autotune_chain(a);
+    if (linkable) tune_.chain = 0;
     if (timed) HIP_CHECK(hipEventRecord(timed->e0, s));
     const int drift = hipk::launch_life_block(a, tune_, s);
     HIP_CHECK(hipGetLastError());
@@ -494,6 +545,7 @@ class HipBackend final : public Backend {
   // The single-step LDS kernel reads rows modulo the torus too (T = 1).
   bool wraps_rows(Layout l) const override { return tune_.wrap && l == Layout::U8 && tune_.u8_lds; }
   void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override {
+    join_streams();
     GOL_ON_DEVICE();
     hipk::launch_rotate_cols(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), g, shift, stream_);
     HIP_CHECK(hipGetLastError());
@@ -534,12 +586,15 @@ class HipBackend final : public Backend {
     const uint32_t e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
     if (e != 0) {
       *err_host_ = 0;
-      fail(std::string(e == 2 ? "life_group kernel (chained groups): a wave gave up waiting for the group below"
-                              : "life_short kernel: a wave gave up waiting for its neighbour's LDS rows") +
+      fail(std::string(e == 2   ? "life_group kernel (chained groups): a wave gave up waiting for the group below"
+                       : e == 3 ? "life_group kernel (linked launches): a group gave up waiting for the previous "
+                                  "launch's rows"
+                                : "life_short kernel: a wave gave up waiting for its neighbour's LDS rows") +
            " (device error word " + std::to_string(e) + "); the rows of that launch are invalid");
     }
   }
   void fill_periodic(void* buf, const TileGeom& g, bool cols, bool rows) override {
+    join_streams();
     GOL_ON_DEVICE();
     auto* p = static_cast<uint8_t*>(buf);
     if (!(cols && rows && hipk::launch_fill_all(p, g, stream_))) {
@@ -549,17 +604,20 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGetLastError());
   }
   void fill_cols_rows(void* buf, const TileGeom& g, int64_t r0, int64_t n, void* stream) override {
+    join_streams();
     GOL_ON_DEVICE();
     hipk::launch_fill_cols_rows(static_cast<uint8_t*>(buf), g, r0, n, stream ? static_cast<hipStream_t>(stream) : stream_);
     HIP_CHECK(hipGetLastError());
   }
   void alive_any(const void* buf, const TileGeom& g, uint32_t* flag) override {
+    join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipMemsetAsync(flag, 0, 4, stream_));
     hipk::launch_alive(static_cast<const uint8_t*>(buf), g, flag, nullptr, stream_);
     HIP_CHECK(hipGetLastError());
   }
   int64_t alive_count(const void* buf, const TileGeom& g) override {
+    join_streams();
     GOL_ON_DEVICE();
     unsigned long long* d = nullptr;
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d), 8, stream_));
@@ -576,6 +634,7 @@ class HipBackend final : public Backend {
   // Host <-> tile transfers go through a bounded device staging buffer so a
   // 32768^2 (1 GiB) or larger grid never needs a second full-size copy.
   void load_owned(void* buf, const TileGeom& g, const uint8_t* cells, int64_t ld) override {
+    join_streams();
     GOL_ON_DEVICE();
     const int64_t chunk = rows_per_chunk(g);
     uint8_t* stage = static_cast<uint8_t*>(stage_buf(chunk * g.W));
@@ -589,6 +648,7 @@ class HipBackend final : public Backend {
     }
   }
   void store_owned(const void* buf, const TileGeom& g, uint8_t* cells, int64_t ld, bool ascii) override {
+    join_streams();
     GOL_ON_DEVICE();
     const int64_t chunk = rows_per_chunk(g);
     uint8_t* stage = static_cast<uint8_t*>(stage_buf(chunk * g.W));
@@ -603,6 +663,7 @@ class HipBackend final : public Backend {
   }
   void init_random(void* buf, const TileGeom& g, uint64_t seed, double density, int64_t grow0,
                    int64_t gcol0) override {
+    join_streams();
     GOL_ON_DEVICE();
     hipk::launch_init_random(static_cast<uint8_t*>(buf), g, seed, density_thresh(density), grow0, gcol0,
                              stream_);
@@ -650,8 +711,10 @@ class HipBackend final : public Backend {
   hipStream_t comm_ = nullptr;
   void* scratch_ = nullptr;  // split-schedule boundary states
   size_t scratch_bytes_ = 0;
-  void* chain_[2] = {nullptr, nullptr};  // chained groups: flags, slots (LifeTuning::chain_mem)
-  size_t chain_bytes_[2] = {0, 0};
+  void* chain_[5] = {};  // chained groups: flags, slots; linked launches: 3 x completion words (chain_mem)
+  size_t chain_bytes_[5] = {};
+  hipk::LinkState link_;  // linked launches (GOL_LINK)
+  bool link_on_ = false;
   uint32_t chain_seq_ = 0;
   bool u8_pipe_ = true;  // GOL_U8_PIPE: T = 48 / 64 byte passes
   int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, 2 timing probe, -1 autotuned per launch shape

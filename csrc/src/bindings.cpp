@@ -216,6 +216,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_readonly("overlapped", &RunResult::overlapped)
       .def_readonly("graph_launches", &RunResult::graph_launches)
       .def_readonly("halo_bytes", &RunResult::halo_bytes)
+      .def_readonly("linked_launches", &RunResult::linked_launches)
       .def_readonly("phase_timed", &RunResult::phase_timed)
       .def_readonly("compute_ms", &RunResult::compute_ms)
       .def_readonly("halo_ms", &RunResult::halo_ms)
@@ -235,6 +236,7 @@ PYBIND11_MODULE(_gol, m) {
         d["overlapped"] = r.overlapped;
         d["graph_launches"] = r.graph_launches;
         d["halo_bytes"] = r.halo_bytes;
+        d["linked_launches"] = r.linked_launches;
         d["phase_timed"] = r.phase_timed;
         d["compute_ms"] = r.compute_ms;
         d["halo_ms"] = r.halo_ms;

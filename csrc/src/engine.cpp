@@ -269,6 +269,7 @@ void Engine::exchange_columns(void* buf) {
 // (src/game_mpi.c:335-383).
 void Engine::halo_exchange() {
   trace::Range tr("gol.halo_exchange");
+  be_->join_streams();  // transports enqueue on the compute stream directly
   void* buf = buf_[cur_];
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
@@ -539,6 +540,7 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   p.to = to;
   const int64_t n = to - from;
   if (n <= 0) return p;
+  be_->join_streams();  // transports enqueue on the compute stream directly
   uint32_t* dev = flags_ + (from + 1 - flags_base_);
   if (poll_side_) {
     // Flags of (from, to] are complete at the compute stream's current mark.
@@ -656,6 +658,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   }
   const int64_t g0 = graph_runs_;
   const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_, es0 = early_sends_;
+  const int64_t lk0 = be_->linked_launches();
   trace::Range trace_run("gol.run");
   if (cfg_.timing_barriers) {
     settle_pending(false);  // one stream at a time on the communicator
@@ -744,6 +747,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.overlapped = overlap_ || early_sends_ > es0;
   res.graph_launches = graph_runs_ - g0;
   res.halo_bytes = halo_bytes_ - hb0;
+  res.linked_launches = be_->linked_launches() - lk0;
   res.generations = limit;
   collect_phases(res);
   if (found >= 0) {

@@ -109,6 +109,7 @@ class RunReport:
     overlapped: bool = False
     graph_launches: int = 0
     halo_bytes: int = 0
+    linked_launches: int = 0  # launches that overlapped the previous one (GOL_LINK)
     # Per-phase device time (Simulation.phase_timing).
     phase_timed: bool = False
     compute_ms: float = 0.0
@@ -229,7 +230,8 @@ class Simulation:
                         loop_ms=r.loop_ms, first_unchanged=r.first_unchanged, extinct=r.extinct,
                         exchanges=r.exchanges, polls=r.polls, kernel_launches=r.kernel_launches,
                         cells=self.config.width * self.config.height, overlapped=r.overlapped,
-                        graph_launches=r.graph_launches, halo_bytes=r.halo_bytes, phase_timed=r.phase_timed,
+                        graph_launches=r.graph_launches, halo_bytes=r.halo_bytes,
+                        linked_launches=r.linked_launches, phase_timed=r.phase_timed,
                         compute_ms=r.compute_ms, halo_ms=r.halo_ms, fill_ms=r.fill_ms,
                         allreduce_ms=r.allreduce_ms)
         self.last_report = rep

@@ -722,3 +722,40 @@ def test_pipelined_byte_pass_t48_termination_and_ranks(gpu):
     reps = grp.advance(gens)
     assert all(r.overlapped for r in reps)
     assert (grp.gather() == want).all()
+
+
+@pytest.mark.parametrize("W,H", [(32768, 1024), (4096, 700), (2048 * 3, 333), (32 * 100, 1000)])
+@pytest.mark.parametrize("xlane,tmax", [(0, 16), (0, 8), (3, 12), (0, 12)])
+def test_linked_launches_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
+    """Linked launches (GOL_LINK=1, LifeBlockParams::link_*): consecutive
+    grouped launches of an epoch run on two streams at once and order their
+    rows through per-group completion words; against the fp32 conv oracle,
+    with several epochs, the drifting adder window and partial epochs."""
+    monkeypatch.setenv("GOL_LINK", "1")
+    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    g = random_grid(W, H, W + 3 * H + tmax)
+    gens = 10 * tmax + 7
+    want = life_step_torch(g, gens, device="cuda")
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax), engine="hip")
+    sim.load(g)
+    rep = sim.advance(gens)
+    assert (sim.tile() == want).all()
+    assert rep.linked_launches > 0
+
+
+def test_linked_launches_termination_and_subdomains(gpu, monkeypatch):
+    monkeypatch.setenv("GOL_LINK", "1")
+    grid = np.zeros((1024, 2048), dtype=np.uint8)
+    W, H, seed, density = CONVERGING[5]
+    grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(grid)
+    out, rep = simulate(grid, 1000, engine="hip", tmax=16)
+    assert rep.generations == rgens
+    assert (out == ref).all()
+    W, H, gens = 32 * 64, 4 * 300, 400
+    g = random_grid(W, H, 12)
+    want = life_step_torch(g, gens, device="cuda")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x4", tmax=16), 4, engine="hip", devices=[0])
+    grp.load(g)
+    grp.advance(gens)
+    assert (grp.gather() == want).all()
