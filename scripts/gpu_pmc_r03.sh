@@ -20,6 +20,7 @@ run() {  # run NAME LIMIT CMD...
   echo "step $name rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 }
+[ -x bin/ubench_clock ] || hipcc --offload-arch=gfx950 -O3 csrc/tools/ubench_clock.hip -o bin/ubench_clock
 run clock 90 rocprofv3 --pmc $OCC --output-format csv -d $O/clock -o run -- bin/ubench_clock
 run full 150 rocprofv3 --pmc $OCC --output-format csv -d $O/full -o run -- python3 bench.py $B
 run tile 150 rocprofv3 --pmc $OCC --output-format csv -d $O/tile -o run -- python3 bench.py $B --height 4096
