@@ -123,6 +123,8 @@ def parse_args(argv=None):
     ap.add_argument("--size", type=int, default=32768, help="grid side (cells)")
     ap.add_argument("--height", type=int, default=0, help="grid height if not square (experiments only)")
     ap.add_argument("--layout", default="bits", choices=["bits", "u8"])
+    ap.add_argument("--u8-compute", default="auto", choices=["auto", "bits", "bytes"],
+                    help="byte layout: epochs on bit words (auto on the GPU) or on the bytes themselves")
     ap.add_argument("--engine", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"],
                     help="halo transport between rank processes (auto: rccl on GPU, torch/gloo on CPU)")
@@ -212,7 +214,7 @@ def main() -> int:
     total = a.prewarm + (a.warmup + a.steps * a.repeats) * gps + extra
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
                      poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs, timing_barriers=False,
-                     self_exchange=bool(a.rehearse_rccl and world == 1),
+                     self_exchange=bool(a.rehearse_rccl and world == 1), u8_compute=a.u8_compute,
                      watchdog_s=300.0)  # a stuck rank or kernel fails the run instead of hanging it
     sim = Simulation(cfg, transport=transport, backend=backend)
     eng = sim.native_engine
@@ -284,7 +286,10 @@ def main() -> int:
             dev = "cuda" if on_gpu else "cpu"
             want = life_step_torch_roll(snap, done, device=dev)
             ok_torch = bool(np.array_equal(final, want))
-            u8 = Simulation(LifeConfig(S, Hg, gen_limit=done, layout="u8", check_similarity=False),
+            # The byte kernels themselves: an engine path independent of the
+            # bit kernels (whatever layout the timed run used).
+            u8 = Simulation(LifeConfig(S, Hg, gen_limit=done, layout="u8", u8_compute="bytes",
+                                       check_similarity=False),
                             transport=native().self_transport(), backend=backend)
             u8.load(snap)
             u8.advance(done)
@@ -321,6 +326,7 @@ def main() -> int:
                 "parallelism": f"{desc['decomp']} row/col tiles, {desc['transport'] if world > 1 else 'rccl-self (rehearsal)' if a.rehearse_rccl else 'single'} halos",
                 "grid": f"{S}x{Hg}",
                 "layout": a.layout,
+                "u8_compute": desc["u8_compute"],
                 "engine": backend.name(),
                 "kernel": desc["kernel"],
                 "tmax": desc["tmax"],

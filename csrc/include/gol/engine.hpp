@@ -77,6 +77,17 @@ struct EngineConfig {
   // to itself) instead of the local periodic fill, with the multi-rank epoch
   // depth and overlap.  Results are identical (the torus wraps to self).
   bool self_exchange = false;
+  // Compute representation of the byte layout (width % 32 == 0):
+  //    1 bits: the byte-per-cell grid stays the storage (load / store / read-
+  //      out / drift rotation / alive count), but each epoch packs the owned
+  //      rows into bit words inside the spare byte buffer, exchanges or fills
+  //      the halos there (8x fewer bytes), runs the bit-sliced temporal
+  //      blocks, and unpacks the owned rows back: two byte passes per epoch
+  //      instead of one per temporal block (docs/PERFORMANCE.md);
+  //    0 bytes: temporal blocks on the byte grid itself (the byte kernels);
+  //   -1 auto: bits on a device backend with the plain or auto schedule
+  //      (GOL_U8_VIA_BITS=0|1 overrides), else bytes.
+  int u8_compute = -1;
 };
 
 struct RunResult {
@@ -145,6 +156,8 @@ class Engine {
   int64_t drift() const { return drift_; }
   // Whether temporal blocks may run the drifting (adder-window) kernel.
   bool drifting() const { return drift_ok_; }
+  // Whether byte-layout epochs compute on bit words (EngineConfig::u8_compute).
+  bool via_bits() const { return via_bits_; }
   // Rotates the drift out of the current buffer (owned rows); every
   // read-out (store_cells) does this first.
   void normalize();
@@ -186,7 +199,11 @@ class Engine {
   int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base,
              void* stream = nullptr, int64_t dual_offset = 0, bool prio_boost = false);
   void add_drift(int64_t cells);
-  void exchange_columns(void* buf);
+  void exchange_columns(void* buf, const TileGeom& g);
+  void halo_exchange_on(void* buf, const TileGeom& g);
+  // One byte-layout epoch on bit words (EngineConfig::u8_compute = 1).
+  void epoch_via_bits(int64_t d);
+  void* bit_scratch(int i) const;
   // Stream carrying this engine's transport operations (comm stream in the
   // early-boundary schedule, else the compute stream), and the two orderings.
   void* rccl_stream() const;
@@ -251,6 +268,9 @@ class Engine {
   bool drift_ok_ = false;   // whole-width tile of 32-cell words on a drifting backend
   bool cols_filled_ = true; // column halos kept valid by fills (false: the backend wraps column reads)
   bool rows_wrapped_ = false; // single-rank torus read modulo its rows (no fills at all)
+  bool via_bits_ = false;    // byte layout computed on bit words (epoch_via_bits)
+  TileGeom gb_;              // the tile in the bit layout (same rows, halos, words)
+  void* bitbuf_[2] = {nullptr, nullptr};  // own bit scratch when the spare byte buffer cannot hold it
   bool poll_side_ = false;   // termination polls reduce on the comm stream (Transport::side_reduce)
   int64_t drift_ = 0;
   int64_t graph_drift_[2] = {0, 0};

@@ -104,14 +104,22 @@ __device__ __forceinline__ void chain_fetch(const LifeBlockParams& p, int64_t sl
                                             uint32_t* lds_slot, int lane) {
   constexpr int kRows = (T - 1) * 2 * W;
   bool arrived = false;
-  for (int spin = 0; spin < (1 << 16); ++spin) {  // each poll is an L2-bypassing load (~1-2 us)
-    if (__hip_atomic_load(p.chain_flag + flag_below, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.chain_seq) {
+  uint32_t seen = 0;
+  const int spins = 1 << p.chain_spin_log2;
+  for (int spin = 0; spin < spins; ++spin) {  // each poll is an L2-bypassing load (~1-2 us)
+    seen = __hip_atomic_load(p.chain_flag + flag_below, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen == p.chain_seq) {
       arrived = true;
       break;
     }
     __builtin_amdgcn_s_sleep(2);
   }
-  if (!arrived && p.err && lane == 0) __hip_atomic_store(p.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!arrived && p.err && lane == 0) {  // diagnostics first, then the code the host checks
+    __hip_atomic_store(p.err + 1, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.err + 2, p.chain_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.err + 3, uint32_t(flag_below), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const BufRsrc src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p.chain_buf + slot_below), short(0),
                                                         kRows * 64 * 4, kBufFlags);

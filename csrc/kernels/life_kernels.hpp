@@ -43,6 +43,8 @@ struct LifeBlockParams {
   // a kernel that has to give up (life_short_kernel's bounded LDS hand-off
   // wait) sets it instead of continuing silently with invalid rows.
   uint32_t* err;
+  // Chained-group spin bound, log2 of polls (GOL_CHAIN_SPIN, default 16).
+  int chain_spin_log2;
   // Dual launch (BlockArgs::dual_offset): blocks / waves past the first
   // ncolw x nseg evaluate the same row range shifted by row_alt rows.
   int64_t row_alt;
@@ -150,7 +152,8 @@ struct LifeTuning {
   std::function<uint32_t*(int which, size_t n)> chain_mem;
   LinkState* link = nullptr;     // linked launches on (null: every launch on the given stream)
   uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
-  uint32_t* err = nullptr;       // LifeBlockParams::err
+  uint32_t* err = nullptr;       // LifeBlockParams::err (4 words: code, then a give-up's diagnostics)
+  int chain_spin_log2 = 16;      // LifeBlockParams::chain_spin_log2
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).
   std::function<void*(size_t)> scratch;
 };
@@ -202,6 +205,10 @@ void launch_init_random(uint8_t* buf, const TileGeom& g, uint64_t seed, uint32_t
 // `dst`: dst cell x = src cell (x + shift) mod W.  Undoes the adder window's
 // storage drift.
 void launch_rotate_cols(const uint8_t* src, uint8_t* dst, const TileGeom& g, int64_t shift, hipStream_t s);
+// Rows [r0, r0 + nrows) of every padded word, byte cells <-> bit words (the
+// two geometries differ only in layout and pitch).
+void launch_convert_rows(const uint8_t* src, const TileGeom& gs, uint8_t* dst, const TileGeom& gd, int64_t r0,
+                         int64_t nrows, hipStream_t s);
 
 }  // namespace hipk
 }  // namespace gol

@@ -219,7 +219,58 @@ __global__ void rotate_cols_u8(const uint8_t* in, uint8_t* out, int64_t pitch, i
   }
 }
 
+// Byte cells <-> bit words (one 32-cell word per thread, two 16-byte loads or
+// stores).  Four cells at a time: the 0/1 bytes of a dword are gathered into
+// its top nibble by one multiply (byte k lands on bit 24 + k), and a nibble is
+// spread back over four bytes by the inverse multiply (disjoint shifts 0, 7,
+// 14, 21, so no carries).
+__device__ __forceinline__ uint32_t nibble_of(uint32_t v) {
+  v = ((v & 0x7f7f7f7fu) + 0x7f7f7f7fu) | v;  // any nonzero byte -> top bit set
+  return (((v >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+}
+__device__ __forceinline__ uint32_t bytes_of(uint32_t n) { return ((n & 0xfu) * 0x00204081u) & 0x01010101u; }
+
+__global__ void pack_rows_k(const uint8_t* u8, int64_t pitch, uint32_t* bits, int64_t pitch_w, int64_t r0,
+                            int64_t nrows, int64_t wp) {
+  const int64_t n = nrows * wp;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n; t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / wp, k = t - i * wp;
+    const uint4* src = reinterpret_cast<const uint4*>(u8 + (r0 + i) * pitch + 32 * k);
+    const uint4 a = src[0], b = src[1];
+    const uint32_t w = nibble_of(a.x) | nibble_of(a.y) << 4 | nibble_of(a.z) << 8 | nibble_of(a.w) << 12 |
+                       nibble_of(b.x) << 16 | nibble_of(b.y) << 20 | nibble_of(b.z) << 24 | nibble_of(b.w) << 28;
+    bits[(r0 + i) * pitch_w + k] = w;
+  }
+}
+
+__global__ void unpack_rows_k(const uint32_t* bits, int64_t pitch_w, uint8_t* u8, int64_t pitch, int64_t r0,
+                              int64_t nrows, int64_t wp) {
+  const int64_t n = nrows * wp;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n; t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = t / wp, k = t - i * wp;
+    const uint32_t w = bits[(r0 + i) * pitch_w + k];
+    uint4* dst = reinterpret_cast<uint4*>(u8 + (r0 + i) * pitch + 32 * k);
+    dst[0] = make_uint4(bytes_of(w), bytes_of(w >> 4), bytes_of(w >> 8), bytes_of(w >> 12));
+    dst[1] = make_uint4(bytes_of(w >> 16), bytes_of(w >> 20), bytes_of(w >> 24), bytes_of(w >> 28));
+  }
+}
+
 }  // namespace
+
+void launch_convert_rows(const uint8_t* src, const TileGeom& gs, uint8_t* dst, const TileGeom& gd, int64_t r0,
+                         int64_t nrows, hipStream_t s) {
+  GOL_REQUIRE(gs.layout != gd.layout, "convert_rows: layouts must differ");
+  GOL_REQUIRE(gs.Wp() == gd.Wp() && gs.R() == gd.R() && gs.W % 32 == 0, "convert_rows: geometries differ");
+  GOL_REQUIRE(r0 >= 0 && nrows >= 0 && r0 + nrows <= gs.R(), "convert_rows: rows out of range");
+  if (nrows == 0) return;
+  const int64_t n = nrows * gs.Wp();
+  if (gs.layout == Layout::U8)
+    hipLaunchKernelGGL(pack_rows_k, dim3(grid_for(n, 1 << 16)), dim3(kBlock), 0, s, src, gs.pitch,
+                       reinterpret_cast<uint32_t*>(dst), gd.pitch / 4, r0, nrows, gs.Wp());
+  else
+    hipLaunchKernelGGL(unpack_rows_k, dim3(grid_for(n, 1 << 16)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const uint32_t*>(src), gs.pitch / 4, dst, gd.pitch, r0, nrows, gs.Wp());
+}
 
 void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s) {
   hipLaunchKernelGGL(i64_k, dim3(1), dim3(1), 0, s, p, v, add ? 1 : 0);

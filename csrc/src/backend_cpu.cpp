@@ -89,6 +89,8 @@ class CpuBackend final : public Backend {
   std::string name() const override { return drift_ ? "cpu [drift]" : "cpu"; }
   bool drifts(Layout) const override { return drift_; }
   void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override;
+  void convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t r0,
+                    int64_t n) override;
   bool is_device() const override { return false; }
 
   void* alloc(size_t bytes) override {
@@ -280,6 +282,34 @@ void CpuBackend::rotate_cols(const void* src, void* dst, const TileGeom& g, int6
           byte = uint8_t((byte & ~(1u << (c % 8))) | (unsigned(v) << (c % 8)));
         } else {
           out[c] = v;
+        }
+      }
+    }
+  });
+}
+
+void CpuBackend::convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t r0,
+                              int64_t n) {
+  GOL_REQUIRE(gs.layout != gd.layout, "convert_rows: layouts must differ");
+  GOL_REQUIRE(gs.Wp() == gd.Wp() && gs.R() == gd.R() && gs.W % 32 == 0, "convert_rows: geometries differ");
+  GOL_REQUIRE(r0 >= 0 && n >= 0 && r0 + n <= gs.R(), "convert_rows: rows out of range");
+  auto* s = static_cast<const uint8_t*>(src);
+  auto* d = static_cast<uint8_t*>(dst);
+  const int64_t wp = gs.Wp();
+  const bool to_bits = gs.layout == Layout::U8;
+  pool_.parallel_for(n, [&](int64_t b, int64_t e) {
+    for (int64_t i = r0 + b; i < r0 + e; ++i) {
+      const uint8_t* in = s + i * gs.pitch;
+      uint8_t* out = d + i * gd.pitch;
+      for (int64_t k = 0; k < wp; ++k) {
+        if (to_bits) {
+          uint32_t w = 0;
+          for (int j = 0; j < 32; ++j) w |= uint32_t(in[32 * k + j] != 0) << j;
+          std::memcpy(out + 4 * k, &w, 4);
+        } else {
+          uint32_t w;
+          std::memcpy(&w, in + 4 * k, 4);
+          for (int j = 0; j < 32; ++j) out[32 * k + j] = uint8_t((w >> j) & 1u);
         }
       }
     }

@@ -99,7 +99,7 @@ class HipBackend final : public Backend {
         if (link_.stream[1]) HIP_CHECK(hipStreamSynchronize(link_.stream[1]));
         if (buf) HIP_CHECK(hipFree(buf));
         HIP_CHECK(hipMalloc(&buf, n));
-        if (which != 1) HIP_CHECK(hipMemset(buf, 0, n));
+        if (which != 1) HIP_CHECK(hipMemsetAsync(buf, 0, n, stream_));  // ordered before the launch on stream_
         cap = n;
       }
       if (check_dev_) check_ptr(buf, which == 0 ? "chain flags" : which == 1 ? "chain slots" : "link words");
@@ -115,8 +115,9 @@ class HipBackend final : public Backend {
     }
     // Kernel error word: fine-grained pinned host memory the kernels write
     // through its device alias and the host reads without a copy.
-    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(uint32_t), hipHostMallocMapped));
-    *err_host_ = 0;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 4 * sizeof(uint32_t), hipHostMallocMapped));
+    for (int i = 0; i < 4; ++i) err_host_[i] = 0;
+    tune_.chain_spin_log2 = std::min(24, std::max(4, env_int("GOL_CHAIN_SPIN", 16)));
     HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&tune_.err), err_host_, 0));
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
@@ -550,6 +551,14 @@ class HipBackend final : public Backend {
     hipk::launch_rotate_cols(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), g, shift, stream_);
     HIP_CHECK(hipGetLastError());
   }
+  void convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t r0,
+                    int64_t n) override {
+    join_streams();
+    GOL_ON_DEVICE();
+    hipk::launch_convert_rows(static_cast<const uint8_t*>(src), gs, static_cast<uint8_t*>(dst), gd, r0, n,
+                              stream_);
+    HIP_CHECK(hipGetLastError());
+  }
   // GOL_WG_TRACE=<launch index>:<csv path>: one life_block launch records
   // where and when each of its waves ran (grouped kernel, LifeBlockParams::
   // wg_trace); scripts/wg_trace.py turns the CSV into a per-CU makespan view.
@@ -586,7 +595,11 @@ class HipBackend final : public Backend {
     const uint32_t e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
     if (e != 0) {
       *err_host_ = 0;
-      fail(std::string(e == 2   ? "life_group kernel (chained groups): a wave gave up waiting for the group below"
+      const std::string diag = e == 2 ? " [flag " + std::to_string(err_host_[3]) + " read " +
+                                            std::to_string(err_host_[1]) + ", expected " +
+                                            std::to_string(err_host_[2]) + "]"
+                                      : "";
+      fail(std::string(e == 2   ? "life_group kernel (chained groups): a wave gave up waiting for the group below" + diag
                        : e == 3 ? "life_group kernel (linked launches): a group gave up waiting for the previous "
                                   "launch's rows"
                                 : "life_short kernel: a wave gave up waiting for its neighbour's LDS rows") +

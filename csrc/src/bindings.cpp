@@ -200,6 +200,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_readwrite("lagged_poll", &EngineConfig::lagged_poll)
       .def_readwrite("timing_barriers", &EngineConfig::timing_barriers)
       .def_readwrite("self_exchange", &EngineConfig::self_exchange)
+      .def_readwrite("u8_compute", &EngineConfig::u8_compute)
       .def_readwrite("graphs", &EngineConfig::graphs)
       .def_readwrite("watchdog_s", &EngineConfig::watchdog_s);
 
@@ -266,6 +267,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property("generation", &Engine::generation, &Engine::set_generation)
       .def_property_readonly("drift", &Engine::drift)
       .def_property_readonly("drifting", &Engine::drifting)
+      .def_property_readonly("via_bits", &Engine::via_bits)
       .def("normalize", &Engine::normalize, py::call_guard<py::gil_scoped_release>())
       .def("current_buffer", [](const Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })
       .def("load_cells",

@@ -41,12 +41,24 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     GOL_REQUIRE(cfg_.W % 32 == 0, "bit-packed layout needs width % 32 == 0 (use the u8 layout)");
   dec_ = Decomposition::make(cfg_.W, cfg_.H, tr_->size(), cfg_.decomp, unit);
 
+  // Byte layout computed on bit words (EngineConfig::u8_compute): the same
+  // decision on every rank (configuration, backend kind and environment).
+  if (cfg_.layout == Layout::U8 && cfg_.W % 32 == 0) {
+    int mode = cfg_.u8_compute;
+    if (mode < 0) {
+      const char* e = std::getenv("GOL_U8_VIA_BITS");
+      mode = e ? (std::atoi(e) != 0) : (be_->is_device() && cfg_.overlap != 1 && cfg_.overlap != 2);
+    }
+    via_bits_ = mode == 1;
+  }
+  // Layout the temporal blocks run on.
+  const Layout cl = via_bits_ ? Layout::Bits : cfg_.layout;
   // Every rank must take the same decision (a drifting frame or a schedule
   // that moves a halo exchange is only consistent in lockstep), so it is
   // made for the smallest tile of the decomposition, not this rank's.
   const Backend::KernelChoice kc =
-      be_->choose_kernel(cfg_.layout, min_tile_rows(dec_), std::max<int64_t>(1, min_tile_cols(dec_)), cfg_.tmax);
-  tmax_ = std::min(kc.tmax, cfg_.layout == Layout::U8 ? 48 : 16);
+      be_->choose_kernel(cl, min_tile_rows(dec_), std::max<int64_t>(1, min_tile_cols(dec_)), cfg_.tmax);
+  tmax_ = std::min(kc.tmax, cl == Layout::U8 ? 48 : 16);
   // Epoch depth: a deeper halo means fewer latency-bound exchanges (or local
   // periodic fills: two ~5 us launches each) but ~D redundant rows per epoch.
   // With the grouped kernel the per-rank tile costs the same from 8T to 24T
@@ -54,7 +66,9 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // and several ranks 16T: half the RCCL exchanges (4 per 1000 generations),
   // each one latency-bound.
   const bool row_exchange = dec_.Py > 1 || cfg_.self_exchange;
-  int D = cfg_.epoch > 0 ? cfg_.epoch : (tr_->size() > 1 || cfg_.self_exchange ? 16 : 8) * tmax_;
+  // On bit words a byte-layout epoch also pays one pack and one unpack pass
+  // over the byte grid (~2.25 bytes per cell), so it runs 32T generations.
+  int D = cfg_.epoch > 0 ? cfg_.epoch : (via_bits_ ? 32 : tr_->size() > 1 || cfg_.self_exchange ? 16 : 8) * tmax_;
   if (dec_.Py > 1) D = int(std::min<int64_t>(D, min_tile_rows(dec_)));
   if (dec_.Px > 1) {
     int64_t cap = 32 * (min_tile_cols(dec_) / 32);
@@ -71,7 +85,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     const int64_t h = min_tile_rows(dec_);
     int64_t min_rows = h;
     if (row_exchange && h >= 2 * int64_t(D_) + 1) min_rows = std::min({h, int64_t(D_), h - 2 * int64_t(D_)});
-    while (tmax_ > 1 && be_->min_block_rows(cfg_.layout, tmax_) > min_rows) tmax_ = pick_T(tmax_ - 1);
+    while (tmax_ > 1 && be_->min_block_rows(cl, tmax_) > min_rows) tmax_ = pick_T(tmax_ - 1);
   }
   // A drifting kernel (one-sided window, Backend::drifts) consumes 2 cells of
   // left halo per generation and none on the right; it needs the tile to be
@@ -79,11 +93,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   drift_ok_ = kc.drift && dec_.Px == 1 && cfg_.W % 32 == 0;
   // Whole-width tiles on a backend that wraps column reads (lane_cols in the
   // HIP kernels) never read their halo columns: no column fills.
-  cols_filled_ = !(dec_.Px == 1 && cfg_.W % 32 == 0 && be_->wraps_columns(cfg_.layout));
+  cols_filled_ = !(dec_.Px == 1 && cfg_.W % 32 == 0 && be_->wraps_columns(cl));
   // A single-rank torus on a backend that also wraps row reads (the T = 1
   // LDS kernel): one-generation epochs over the owned rows, no fills at all.
   rows_wrapped_ = !cols_filled_ && dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && tmax_ == 1 &&
-                  be_->wraps_rows(cfg_.layout);
+                  be_->wraps_rows(cl);
   if (rows_wrapped_) D_ = 1;
   // Halo columns: none when the kernels wrap (smaller rows to exchange and
   // fill); else D cells per side, 2D on the left for the drifting window.
@@ -98,6 +112,13 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : (tr_->size() > 1 || cfg_.self_exchange) ? 512 : 256;
 
   for (auto& b : buf_) b = be_->alloc(size_t(g_.bytes()));
+  if (via_bits_) {
+    // The bit words live in the spare byte buffer (an eighth of its size per
+    // parity) unless a tiny tile's pitch rounding does not leave room.
+    gb_ = TileGeom::make(Layout::Bits, g_.H, g_.W, g_.Dv, g_.hw);
+    if (2 * gb_.bytes() > g_.bytes())
+      for (auto& b : bitbuf_) b = be_->alloc(size_t(gb_.bytes()));
+  }
   alive_dev_ = static_cast<uint32_t*>(be_->alloc(64));
   if (dec_.Px > 1) {
     size_t n = size_t(g_.span_bytes(32 * int64_t(g_.hw)) * g_.H);
@@ -108,8 +129,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // epoch), which on the 32768 x 4096 per-rank tile cost 4x more than the
   // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
   const bool interior = min_tile_rows(dec_) >= 2 * int64_t(D_) + 1;  // on every rank
-  overlap_ = row_exchange && cfg_.overlap == 2 && interior;
-  const bool early_ok = row_exchange && dec_.Px == 1 && interior;
+  overlap_ = row_exchange && cfg_.overlap == 2 && interior && !via_bits_;
+  const bool early_ok = row_exchange && dec_.Px == 1 && interior && !via_bits_;
   early_ = early_ok && cfg_.overlap == 1;
   // With the early-boundary schedule every transport operation runs on the
   // comm stream (one stream per communicator, in issue order), so the flag
@@ -173,6 +194,8 @@ Engine::~Engine() {
     if (b) be_->release(b);
   for (auto& b : colbuf_)
     if (b) be_->release(b);
+  for (auto& b : bitbuf_)
+    if (b) be_->release(b);
   for (auto& e : edge_)
     for (auto& b : e)
       if (b) be_->release(b);
@@ -232,24 +255,24 @@ int Engine::pick_T(int64_t remaining) const {
 // cells travel with the rows): 4 messages instead of the reference's 8
 // per-generation messages with a strided MPI_Type_vector column
 // (src/game_mpi.c:335-383).
-void Engine::exchange_columns(void* buf) {
+void Engine::exchange_columns(void* buf, const TileGeom& g) {
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
-  const int64_t H = g_.H, pitch = g_.pitch;
+  const int64_t H = g.H, pitch = g.pitch;
   if (dec_.Px == 1) {
     if (cols_filled_) {
       void* t = phase_begin(nullptr);
-      be_->fill_periodic(buf, g_, /*cols=*/true, /*rows=*/false);
+      be_->fill_periodic(buf, g, /*cols=*/true, /*rows=*/false);
       phase_end(kFill, t, nullptr);
     }
     return;
   }
   void* t = phase_begin(nullptr);
-  const int64_t halo = 32 * int64_t(g_.hw);
-  const int64_t span = g_.span_bytes(halo);
-  const int64_t r0 = g_.row0();
-  be_->copy_2d_async(colbuf_[0], span, base + g_.offset(r0, g_.cell0()), pitch, span, H);
-  be_->copy_2d_async(colbuf_[1], span, base + g_.offset(r0, g_.cell0() + g_.W - halo), pitch, span, H);
+  const int64_t halo = 32 * int64_t(g.hw);
+  const int64_t span = g.span_bytes(halo);
+  const int64_t r0 = g.row0();
+  be_->copy_2d_async(colbuf_[0], span, base + g.offset(r0, g.cell0()), pitch, span, H);
+  be_->copy_2d_async(colbuf_[1], span, base + g.offset(r0, g.cell0() + g.W - halo), pitch, span, H);
   std::vector<P2POp> ops = {
       {true, nb[kWest], colbuf_[0], size_t(span * H)},
       {false, nb[kEast], colbuf_[3], size_t(span * H)},
@@ -258,8 +281,8 @@ void Engine::exchange_columns(void* buf) {
   };
   tr_->exchange(ops, be_->stream());
   halo_bytes_ += 2 * span * H;
-  be_->copy_2d_async(base + g_.offset(r0, 0), pitch, colbuf_[2], span, span, H);
-  be_->copy_2d_async(base + g_.offset(r0, g_.cell0() + g_.W), pitch, colbuf_[3], span, span, H);
+  be_->copy_2d_async(base + g.offset(r0, 0), pitch, colbuf_[2], span, span, H);
+  be_->copy_2d_async(base + g.offset(r0, g.cell0() + g.W), pitch, colbuf_[3], span, span, H);
   phase_end(kHalo, t, nullptr);
 }
 
@@ -267,33 +290,34 @@ void Engine::exchange_columns(void* buf) {
 // cells travel with the rows): 4 messages instead of the reference's 8
 // per-generation messages with a strided MPI_Type_vector column
 // (src/game_mpi.c:335-383).
-void Engine::halo_exchange() {
+void Engine::halo_exchange() { halo_exchange_on(buf_[cur_], g_); }
+
+void Engine::halo_exchange_on(void* buf, const TileGeom& g) {
   trace::Range tr("gol.halo_exchange");
   be_->join_streams();  // transports enqueue on the compute stream directly
-  void* buf = buf_[cur_];
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
-  const int64_t H = g_.H, pitch = g_.pitch;
+  const int64_t H = g.H, pitch = g.pitch;
   if (rows_wrapped_) {  // the kernels read the torus modulo its rows and columns
     ++exchanges_;
     return;
   }
   if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange) {  // one rank: both periodic fills, one launch
     void* t = phase_begin(nullptr);
-    be_->fill_periodic(buf, g_, /*cols=*/cols_filled_, /*rows=*/true);
+    be_->fill_periodic(buf, g, /*cols=*/cols_filled_, /*rows=*/true);
     phase_end(kFill, t, nullptr);
     ++exchanges_;
     return;
   }
   // Phase A: west/east halo columns of the owned rows.
-  exchange_columns(buf);
+  exchange_columns(buf, g);
   // Phase B: north/south halo rows over the full padded width.
   if (dec_.Py == 1 && !cfg_.self_exchange) {
     void* t = phase_begin(nullptr);
-    be_->fill_periodic(buf, g_, /*cols=*/false, /*rows=*/true);
+    be_->fill_periodic(buf, g, /*cols=*/false, /*rows=*/true);
     phase_end(kFill, t, nullptr);
   } else {
-    const int64_t Dv = g_.Dv;
+    const int64_t Dv = g.Dv;
     const size_t bytes = size_t(Dv * pitch);
     std::vector<P2POp> ops = {
         {true, nb[kNorth], base + Dv * pitch, bytes},        // my top rows -> north's bottom halo
@@ -331,7 +355,7 @@ void Engine::epoch_overlapped(int64_t d) {
   auto nb = dec_.neighbors(rank_);
   const int64_t D = D_, H = g_.H, Dv = g_.Dv, pitch = g_.pitch;
   auto* main_in = static_cast<uint8_t*>(buf_[cur_]);
-  exchange_columns(main_in);
+  exchange_columns(main_in, g_);
   auto* top = static_cast<uint8_t*>(edge_[0][0]);
   auto* bot = static_cast<uint8_t*>(edge_[1][0]);
   be_->copy_2d_async(top + D * pitch, pitch, main_in + Dv * pitch, pitch, pitch, 2 * D);
@@ -384,7 +408,45 @@ void Engine::epoch_overlapped(int64_t d) {
   gen_ += d;
 }
 
+void* Engine::bit_scratch(int i) const {
+  if (bitbuf_[i]) return bitbuf_[i];
+  return static_cast<uint8_t*>(buf_[cur_ ^ 1]) + i * gb_.bytes();
+}
+
+// Byte-layout epoch on bit words.  The byte grid is read once (owned rows ->
+// bit words in the spare byte buffer) and written once (bit words -> owned
+// rows) per epoch; the halo exchange or fill and every temporal block run on
+// the bit tile, whose per-generation flags are those of the same cells.  The
+// byte grid's halo rows and columns are never read.  A drifting bit kernel
+// leaves the byte grid drifted by the same amount (a relabeling of columns,
+// rotated out by normalize() like the bit layout's).
+void Engine::epoch_via_bits(int64_t d) {
+  trace::Range tr("gol.epoch_via_bits");
+  void* bytes = buf_[cur_];
+  void* t = phase_begin(nullptr);
+  be_->convert_rows(bytes, g_, bit_scratch(0), gb_, g_.row0(), g_.H);
+  phase_end(kCompute, t, nullptr);
+  halo_exchange_on(bit_scratch(0), gb_);
+  int64_t a = 0;
+  int par = 0;
+  while (d > 0) {
+    const int T = pick_T(d);
+    add_drift(launch(bit_scratch(par), bit_scratch(par ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
+    par ^= 1;
+    gen_ += T;
+    a += T;
+    d -= T;
+  }
+  t = phase_begin(nullptr);
+  be_->convert_rows(bit_scratch(par), gb_, bytes, g_, g_.row0(), g_.H);
+  phase_end(kCompute, t, nullptr);
+}
+
 void Engine::run_epoch(int64_t d) {
+  if (via_bits_) {
+    epoch_via_bits(d);
+    return;
+  }
   if (overlap_) {
     epoch_overlapped(d);
     return;

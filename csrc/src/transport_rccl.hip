@@ -101,7 +101,8 @@ class RcclTransport final : public Transport {
     }
     HIP_CHECK(hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking));
     HIP_CHECK(hipMalloc(&barrier_buf_, 64));
-    HIP_CHECK(hipMemset(barrier_buf_, 0, 64));
+    HIP_CHECK(hipMemsetAsync(barrier_buf_, 0, 64, barrier_stream_));  // HIP's hipMemset may return before it ran
+    HIP_CHECK(hipStreamSynchronize(barrier_stream_));
   }
   ~RcclTransport() override {
     DeviceScope on(dev_);

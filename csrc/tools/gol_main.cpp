@@ -50,6 +50,7 @@ struct Options {
   uint64_t seed = 1;
   double density = 0.5;
   int ranks = 1, gpus = 0, threads = 0, tmax = 0, epoch = 0, poll = 0, overlap = -1, graphs = 0;
+  int u8_compute = -1;  // auto | bytes (0) | bits (1)
   bool show = false;
   bool phase_timing = false;  // per-phase device times in --metrics-json
   int64_t checkpoint_every = 0;     // generations between checkpoints (0: none)
@@ -65,6 +66,8 @@ struct Options {
                "usage: gol [width] [height] [input_file] [options]\n"
                "  --engine auto|hip|cpu|ref   compute engine (ref = exact serial game.c loop)\n"
                "  --layout auto|bits|u8       cell storage (bits needs width %% 32 == 0)\n"
+               "  --u8-compute auto|bits|bytes  byte-layout epochs on bit words (packed once per\n"
+               "                              epoch; auto: on the GPU) or on the bytes themselves\n"
                "  --gens N                    GEN_LIMIT (default 1000)\n"
                "  --sim-freq F                SIMILARITY_FREQUENCY (default 3)\n"
                "  --no-similarity             disable the similarity check\n"
@@ -108,6 +111,11 @@ Options parse(int argc, char** argv) {
     if (a == "-h" || a == "--help") usage(0);
     else if (a == "--engine") o.engine = next();
     else if (a == "--layout") o.layout = next();
+    else if (a == "--u8-compute") {
+      std::string v = next();
+      if (v != "auto" && v != "bits" && v != "bytes") usage(2);
+      o.u8_compute = v == "bits" ? 1 : v == "bytes" ? 0 : -1;
+    }
     else if (a == "--decomp") o.decomp = next();
     else if (a == "--comm") o.comm = next();
     else if (a == "--gens") o.gens = std::atoll(next().c_str()), o.gens_set = true;
@@ -255,6 +263,7 @@ int run(const Options& o) {
     cfg.poll_gens = o.poll;
     cfg.overlap = o.overlap;
     cfg.graphs = o.graphs;
+    cfg.u8_compute = o.u8_compute;
     cfg.start_gen = o.start_gen;
     cfg.sim_phase = o.sim_phase;
     int ndev = 1;

@@ -26,6 +26,8 @@ def parse_args(argv=None):
     p.add_argument("input_file", nargs="?", default=None)
     p.add_argument("--engine", default="auto", choices=["auto", "hip", "cpu", "ref"])
     p.add_argument("--layout", default="auto", choices=["auto", "bits", "u8"])
+    p.add_argument("--u8-compute", default="auto", choices=["auto", "bits", "bytes"],
+                   help="byte layout: epochs on bit words packed once per epoch (auto: on the GPU) or on the bytes")
     p.add_argument("--gens", type=int, default=1000, help="GEN_LIMIT")
     p.add_argument("--sim-freq", type=int, default=None, help="SIMILARITY_FREQUENCY (default 3)")
     p.add_argument("--no-similarity", action="store_true")
@@ -116,7 +118,8 @@ def main(argv=None) -> int:
 
     cfg = LifeConfig(a.width, a.height, gen_limit=a.gens, check_similarity=not a.no_similarity,
                      sim_freq=a.sim_freq, layout=a.layout, decomp=a.decomp, tmax=a.tmax,
-                     epoch=a.epoch, poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs)
+                     epoch=a.epoch, poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs,
+                     u8_compute=a.u8_compute)
     src = a.input_file
     if a.resume:
         from .utils.checkpoint import load_checkpoint  # noqa: PLC0415

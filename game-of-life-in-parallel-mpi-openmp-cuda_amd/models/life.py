@@ -50,6 +50,8 @@ class LifeConfig:
     timing_barriers: bool = True  # barrier + sync around each run's loop (off: the caller brackets it)
     self_exchange: bool = False   # rehearse the multi-rank row-halo schedule on one rank (transport to self)
     watchdog_s: float = 0.0       # fail when a termination poll waits longer (0 = GOL_WATCHDOG_S or 900 s)
+    u8_compute: str = "auto"      # auto | bits | bytes: byte-layout epochs on bit words (packed once per epoch)
+                                  # or on the bytes themselves; auto = bits on the GPU with the plain schedule
 
     def resolved_layout(self) -> str:
         if self.layout == "auto":
@@ -79,6 +81,7 @@ class LifeConfig:
         c.timing_barriers = bool(self.timing_barriers)
         c.self_exchange = bool(self.self_exchange)
         c.watchdog_s = float(self.watchdog_s)
+        c.u8_compute = {"auto": -1, "bytes": 0, "bits": 1}[self.u8_compute]
         return c
 
 
@@ -195,6 +198,7 @@ class Simulation:
                 "graphs": self._eng.graphs(), "overlap_mode": self._eng.overlap_mode(),
                 "overlap_trial_ms_plain": self._eng.trial_ms_plain,
                 "overlap_trial_ms_early": self._eng.trial_ms_early,
+                "u8_compute": ("bits" if self._eng.via_bits else "bytes") if self.config.resolved_layout() == "u8" else None,
                 "kernel": "adder window (drifting frame)" if self._eng.drifting else "symmetric window"}
 
     # -- state -----------------------------------------------------------

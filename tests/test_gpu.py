@@ -13,6 +13,14 @@ from golden import CASES, CONVERGING, GLIDER
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _byte_kernels(monkeypatch):
+    """The byte-layout tests here exercise the byte kernels themselves; the
+    GPU's default byte-layout path (bit words, EngineConfig::u8_compute auto)
+    has its own tests at the end of this file (test_u8_via_bits_*)."""
+    monkeypatch.setenv("GOL_U8_VIA_BITS", "0")
+
+
 def test_hip_backend_is_native_gfx950(gpu):
     be = gpu.hip_backend(0)
     assert be.is_device()
@@ -758,4 +766,56 @@ def test_linked_launches_termination_and_subdomains(gpu, monkeypatch):
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x4", tmax=16), 4, engine="hip", devices=[0])
     grp.load(g)
     grp.advance(gens)
+    assert (grp.gather() == want).all()
+
+
+# ---- byte layout on bit words (Engine::epoch_via_bits), the GPU default ----
+
+@pytest.mark.parametrize("W,H,gens,tmax", [(32, 1, 40, 0), (96, 70, 77, 4), (2048, 40, 200, 0), (6400, 700, 131, 8),
+                                           (8192, 1024, 1000, 0)])
+def test_u8_via_bits_default_vs_torch(gpu, monkeypatch, W, H, gens, tmax):
+    monkeypatch.delenv("GOL_U8_VIA_BITS", raising=False)
+    g = random_grid(W, H, W + H + gens)
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=tmax), engine="hip")
+    d = sim.describe()
+    assert d["u8_compute"] == "bits" and d["layout"] == "u8"
+    sim.load(g)
+    sim.advance(gens)
+    assert (sim.tile() == life_step_torch(g, gens, device="cuda")).all()
+
+
+def test_u8_via_bits_ragged_width_falls_back(gpu, monkeypatch):
+    monkeypatch.delenv("GOL_U8_VIA_BITS", raising=False)
+    W, H = 1000, 64
+    g = random_grid(W, H, 3)
+    sim = Simulation(LifeConfig(W, H, gen_limit=50, layout="u8"), engine="hip")
+    assert sim.describe()["u8_compute"] == "bytes"
+    sim.load(g)
+    sim.advance(50)
+    assert (sim.tile() == life_step_torch(g, 50, device="cuda")).all()
+
+
+@pytest.mark.parametrize("W,H,seed,density", [(32, 16, 1, 0.2), (64, 20, 1, 0.2), (128, 12, 11, 0.2)] +
+                         [c for c in CONVERGING if c[0] % 32 == 0])
+def test_u8_via_bits_termination(gpu, W, H, seed, density):
+    g = random_grid(W, H, seed, density)
+    ref, rgens, _ = reference_run(g)
+    for tmax, epoch in [(0, 0), (4, 7), (1, 1)]:
+        sim = Simulation(LifeConfig(W, H, layout="u8", u8_compute="bits", tmax=tmax, epoch=epoch), engine="hip")
+        sim.load(g)
+        rep = sim.run()
+        assert rep.generations == rgens, (tmax, epoch)
+        assert (sim.tile() == ref).all()
+
+
+@pytest.mark.parametrize("spec,P", [("1x2", 2), ("2x2", 4), ("1x4", 4)])
+def test_u8_via_bits_subdomains_one_gpu(gpu, spec, P):
+    W, H = 4096, 512
+    g = random_grid(W, H, 41)
+    want = life_step_torch(g, 300, device="cuda")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=300, decomp=spec, layout="u8", u8_compute="bits",
+                                    check_similarity=False), P, engine="hip")
+    grp.load(g)
+    grp.parallel(lambda s: s.advance(300))
+    assert all(s.native_engine.via_bits for s in grp.sims)
     assert (grp.gather() == want).all()
