@@ -114,10 +114,11 @@ class Backend {
   // Owned rows of src rotated left by `shift` cells (0 < shift < W) into dst:
   // dst cell x = src cell (x + shift) mod W.  Halos of dst are not written.
   virtual void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) = 0;
-  // Padded rows [r0, r0 + n) of src (geometry gs) converted into dst
-  // (geometry gd: the same tile in the other layout) over every padded word:
-  // byte cells -> bit words or back.  Enqueued on the compute stream.
-  virtual void convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t r0,
+  // Owned rows [i0, i0 + n) of src (geometry gs) converted into dst
+  // (geometry gd: the same owned tile in the other layout, halos and pitch
+  // may differ), owned cells only: byte cells -> bit words or back.
+  // Enqueued on the compute stream.
+  virtual void convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t i0,
                             int64_t n) = 0;
   // Throws if a kernel enqueued so far reported an error through the
   // backend's device-visible error word (call after the work completed).

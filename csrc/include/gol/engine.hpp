@@ -130,6 +130,10 @@ class Engine {
   const EngineConfig& config() const { return cfg_; }
   const Decomposition& decomp() const { return dec_; }
   const TileGeom& geom() const { return g_; }
+  // The tile the temporal blocks run on: geom(), or its bit-word image when
+  // the byte layout computes on bit words (via_bits(); the byte tile then has
+  // no halos).
+  const TileGeom& compute_geom() const { return via_bits_ ? gb_ : g_; }
   int rank() const { return rank_; }
   Extent rows() const { return dec_.rows(rank_); }
   Extent cols() const { return dec_.cols(rank_); }

@@ -205,9 +205,9 @@ void launch_init_random(uint8_t* buf, const TileGeom& g, uint64_t seed, uint32_t
 // `dst`: dst cell x = src cell (x + shift) mod W.  Undoes the adder window's
 // storage drift.
 void launch_rotate_cols(const uint8_t* src, uint8_t* dst, const TileGeom& g, int64_t shift, hipStream_t s);
-// Rows [r0, r0 + nrows) of every padded word, byte cells <-> bit words (the
-// two geometries differ only in layout and pitch).
-void launch_convert_rows(const uint8_t* src, const TileGeom& gs, uint8_t* dst, const TileGeom& gd, int64_t r0,
+// Owned rows [i0, i0 + nrows) of the owned cells, byte cells <-> bit words
+// (the two geometries hold the same owned tile; halos and pitch may differ).
+void launch_convert_rows(const uint8_t* src, const TileGeom& gs, uint8_t* dst, const TileGeom& gd, int64_t i0,
                          int64_t nrows, hipStream_t s);
 
 }  // namespace hipk

@@ -230,26 +230,28 @@ __device__ __forceinline__ uint32_t nibble_of(uint32_t v) {
 }
 __device__ __forceinline__ uint32_t bytes_of(uint32_t n) { return ((n & 0xfu) * 0x00204081u) & 0x01010101u; }
 
-__global__ void pack_rows_k(const uint8_t* u8, int64_t pitch, uint32_t* bits, int64_t pitch_w, int64_t r0,
-                            int64_t nrows, int64_t wp) {
-  const int64_t n = nrows * wp;
+// Owned cells only: `src`/`dst` point at owned row 0, owned word 0 of each
+// geometry (the two may differ in halo rows, halo words and pitch).
+__global__ void pack_rows_k(const uint8_t* u8, int64_t pitch, uint32_t* bits, int64_t pitch_w, int64_t nrows,
+                            int64_t ow) {
+  const int64_t n = nrows * ow;
   for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n; t += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t i = t / wp, k = t - i * wp;
-    const uint4* src = reinterpret_cast<const uint4*>(u8 + (r0 + i) * pitch + 32 * k);
+    const int64_t i = t / ow, k = t - i * ow;
+    const uint4* src = reinterpret_cast<const uint4*>(u8 + i * pitch + 32 * k);
     const uint4 a = src[0], b = src[1];
     const uint32_t w = nibble_of(a.x) | nibble_of(a.y) << 4 | nibble_of(a.z) << 8 | nibble_of(a.w) << 12 |
                        nibble_of(b.x) << 16 | nibble_of(b.y) << 20 | nibble_of(b.z) << 24 | nibble_of(b.w) << 28;
-    bits[(r0 + i) * pitch_w + k] = w;
+    bits[i * pitch_w + k] = w;
   }
 }
 
-__global__ void unpack_rows_k(const uint32_t* bits, int64_t pitch_w, uint8_t* u8, int64_t pitch, int64_t r0,
-                              int64_t nrows, int64_t wp) {
-  const int64_t n = nrows * wp;
+__global__ void unpack_rows_k(const uint32_t* bits, int64_t pitch_w, uint8_t* u8, int64_t pitch, int64_t nrows,
+                              int64_t ow) {
+  const int64_t n = nrows * ow;
   for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < n; t += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t i = t / wp, k = t - i * wp;
-    const uint32_t w = bits[(r0 + i) * pitch_w + k];
-    uint4* dst = reinterpret_cast<uint4*>(u8 + (r0 + i) * pitch + 32 * k);
+    const int64_t i = t / ow, k = t - i * ow;
+    const uint32_t w = bits[i * pitch_w + k];
+    uint4* dst = reinterpret_cast<uint4*>(u8 + i * pitch + 32 * k);
     dst[0] = make_uint4(bytes_of(w), bytes_of(w >> 4), bytes_of(w >> 8), bytes_of(w >> 12));
     dst[1] = make_uint4(bytes_of(w >> 16), bytes_of(w >> 20), bytes_of(w >> 24), bytes_of(w >> 28));
   }
@@ -257,19 +259,23 @@ __global__ void unpack_rows_k(const uint32_t* bits, int64_t pitch_w, uint8_t* u8
 
 }  // namespace
 
-void launch_convert_rows(const uint8_t* src, const TileGeom& gs, uint8_t* dst, const TileGeom& gd, int64_t r0,
+void launch_convert_rows(const uint8_t* src, const TileGeom& gs, uint8_t* dst, const TileGeom& gd, int64_t i0,
                          int64_t nrows, hipStream_t s) {
   GOL_REQUIRE(gs.layout != gd.layout, "convert_rows: layouts must differ");
-  GOL_REQUIRE(gs.Wp() == gd.Wp() && gs.R() == gd.R() && gs.W % 32 == 0, "convert_rows: geometries differ");
-  GOL_REQUIRE(r0 >= 0 && nrows >= 0 && r0 + nrows <= gs.R(), "convert_rows: rows out of range");
+  GOL_REQUIRE(gs.H == gd.H && gs.W == gd.W && gs.W % 32 == 0, "convert_rows: geometries differ");
+  GOL_REQUIRE(i0 >= 0 && nrows >= 0 && i0 + nrows <= gs.H, "convert_rows: rows out of range");
+  GOL_REQUIRE(gs.cell0() % 32 == 0 && gd.cell0() % 32 == 0 && gs.pitch % 16 == 0 && gd.pitch % 16 == 0,
+              "convert_rows: owned words must be 16-byte aligned");
   if (nrows == 0) return;
-  const int64_t n = nrows * gs.Wp();
+  const int64_t ow = gs.W / 32;
+  const uint8_t* a = src + gs.offset(gs.row0() + i0, gs.cell0());
+  uint8_t* b = dst + gd.offset(gd.row0() + i0, gd.cell0());
   if (gs.layout == Layout::U8)
-    hipLaunchKernelGGL(pack_rows_k, dim3(grid_for(n, 1 << 16)), dim3(kBlock), 0, s, src, gs.pitch,
-                       reinterpret_cast<uint32_t*>(dst), gd.pitch / 4, r0, nrows, gs.Wp());
+    hipLaunchKernelGGL(pack_rows_k, dim3(grid_for(nrows * ow, 1 << 16)), dim3(kBlock), 0, s, a, gs.pitch,
+                       reinterpret_cast<uint32_t*>(b), gd.pitch / 4, nrows, ow);
   else
-    hipLaunchKernelGGL(unpack_rows_k, dim3(grid_for(n, 1 << 16)), dim3(kBlock), 0, s,
-                       reinterpret_cast<const uint32_t*>(src), gs.pitch / 4, dst, gd.pitch, r0, nrows, gs.Wp());
+    hipLaunchKernelGGL(unpack_rows_k, dim3(grid_for(nrows * ow, 1 << 16)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const uint32_t*>(a), gs.pitch / 4, b, gd.pitch, nrows, ow);
 }
 
 void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s) {

@@ -288,20 +288,20 @@ void CpuBackend::rotate_cols(const void* src, void* dst, const TileGeom& g, int6
   });
 }
 
-void CpuBackend::convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t r0,
+void CpuBackend::convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t i0,
                               int64_t n) {
   GOL_REQUIRE(gs.layout != gd.layout, "convert_rows: layouts must differ");
-  GOL_REQUIRE(gs.Wp() == gd.Wp() && gs.R() == gd.R() && gs.W % 32 == 0, "convert_rows: geometries differ");
-  GOL_REQUIRE(r0 >= 0 && n >= 0 && r0 + n <= gs.R(), "convert_rows: rows out of range");
+  GOL_REQUIRE(gs.H == gd.H && gs.W == gd.W && gs.W % 32 == 0, "convert_rows: geometries differ");
+  GOL_REQUIRE(i0 >= 0 && n >= 0 && i0 + n <= gs.H, "convert_rows: rows out of range");
   auto* s = static_cast<const uint8_t*>(src);
   auto* d = static_cast<uint8_t*>(dst);
-  const int64_t wp = gs.Wp();
+  const int64_t ow = gs.W / 32;
   const bool to_bits = gs.layout == Layout::U8;
   pool_.parallel_for(n, [&](int64_t b, int64_t e) {
-    for (int64_t i = r0 + b; i < r0 + e; ++i) {
-      const uint8_t* in = s + i * gs.pitch;
-      uint8_t* out = d + i * gd.pitch;
-      for (int64_t k = 0; k < wp; ++k) {
+    for (int64_t i = i0 + b; i < i0 + e; ++i) {
+      const uint8_t* in = s + gs.offset(gs.row0() + i, gs.cell0());
+      uint8_t* out = d + gd.offset(gd.row0() + i, gd.cell0());
+      for (int64_t k = 0; k < ow; ++k) {
         if (to_bits) {
           uint32_t w = 0;
           for (int j = 0; j < 32; ++j) w |= uint32_t(in[32 * k + j] != 0) << j;

@@ -551,11 +551,11 @@ class HipBackend final : public Backend {
     hipk::launch_rotate_cols(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), g, shift, stream_);
     HIP_CHECK(hipGetLastError());
   }
-  void convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t r0,
+  void convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t i0,
                     int64_t n) override {
     join_streams();
     GOL_ON_DEVICE();
-    hipk::launch_convert_rows(static_cast<const uint8_t*>(src), gs, static_cast<uint8_t*>(dst), gd, r0, n,
+    hipk::launch_convert_rows(static_cast<const uint8_t*>(src), gs, static_cast<uint8_t*>(dst), gd, i0, n,
                               stream_);
     HIP_CHECK(hipGetLastError());
   }

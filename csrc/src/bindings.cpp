@@ -256,6 +256,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("cols", &Engine::cols)
       .def_property_readonly("decomp", &Engine::decomp)
       .def_property_readonly("geom", &Engine::geom)
+      .def_property_readonly("compute_geom", &Engine::compute_geom)
       .def_property_readonly("epoch_depth", &Engine::epoch_depth)
       .def_property_readonly("tmax", &Engine::tmax)
       .def("overlap", &Engine::overlap)

@@ -1,6 +1,7 @@
 #include "gol/engine.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -66,9 +67,17 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // and several ranks 16T: half the RCCL exchanges (4 per 1000 generations),
   // each one latency-bound.
   const bool row_exchange = dec_.Py > 1 || cfg_.self_exchange;
-  // On bit words a byte-layout epoch also pays one pack and one unpack pass
-  // over the byte grid (~2.25 bytes per cell), so it runs 32T generations.
-  int D = cfg_.epoch > 0 ? cfg_.epoch : (via_bits_ ? 32 : tr_->size() > 1 || cfg_.self_exchange ? 16 : 8) * tmax_;
+  int D = cfg_.epoch > 0 ? cfg_.epoch : (tr_->size() > 1 || cfg_.self_exchange ? 16 : 8) * tmax_;
+  if (via_bits_ && cfg_.epoch <= 0) {
+    // On bit words a byte-layout epoch also pays one pack and one unpack pass
+    // over the byte grid (~2.25 B per cell: about 46 generations of the bit
+    // kernel at 1e14 cells/s and ~5 TB/s), while D halo rows add ~D/h of a
+    // generation to each: D = sqrt(46 h) balances the two (1152 on 32768
+    // rows at T = 12), within [8T, 96T].
+    const double h = double(min_tile_rows(dec_));
+    const int t = std::max(1, tmax_);
+    D = int(std::clamp<int64_t>(round_up(int64_t(std::sqrt(46.0 * h)), int64_t(t)), 8 * int64_t(t), 96 * int64_t(t)));
+  }
   if (dec_.Py > 1) D = int(std::min<int64_t>(D, min_tile_rows(dec_)));
   if (dec_.Px > 1) {
     int64_t cap = 32 * (min_tile_cols(dec_) / 32);
@@ -103,7 +112,14 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // fill); else D cells per side, 2D on the left for the drifting window.
   int hw = cols_filled_ ? int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32)) : 0;
   Extent r = rows(), c = cols();
-  g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
+  if (via_bits_) {
+    // The byte tile is storage only (owned cells, no halos); the epochs run
+    // on its bit-word image, which carries the halos.
+    g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), 0, 0);
+    gb_ = TileGeom::make(Layout::Bits, r.size(), c.size(), D_, hw);
+  } else {
+    g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
+  }
   // Experiment knob: extra bytes per padded row (multiple of 256).
   if (const char* pad = std::getenv("GOL_PITCH_PAD")) g_.pitch += 256 * (std::max(0, std::atoi(pad)) / 256);
   // Several ranks: every poll is a flag all-reduce on the compute stream
@@ -113,15 +129,16 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
 
   for (auto& b : buf_) b = be_->alloc(size_t(g_.bytes()));
   if (via_bits_) {
-    // The bit words live in the spare byte buffer (an eighth of its size per
-    // parity) unless a tiny tile's pitch rounding does not leave room.
-    gb_ = TileGeom::make(Layout::Bits, g_.H, g_.W, g_.Dv, g_.hw);
+    // The bit words live in the spare byte buffer (about an eighth of its
+    // size per parity) unless a small tile's halo rows or pitch rounding do
+    // not leave room.
     if (2 * gb_.bytes() > g_.bytes())
       for (auto& b : bitbuf_) b = be_->alloc(size_t(gb_.bytes()));
   }
   alive_dev_ = static_cast<uint32_t*>(be_->alloc(64));
   if (dec_.Px > 1) {
-    size_t n = size_t(g_.span_bytes(32 * int64_t(g_.hw)) * g_.H);
+    const TileGeom& gc = via_bits_ ? gb_ : g_;  // the tile whose halos are exchanged
+    size_t n = size_t(gc.span_bytes(32 * int64_t(gc.hw)) * gc.H);
     for (auto& b : colbuf_) b = be_->alloc(n);
   }
   // The overlapped schedule needs a non-empty interior (H > 2D).  It is
@@ -424,7 +441,7 @@ void Engine::epoch_via_bits(int64_t d) {
   trace::Range tr("gol.epoch_via_bits");
   void* bytes = buf_[cur_];
   void* t = phase_begin(nullptr);
-  be_->convert_rows(bytes, g_, bit_scratch(0), gb_, g_.row0(), g_.H);
+  be_->convert_rows(bytes, g_, bit_scratch(0), gb_, 0, g_.H);
   phase_end(kCompute, t, nullptr);
   halo_exchange_on(bit_scratch(0), gb_);
   int64_t a = 0;
@@ -438,7 +455,7 @@ void Engine::epoch_via_bits(int64_t d) {
     d -= T;
   }
   t = phase_begin(nullptr);
-  be_->convert_rows(bit_scratch(par), gb_, bytes, g_, g_.row0(), g_.H);
+  be_->convert_rows(bit_scratch(par), gb_, bytes, g_, 0, g_.H);
   phase_end(kCompute, t, nullptr);
 }
 

@@ -189,12 +189,12 @@ class Simulation:
 
     def describe(self) -> dict[str, Any]:
         d = self._eng.decomp
-        g = self._eng.geom
+        g = self._eng.compute_geom  # the tile the temporal blocks run on (halos)
         return {"backend": self.backend.name(), "transport": self.transport.name(),
                 "layout": self.config.resolved_layout(), "decomp": d.describe(),
                 "rank": self.rank, "ranks": d.nranks(), "tile_rows": g.H, "tile_cols": g.W,
                 "halo_rows": g.Dv, "halo_words": g.hw, "tmax": self._eng.tmax,
-                "epoch": self._eng.epoch_depth, "pitch": g.pitch, "overlap": self._eng.overlap(),
+                "epoch": self._eng.epoch_depth, "pitch": self._eng.geom.pitch, "overlap": self._eng.overlap(),
                 "graphs": self._eng.graphs(), "overlap_mode": self._eng.overlap_mode(),
                 "overlap_trial_ms_plain": self._eng.trial_ms_plain,
                 "overlap_trial_ms_early": self._eng.trial_ms_early,

@@ -13,3 +13,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-me
 rc=$?; echo "gpu tier rc=$rc"; grep -E "^FAILED|passed|failed" $O/pytest_gpu.log | tail -30; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc"; cut -c1-300 $O/bench.json
+[ $rc -eq 0 ] || exit $rc
+bash scripts/gpu_u8bits.sh

@@ -55,7 +55,9 @@ def test_epoch_depth_and_scratch_sharing(native):
     W, H = 256, 200
     g = random_grid(W, H, 8)
     sim = Simulation(u8_bits(W, H, gen_limit=1000, tmax=4), engine="cpu")
-    assert sim.epoch_depth == 32 * 4
+    assert sim.epoch_depth == 96  # sqrt(46 h) = 95.9 rounded up to a multiple of T, within [8T, 96T]
+    d = sim.describe()
+    assert d["halo_rows"] == 96 and sim.native_engine.geom.Dv == 0  # halos live on the bit tile only
     sim.load(g)
     sim.advance(300)
     mid = sim.tile()
