@@ -79,11 +79,12 @@ struct EngineConfig {
   bool self_exchange = false;
   // Compute representation of the byte layout (width % 32 == 0):
   //    1 bits: the byte-per-cell grid stays the storage (load / store / read-
-  //      out / drift rotation / alive count), but each epoch packs the owned
-  //      rows into bit words inside the spare byte buffer, exchanges or fills
-  //      the halos there (8x fewer bytes), runs the bit-sliced temporal
-  //      blocks, and unpacks the owned rows back: two byte passes per epoch
-  //      instead of one per temporal block (docs/PERFORMANCE.md);
+  //      out / drift rotation / alive count / checkpoints), but each run packs
+  //      the owned rows into bit words inside the spare byte buffer, its
+  //      epochs exchange or fill the halos there (8x fewer bytes) and run the
+  //      bit-sliced temporal blocks, and the run ends by unpacking the owned
+  //      rows back: two byte passes per run instead of one per temporal block
+  //      (docs/PERFORMANCE.md);
   //    0 bytes: temporal blocks on the byte grid itself (the byte kernels);
   //   -1 auto: bits on a device backend with the plain or auto schedule
   //      (GOL_U8_VIA_BITS=0|1 overrides), else bytes.
@@ -205,8 +206,11 @@ class Engine {
   void add_drift(int64_t cells);
   void exchange_columns(void* buf, const TileGeom& g);
   void halo_exchange_on(void* buf, const TileGeom& g);
-  // One byte-layout epoch on bit words (EngineConfig::u8_compute = 1).
+  // Byte layout on bit words (EngineConfig::u8_compute = 1): one epoch on
+  // the bit tile, and the per-run pack / unpack of the byte tile.
   void epoch_via_bits(int64_t d);
+  void pack_bits();
+  void unpack_bits();
   void* bit_scratch(int i) const;
   // Stream carrying this engine's transport operations (comm stream in the
   // early-boundary schedule, else the compute stream), and the two orderings.
@@ -275,6 +279,7 @@ class Engine {
   bool via_bits_ = false;    // byte layout computed on bit words (epoch_via_bits)
   TileGeom gb_;              // the tile in the bit layout (same rows, halos, words)
   void* bitbuf_[2] = {nullptr, nullptr};  // own bit scratch when the spare byte buffer cannot hold it
+  int bpar_ = 0;             // bit_scratch(bpar_) holds the current generation during a run
   bool poll_side_ = false;   // termination polls reduce on the comm stream (Transport::side_reduce)
   int64_t drift_ = 0;
   int64_t graph_drift_[2] = {0, 0};

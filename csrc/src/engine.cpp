@@ -1,7 +1,6 @@
 #include "gol/engine.hpp"
 
 #include <algorithm>
-#include <cmath>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -68,16 +67,6 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // each one latency-bound.
   const bool row_exchange = dec_.Py > 1 || cfg_.self_exchange;
   int D = cfg_.epoch > 0 ? cfg_.epoch : (tr_->size() > 1 || cfg_.self_exchange ? 16 : 8) * tmax_;
-  if (via_bits_ && cfg_.epoch <= 0) {
-    // On bit words a byte-layout epoch also pays one pack and one unpack pass
-    // over the byte grid (~2.25 B per cell: about 46 generations of the bit
-    // kernel at 1e14 cells/s and ~5 TB/s), while D halo rows add ~D/h of a
-    // generation to each: D = sqrt(46 h) balances the two (1152 on 32768
-    // rows at T = 12), within [8T, 96T].
-    const double h = double(min_tile_rows(dec_));
-    const int t = std::max(1, tmax_);
-    D = int(std::clamp<int64_t>(round_up(int64_t(std::sqrt(46.0 * h)), int64_t(t)), 8 * int64_t(t), 96 * int64_t(t)));
-  }
   if (dec_.Py > 1) D = int(std::min<int64_t>(D, min_tile_rows(dec_)));
   if (dec_.Px > 1) {
     int64_t cap = 32 * (min_tile_cols(dec_) / 32);
@@ -430,32 +419,40 @@ void* Engine::bit_scratch(int i) const {
   return static_cast<uint8_t*>(buf_[cur_ ^ 1]) + i * gb_.bytes();
 }
 
-// Byte-layout epoch on bit words.  The byte grid is read once (owned rows ->
-// bit words in the spare byte buffer) and written once (bit words -> owned
-// rows) per epoch; the halo exchange or fill and every temporal block run on
-// the bit tile, whose per-generation flags are those of the same cells.  The
-// byte grid's halo rows and columns are never read.  A drifting bit kernel
-// leaves the byte grid drifted by the same amount (a relabeling of columns,
-// rotated out by normalize() like the bit layout's).
+// Byte-layout epoch on bit words (run_impl packs the byte tile into
+// bit_scratch(bpar_) when a run starts and unpacks it when the run ends): the
+// halo exchange or fill and every temporal block run on the bit tile, whose
+// per-generation flags are those of the same cells.
 void Engine::epoch_via_bits(int64_t d) {
   trace::Range tr("gol.epoch_via_bits");
-  void* bytes = buf_[cur_];
-  void* t = phase_begin(nullptr);
-  be_->convert_rows(bytes, g_, bit_scratch(0), gb_, 0, g_.H);
-  phase_end(kCompute, t, nullptr);
-  halo_exchange_on(bit_scratch(0), gb_);
-  int64_t a = 0;
-  int par = 0;
+  halo_exchange_on(bit_scratch(bpar_), gb_);
+  int64_t a = D_ - d;  // a partial epoch's trapezoid starts d rows outside the owned rows
   while (d > 0) {
     const int T = pick_T(d);
-    add_drift(launch(bit_scratch(par), bit_scratch(par ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
-    par ^= 1;
+    add_drift(launch(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
+    bpar_ ^= 1;
     gen_ += T;
     a += T;
     d -= T;
   }
-  t = phase_begin(nullptr);
-  be_->convert_rows(bit_scratch(par), gb_, bytes, g_, 0, g_.H);
+}
+
+// The byte grid <-> its bit-word image in the spare byte buffer, once per
+// run: the byte grid is read once when a run starts and written once when it
+// ends, whatever its length, so every observation between runs (read-out,
+// alive count, drift rotation, checkpoints) sees the byte tile.  A drifting
+// bit kernel leaves the byte grid drifted by the same amount (a relabeling of
+// columns, rotated out by normalize() like the bit layout's).
+void Engine::pack_bits() {
+  bpar_ = 0;
+  void* t = phase_begin(nullptr);
+  be_->convert_rows(buf_[cur_], g_, bit_scratch(0), gb_, 0, g_.H);
+  phase_end(kCompute, t, nullptr);
+}
+
+void Engine::unpack_bits() {
+  void* t = phase_begin(nullptr);
+  be_->convert_rows(bit_scratch(bpar_), gb_, buf_[cur_], g_, 0, g_.H);
   phase_end(kCompute, t, nullptr);
 }
 
@@ -478,10 +475,13 @@ void Engine::run_epoch(int64_t d) {
   // The previous epoch ends here (its early rows have arrived).
   if (auto_overlap_) auto_mark();
   if (!sent_early) halo_exchange();
-  int64_t a = 0;
+  // A partial epoch (d < D) needs only d halo rows: its trapezoid starts d
+  // rows outside the owned rows, not D.
+  const bool full = d == D_;
+  int64_t a = D_ - d;
   while (d > 0) {
     const int T = pick_T(d);
-    if (d == T && early_ && send_next_ && a + T == D_)
+    if (d == T && early_ && send_next_ && full)
       last_block_early(T);
     else
       step_block(T, a + T, g_.R() - a - T);
@@ -745,6 +745,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   }
   be_->synchronize();
   auto t0 = std::chrono::steady_clock::now();
+  if (via_bits_) pack_bits();
 
   int64_t checked = start, found = -1;
   const int64_t poll_epochs = std::max<int64_t>(1, poll_gens_ / D_);
@@ -756,8 +757,10 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     send_next_ = gen_ + d < limit;
     if (use_graphs_ && d == D_) {
       // Full epochs replay a captured graph; the only per-epoch input is the
-      // device generation offset, advanced by the graph itself.
-      const int par = cur_;
+      // device generation offset, advanced by the graph itself.  Graphs are
+      // keyed by the parity of the buffer pair the epochs alternate over.
+      int& cur = via_bits_ ? bpar_ : cur_;
+      const int par = cur;
       if (!graph_[par]) {
         const int64_t k0 = launches_;
         const int64_t dr0 = drift_;
@@ -768,13 +771,13 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
         be_->i64_async(gen_dev_, D_, /*add=*/true);
         graph_[par] = be_->capture_end();
         capturing_ = false;
-        graph_flip_[par] = cur_ ^ par;
+        graph_flip_[par] = cur ^ par;
         graph_kernels_[par] = launches_ - k0;
         graph_drift_[par] = ((drift_ - dr0) % cfg_.W + cfg_.W) % cfg_.W;
         be_->graph_launch(graph_[par]);  // capture only recorded it
       } else {
         be_->graph_launch(graph_[par]);
-        cur_ ^= graph_flip_[par];
+        cur ^= graph_flip_[par];
         add_drift(graph_drift_[par]);
         gen_ += D_;
         ++exchanges_;
@@ -804,6 +807,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     }
   }
   if (have_pending) poll_check(pending, &found);
+  if (via_bits_) unpack_bits();
   // A poll issued just before an early stop may still run on the side stream;
   // the final alive reduction below uses the same communicator.
   if (poll_side_) be_->synchronize_stream(be_->comm_stream());

@@ -819,3 +819,21 @@ def test_u8_via_bits_subdomains_one_gpu(gpu, spec, P):
     grp.parallel(lambda s: s.advance(300))
     assert all(s.native_engine.via_bits for s in grp.sims)
     assert (grp.gather() == want).all()
+
+
+def test_u8_via_bits_graphs_and_chunked_runs(gpu):
+    """Captured epochs alternate over the bit-word pair (graphs keyed by its
+    parity); each run packs and unpacks once, so chunked runs and read-outs in
+    between stay exact."""
+    W, H = 4096, 1024
+    g = random_grid(W, H, 12)
+    sim = Simulation(LifeConfig(W, H, gen_limit=2000, layout="u8", u8_compute="bits", graphs="on",
+                                check_similarity=False), engine="hip")
+    assert sim.native_engine.graphs()
+    sim.load(g)
+    want = g
+    for n in (300, 517, 96):
+        sim.advance(n)
+        want = life_step_torch(want, n, device="cuda")
+        assert (sim.tile() == want).all(), n
+    assert sim.last_report.graph_launches > 0

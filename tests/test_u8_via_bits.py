@@ -50,14 +50,15 @@ def test_selection_rules(native, monkeypatch):
 
 
 def test_epoch_depth_and_scratch_sharing(native):
-    # Deep epochs (32T) by default; a large tile keeps its bit words in the
-    # spare byte buffer (results stay exact across many epochs and read-outs).
+    # The bit layout's epoch depth; a large tile keeps its bit words in the
+    # spare byte buffer (results stay exact across many epochs, runs and
+    # read-outs: each run packs the byte tile once and unpacks it once).
     W, H = 256, 200
     g = random_grid(W, H, 8)
     sim = Simulation(u8_bits(W, H, gen_limit=1000, tmax=4), engine="cpu")
-    assert sim.epoch_depth == 96  # sqrt(46 h) = 95.9 rounded up to a multiple of T, within [8T, 96T]
+    assert sim.epoch_depth == 8 * 4
     d = sim.describe()
-    assert d["halo_rows"] == 96 and sim.native_engine.geom.Dv == 0  # halos live on the bit tile only
+    assert d["halo_rows"] == 32 and sim.native_engine.geom.Dv == 0  # halos live on the bit tile only
     sim.load(g)
     sim.advance(300)
     mid = sim.tile()
