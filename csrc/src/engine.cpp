@@ -601,6 +601,7 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
 }
 
 void Engine::step_block(int T, int64_t row_lo, int64_t row_hi) {
+  GOL_REQUIRE(!via_bits_, "step_block: the byte tile has no halos when it computes on bit words (u8_compute)");
   add_drift(launch(buf_[cur_], buf_[cur_ ^ 1], g_, T, row_lo, row_hi, gen_));
   cur_ ^= 1;
   gen_ += T;
