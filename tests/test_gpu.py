@@ -832,8 +832,10 @@ def test_u8_via_bits_graphs_and_chunked_runs(gpu):
     assert sim.native_engine.graphs()
     sim.load(g)
     want = g
+    graphs = 0
     for n in (300, 517, 96):
         sim.advance(n)
+        graphs += sim.last_report.graph_launches  # a run shorter than an epoch replays none
         want = life_step_torch(want, n, device="cuda")
         assert (sim.tile() == want).all(), n
-    assert sim.last_report.graph_launches > 0
+    assert graphs > 0
