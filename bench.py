@@ -181,6 +181,8 @@ def main() -> int:
             # own "node" (socket transport over loopback).
             shared = True
             os.environ["NCCL_HOSTID"] = f"gol-bench-rank{rank}"
+            # Resident epochs need every CU of the device for one launch.
+            os.environ["GOL_RESIDENT"] = "0"
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         local = local % max(1, ndev)
 

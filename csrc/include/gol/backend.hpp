@@ -135,6 +135,16 @@ class Backend {
   virtual KernelChoice choose_kernel(Layout l, int64_t /*rows*/, int64_t /*cols*/, int tmax_req) const {
     return {tmax_req > 0 ? tmax_req : preferred_tmax(l), drifts(l)};
   }
+  // Resident epochs: the epoch depth D (> 16) at which this backend runs a
+  // whole epoch of a rows x cols whole-width bit tile as ONE launch that keeps
+  // the tile in the register file (BlockArgs::resident, any T <= D), or 0.
+  // D_req > 0: the caller's epoch depth; multi: halos come from other ranks.
+  virtual int resident_epoch(Layout /*l*/, int64_t /*rows*/, int64_t /*cols*/, int /*D_req*/,
+                             bool /*multi*/) const {
+    return 0;
+  }
+  // Allocates what resident launches on tile g need (outside any capture).
+  virtual void reserve_resident(const TileGeom& /*g*/) {}
   // Fewest output rows a run_block of T generations accepts (the pipelined
   // deep byte pass plans whole wave-pair groups); the engine keeps every
   // block at least this tall or uses a smaller T.

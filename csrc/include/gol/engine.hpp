@@ -163,6 +163,8 @@ class Engine {
   bool drifting() const { return drift_ok_; }
   // Whether byte-layout epochs compute on bit words (EngineConfig::u8_compute).
   bool via_bits() const { return via_bits_; }
+  // Whether every epoch runs as one resident launch (Backend::resident_epoch).
+  bool resident() const { return resident_; }
   // Rotates the drift out of the current buffer (owned rows); every
   // read-out (store_cells) does this first.
   void normalize();
@@ -277,6 +279,7 @@ class Engine {
   bool cols_filled_ = true; // column halos kept valid by fills (false: the backend wraps column reads)
   bool rows_wrapped_ = false; // single-rank torus read modulo its rows (no fills at all)
   bool via_bits_ = false;    // byte layout computed on bit words (epoch_via_bits)
+  bool resident_ = false;    // one launch per epoch, tile resident in registers (Backend::resident_epoch)
   TileGeom gb_;              // the tile in the bit layout (same rows, halos, words)
   void* bitbuf_[2] = {nullptr, nullptr};  // own bit scratch when the spare byte buffer cannot hold it
   int bpar_ = 0;             // bit_scratch(bpar_) holds the current generation during a run

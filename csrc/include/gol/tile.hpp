@@ -94,6 +94,9 @@ struct BlockArgs {
   // wrap column reads within the owned words instead of reading halo columns,
   // which it then neither reads nor writes.
   bool full_width = false;
+  // The engine runs resident epochs (Backend::resident_epoch): any T, one
+  // launch that keeps the tile in the register file.
+  bool resident = false;
 };
 
 }  // namespace gol

@@ -181,6 +181,54 @@ GOL_LIFE_VARIANT(launch_u8_w1_carry);
 GOL_LIFE_VARIANT(launch_bits_w1_add);
 GOL_LIFE_VARIANT(launch_u8_w1_add);
 
+// ---- Resident epoch kernel (life_resident_impl.hpp) ------------------------
+// A whole temporal block of T generations (a full halo epoch) in ONE launch,
+// with the tile held in the register file: one 1024-thread workgroup per CU
+// owns a column strip (one wave64 wide: 63 owned words + the left halo lane
+// of the adder window) x a band of rows, 16 waves stacked down the band,
+// RW rows per wave in VGPRs.  Waves trade their edge rows through LDS every
+// generation; workgroups trade k halo rows and the halo lane's words through
+// a global mirror every k generations (sc1 stores, per-workgroup flags).
+// Bit layout, whole-width tiles, adder window (the frame drifts T cells).
+struct ResidentParams {
+  const uint8_t* in;
+  uint8_t* out;
+  uint8_t* mirror[2];     // exchange copies by refresh parity (tile geometry)
+  uint32_t* flags;        // per region: last refresh published (zeroed per launch)
+  uint32_t* changed;      // changed[t] <-> generation gen_base + 1 + t (after gen_dev)
+  const int64_t* gen_dev;
+  int64_t gen_rel;
+  uint32_t* err;          // device error word (4: a workgroup gave up waiting)
+  int64_t pitch;
+  int64_t row0;           // padded row of extended row 0 (= row_lo - T)
+  int ext_rows;           // row_hi - row_lo + 2T
+  int T, k;               // generations; refresh period = halo rows per band side (<= 16)
+  int ww, own_w0;         // owned words per row (wrap width), first owned word of a padded row
+  int ns, sw;             // column strips, owned words per strip
+  int nb, band_rows, band_rem;  // row bands per strip (balanced)
+  int nreg;               // ns * nb workgroups
+  int spin_log2;
+  int probe;              // timing probe: 1 = no refresh waits (wrong rows), 0 = exact
+};
+
+struct ResidentPlan {
+  int ns = 0, sw = 0, nb = 0, band_rows = 0, band_rem = 0, rw = 0, k = 0;
+  int64_t ext_rows = 0;
+};
+
+// Register rows per wave the resident kernel is compiled for (ascending).
+extern const int kResidentRW[];
+extern const int kResidentRWCount;
+constexpr int kResidentWaves = 16;
+// Plan of a resident launch over a block (false: the tile does not fit the
+// register file at one workgroup per CU, or the block is not eligible).
+bool plan_resident(const BlockArgs& a, int cus, int k, ResidentPlan* pl);
+// Enqueues the launch (flags zeroed first); returns the drift (T).
+int launch_life_resident(const BlockArgs& a, const ResidentPlan& pl, const LifeTuning& tune, uint8_t* mirror0,
+                         uint8_t* mirror1, uint32_t* flags, int probe, hipStream_t s);
+// Per-RW kernels (life_resident_rw*.hip).
+void launch_resident_rw(int rw, const ResidentParams& p, hipStream_t s);
+
 // Single-generation LDS-tiled byte-layout kernel (life_step_lds.hip).
 void launch_life_step_lds(const BlockArgs& a, int lds_rows, bool wrap, hipStream_t stream);
 

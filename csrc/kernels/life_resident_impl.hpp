@@ -1,0 +1,309 @@
+// Resident epoch kernel: a whole halo epoch (T generations) of a per-rank
+// tile in one launch, the tile held in the register file.
+//
+// Why: the grouped temporal-blocking kernel (life_group_impl.hpp) streams
+// the tile through registers T <= 16 generations per launch and needs
+// segments of at least 2T rows per wave.  The 8-GPU rank tile (32768 x 4096)
+// then has too few segments for four waves per SIMD, the occupancy the adder
+// window needs, and runs at ~55 % of the full-grid per-cell rate
+// (docs/PERFORMANCE.md).  A 16 MiB bit tile is an eighth of the chip's
+// register file, so instead of streaming it, keep it resident:
+//
+//   * one 1024-thread workgroup per CU (LDS > 80 KB forces it), 255 of them
+//     for the 8-GPU tile: 17 column strips x 15 row bands;
+//   * a workgroup owns one column strip (64 lanes: the left halo lane of the
+//     one-sided adder window + up to 63 owned words) x one row band, plus k
+//     halo rows above and below; its 16 waves stack down the band, RW rows
+//     of one 32-bit word per lane each, in VGPRs (4 waves per SIMD);
+//   * every generation each wave updates its RW rows in place (adder window:
+//     15 full-rate VALU ops + 2 SALU shifts per row, no cross-lane data op)
+//     after trading its first and last row with the waves above and below
+//     through LDS (one barrier per generation);
+//   * every k generations the workgroups trade what the light cone has
+//     consumed: the k halo rows per side and the halo lane's word of every
+//     owned row, through a global mirror of the tile (sc1 write-through
+//     stores, s_waitcnt vmcnt(0), barrier, relaxed agent-scope flag; the
+//     consumer polls its 8 neighbours' flags and reads with sc1 loads - the
+//     no-acquire valid form of cdna_hip_programming.md §6 Guideline 16).
+//     The adder window consumes 2 cells of the halo lane per generation, so
+//     k <= 16; the halo rows erode one row per generation.
+//
+// Exactness: the rows a workgroup stores are its owned rows of the block's
+// output range [row_lo, row_hi); the per-generation change flags cover the
+// same rows and its owned words (one LDS slot per generation, flushed to the
+// engine's flag array every 64 generations).  The storage frame drifts one
+// cell right per generation like every adder-window kernel (kXlaneAdd).
+//
+// Deadlock freedom needs every workgroup co-resident: the grid is at most one
+// workgroup per CU and each holds 96 KB of LDS, so no CU takes two; every
+// wait is bounded and raises the device error word (4) instead of hanging.
+//
+// Reference: the per-generation MPI halo exchange + evolve of
+// src/game_mpi.c:392-402 and the CUDA evolve of src/game_cuda.cu:128-148.
+#pragma once
+
+#include "life_block_impl.hpp"
+
+namespace gol {
+namespace hipk {
+namespace lr {
+
+using lb::bop3;
+using lb::BufRsrc;
+using lb::kBufFlags;
+using lb::kCpolSc1;
+
+constexpr int kM = kResidentWaves;          // waves per workgroup, stacked down the band
+constexpr int kBndWords = 2 * kM * 2 * 64;   // [parity][wave][first/last row][lane]
+constexpr int kFlagWords = 128;              // [window parity][64 generations]
+// One workgroup per CU: more than half of the CU's 160 KB LDS (a small RW
+// alone would let the register file take two workgroups).
+constexpr int kLdsWords = 96 * 1024 / 4;
+constexpr int kOOR = int(0x80000000u);       // buffer offset past any record count: access dropped
+
+#ifndef GOL_RES_ROW_FENCE
+#define GOL_RES_ROW_FENCE 2
+#endif
+constexpr int kRowFence = GOL_RES_ROW_FENCE;  // rows between scheduling barriers (0: none)
+constexpr int kLoadBatch = 8;                 // refresh loads per batch (two batches in flight)
+constexpr int kTwoBodyMaxRW = 48;             // larger RW: one masked generation body
+
+struct HS {
+  uint32_t h0, h1, c;
+};
+
+// Horizontal 3-sum of a row word and its centre cell (adder window: cells
+// x-2, x-1, x at bit x; the centre is x-1).
+__device__ __forceinline__ HS hs(uint32_t x) {
+  uint32_t l1, l2;
+  lb::adder_window(x, l1, l2);
+  return {bop3<tt::XOR3>(l2, l1, x), bop3<tt::MAJ>(l2, l1, x), l1};
+}
+
+// One generation of the wave's RW rows, in place; returns the OR of
+// (new ^ old) over the rows [i_lo, i_hi) (all rows unless MASKED).
+template <int RW, bool MASKED>
+__device__ __forceinline__ uint32_t gen_rows(uint32_t (&s)[RW], uint32_t above, uint32_t below, int i_lo,
+                                             int i_hi) {
+  uint32_t acc = 0;
+  HS prev = hs(above), cur = hs(s[0]);
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const HS nxt = hs(i + 1 < RW ? s[i + 1] : below);
+    const uint32_t n = lb::rule(prev.h0, prev.h1, cur.h0, cur.h1, nxt.h0, nxt.h1, cur.c);
+    if constexpr (MASKED) {
+      const uint32_t x = (i >= i_lo && i < i_hi) ? cur.c : n;  // wave-uniform select
+      acc = bop3<tt::OR_XOR>(acc, n, x);
+    } else {
+      acc = bop3<tt::OR_XOR>(acc, n, cur.c);
+    }
+    // Opaque def: otherwise the flag ORs of many rows are deferred into one
+    // late tree that keeps every row's old centre word live.
+    asm("" : "+v"(acc));
+    s[i] = n;
+    prev = cur;
+    cur = nxt;
+    // Rows in order: hoisting later rows' window sums would hold three VGPRs
+    // per row (the scheduler has the whole 128-VGPR budget of four waves per
+    // SIMD to fill); the four waves of a SIMD supply the overlap instead.
+    if constexpr (kRowFence > 0)
+      if ((i + 1) % kRowFence == 0) __builtin_amdgcn_sched_barrier(0);
+  }
+  return acc;
+}
+
+// Wave 0 copies one window of generation flags to the engine's array.
+__device__ __forceinline__ void flush_flags(uint32_t* lflag, uint32_t* changed, int win, int g0, int n, int lane) {
+  if (lane < n) {
+    if (lflag[win * 64 + lane]) changed[g0 + lane] = 1u;
+    lflag[win * 64 + lane] = 0u;
+  }
+}
+
+template <int RW>
+__global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p) {
+  __shared__ uint32_t lds[kLdsWords];
+  uint32_t* const bnd = lds;
+  uint32_t* const lflag = lds + kBndWords;
+  const int lane = int(threadIdx.x & 63);
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+
+  // XCD-aware region map: dispatch puts block b on XCD b % 8, so XCD x gets a
+  // contiguous run of regions (strip-major: a strip's bands are neighbours).
+  const int G = p.nreg, b = int(blockIdx.x);
+  const int per = G >> 3, rem = G & 7, xcd = b & 7;
+  const int j = xcd * per + min(xcd, rem) + (b >> 3);
+  const int strip = j / p.nb, band = j - strip * p.nb;
+
+  // Columns: lane 0 is the halo word left of the strip (the adder window
+  // reads nothing to its right), lanes 1..own_cnt own words.
+  const int own_cnt = min(p.sw, p.ww - strip * p.sw);
+  const int lc = strip * p.sw - 1 + lane;
+  const bool own = lane >= 1 && lane <= own_cnt;
+  const bool last_own = lane == own_cnt;
+  const int vw = 4 * (p.own_w0 + ((lc % p.ww) + p.ww) % p.ww);
+
+  // Rows (extended coordinates, 0 = row_lo - T): the band owns [q0, q0 + cnt);
+  // register row i of wave w holds row eb + i.
+  const int q0 = band * p.band_rows + min(band, p.band_rem);
+  const int cnt = p.band_rows + (band < p.band_rem ? 1 : 0);
+  const int eb = q0 - p.k + w * RW;
+  const int olo = max(q0, p.T), ohi = min(q0 + cnt, p.ext_rows - p.T);  // owned rows of the output range
+  const int i_lo = min(max(olo - eb, 0), RW), i_hi = min(max(ohi - eb, 0), RW);
+  const bool outw = i_lo < i_hi;
+  const bool partial = outw && (i_lo > 0 || i_hi < RW);
+  const int ip = int(p.pitch);
+  const int64_t base = p.row0 * p.pitch;
+  const int range = int(int64_t(p.ext_rows) * p.pitch);
+
+  uint32_t s[RW];
+  {
+    const BufRsrc rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.in) + base, short(0), range, kBufFlags);
+#pragma unroll
+    for (int i = 0; i < RW; ++i) s[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, (eb + i) * ip + vw, 0, 0);
+  }
+  if (threadIdx.x < kFlagWords) lflag[threadIdx.x] = 0u;
+  uint32_t* changed = p.changed;
+  if (changed && p.gen_dev) changed += *p.gen_dev + p.gen_rel;
+  const bool rec = changed != nullptr && outw;
+
+  for (int t = 0; t < p.T; ++t) {
+    if (t > 0 && t % p.k == 0 && !p.probe) {
+      // ---- refresh m: publish, signal, wait for the 8 neighbours, read ----
+      const uint32_t m = uint32_t(t / p.k);
+      // Opaque copies of the row geometry (see the generation step below).
+      int e0 = __builtin_amdgcn_readfirstlane(eb), qa = __builtin_amdgcn_readfirstlane(q0);
+      int nc = __builtin_amdgcn_readfirstlane(cnt), kk = __builtin_amdgcn_readfirstlane(p.k);
+      int ne = __builtin_amdgcn_readfirstlane(p.ext_rows), ipr = ip;
+      asm volatile("" : "+s"(e0), "+s"(qa), "+s"(nc), "+s"(kk), "+s"(ne), "+s"(ipr));
+      const BufRsrc mr = __builtin_amdgcn_make_buffer_rsrc(p.mirror[m & 1] + base, short(0), range, kBufFlags);
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        const int q = e0 + i - qa;
+        const bool orow = q >= 0 && q < nc;
+        const bool edge = orow && (q < kk || q >= nc - kk);
+        const bool ok = edge ? own : (orow && last_own);
+        __builtin_amdgcn_raw_buffer_store_b32(s[i], mr, ok ? (e0 + i) * ipr + vw : kOOR, 0, kCpolSc1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(p.flags + j, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w == 0) {
+        const int nn = lane < 4 ? lane : lane + 1;  // 3 x 3 neighbourhood without its centre
+        const int nbd = band + nn / 3 - 1;
+        const bool valid = lane < 8 && nbd >= 0 && nbd < p.nb;
+        const int nst = (strip + nn % 3 - 1 + p.ns) % p.ns;
+        const uint32_t* f = p.flags + (valid ? nst * p.nb + nbd : 0);
+        bool done = !valid;
+        const int spins = 1 << p.spin_log2;
+        for (int it = 0; it < spins; ++it) {
+          if (!done) done = int(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - m) >= 0;
+          if (__all(done)) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (!__all(done) && lane == 0 && p.err)
+          __hip_atomic_store(p.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __syncthreads();
+      // Fresh opaque copies: per-row values of the publish loop would stay
+      // live across the wait (RW SGPRs and offsets).
+      asm volatile("" : "+s"(e0), "+s"(qa), "+s"(nc), "+s"(kk), "+s"(ne), "+s"(ipr));
+      // Loads in batches of kLoadBatch rows, two batches in flight: every
+      // load needs a temporary until its select, and RW of them would not
+      // fit beside the RW rows of state.
+      constexpr int kNB = (RW + kLoadBatch - 1) / kLoadBatch;
+      uint32_t v[kNB][kLoadBatch];
+#pragma unroll
+      for (int bb = 0; bb <= kNB; ++bb) {
+        if (bb < kNB) {
+#pragma unroll
+          for (int jj = 0; jj < kLoadBatch; ++jj) {
+            const int i = bb * kLoadBatch + jj;
+            if (i < RW) {
+              const int e = e0 + i, q = e - qa;
+              const bool hrow = e >= 0 && e < ne && ((q >= -kk && q < 0) || (q >= nc && q < nc + kk));
+              const bool take = hrow || (q >= 0 && q < nc && lane == 0);
+              v[bb][jj] = __builtin_amdgcn_raw_buffer_load_b32(mr, take ? e * ipr + vw : kOOR, 0, kCpolSc1);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (bb > 0) {
+#pragma unroll
+          for (int jj = 0; jj < kLoadBatch; ++jj) {
+            const int i = (bb - 1) * kLoadBatch + jj;
+            if (i < RW) {
+              const int e = e0 + i, q = e - qa;
+              const bool hrow = e >= 0 && e < ne && ((q >= -kk && q < 0) || (q >= nc && q < nc + kk));
+              const bool take = hrow || (q >= 0 && q < nc && lane == 0);
+              s[i] = take ? v[bb - 1][jj] : s[i];
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // ---- one generation: trade edge rows with the waves above / below ----
+    uint32_t* const slot = bnd + (t & 1) * (kM * 128);
+    slot[w * 128 + lane] = s[0];
+    slot[w * 128 + 64 + lane] = s[RW - 1];
+    __syncthreads();
+    if (t > 0 && (t & 63) == 0 && w == 0 && changed) flush_flags(lflag, changed, ((t >> 6) - 1) & 1, t - 64, 64, lane);
+    const uint32_t up = slot[max(w - 1, 0) * 128 + 64 + lane];
+    const uint32_t dn = slot[min(w + 1, kM - 1) * 128 + lane];
+    const uint32_t above = w > 0 ? up : 0u;
+    const uint32_t below = w < kM - 1 ? dn : 0u;
+    // Opaque copies: the per-row conditions are re-derived each generation
+    // instead of being hoisted out of the loop as RW lane masks (SGPR spills).
+    int lo = __builtin_amdgcn_readfirstlane(i_lo), hi = __builtin_amdgcn_readfirstlane(i_hi);
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    // Two bodies (masked for the few waves whose rows straddle the output
+    // range) cost a second copy of the rows in registers; above 48 rows per
+    // wave that would spill, so one masked body serves every wave there
+    // (one more VALU op per row).
+    uint32_t acc;
+    if constexpr (RW > kTwoBodyMaxRW) {
+      acc = gen_rows<RW, true>(s, above, below, lo, hi);
+    } else {
+      acc = partial ? gen_rows<RW, true>(s, above, below, lo, hi) : gen_rows<RW, false>(s, above, below, 0, RW);
+    }
+    if (rec) {
+      const bool any = __ballot(own && acc != 0u) != 0;
+      if (any && lane == 0) lflag[((t >> 6) & 1) * 64 + (t & 63)] = 1u;
+    }
+  }
+  __syncthreads();
+  if (w == 0 && changed && p.T > 0) {
+    const int g0 = (p.T - 1) & ~63;
+    flush_flags(lflag, changed, ((p.T - 1) >> 6) & 1, g0, p.T - g0, lane);
+  }
+  // Opaque copies again: offsets derived from eb before the loop would stay
+  // live through it (RW VGPRs).
+  int ef = __builtin_amdgcn_readfirstlane(eb), flo = __builtin_amdgcn_readfirstlane(i_lo);
+  int fhi = __builtin_amdgcn_readfirstlane(i_hi), ipf = ip;
+  asm volatile("" : "+s"(ef), "+s"(flo), "+s"(fhi), "+s"(ipf));
+  const BufRsrc ro = __builtin_amdgcn_make_buffer_rsrc(p.out + base, short(0), range, kBufFlags);
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const bool ok = own && i >= flo && i < fhi;
+    __builtin_amdgcn_raw_buffer_store_b32(s[i], ro, ok ? (ef + i) * ipf + vw : kOOR, 0, 0);
+  }
+}
+
+template <int RW>
+void launch_resident(const ResidentParams& p, hipStream_t s) {
+  hipLaunchKernelGGL((life_resident_kernel<RW>), dim3(unsigned(p.nreg)), dim3(64 * kM), 0, s, p);
+}
+
+}  // namespace lr
+}  // namespace hipk
+}  // namespace gol
+
+#define GOL_RESIDENT_RW(RW)                                                   \
+  namespace gol {                                                             \
+  namespace hipk {                                                            \
+  namespace lr {                                                              \
+  template void launch_resident<RW>(const ResidentParams&, hipStream_t);      \
+  }                                                                           \
+  }                                                                           \
+  }

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <deque>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -44,9 +45,24 @@ int env_int(const char* name, int dflt) {
   DeviceScope device_scope_(dev_);   \
   if (check_dev_) assert_current(__func__)
 
+// Live HIP backends per device in this process: resident epochs need every
+// CU of the device for one launch, so they are off when ranks share a GPU.
+std::mutex& live_mu() {
+  static std::mutex m;
+  return m;
+}
+std::map<int, int>& live_backends() {
+  static std::map<int, int> n;
+  return n;
+}
+
 class HipBackend final : public Backend {
  public:
   explicit HipBackend(int device) : dev_(device) {
+    {
+      std::lock_guard<std::mutex> lk(live_mu());
+      ++live_backends()[device];
+    }
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
     GOL_REQUIRE(n > 0, "no HIP device available");
@@ -75,6 +91,13 @@ class HipBackend final : public Backend {
     tune_.wrap = env_int("GOL_WRAP", 1) != 0;
     tune_.fold = env_int("GOL_FOLD", 1) != 0;
     chain_mode_ = env_int("GOL_CHAIN", -1);
+    // Resident epochs (life_resident_impl.hpp): GOL_RESIDENT -1 auto, 0 off,
+    // 1 on where the tile fits; GOL_RES_K refresh period / halo rows (<= 16);
+    // GOL_RES_D epoch depth; GOL_RES_PROBE=1 timing probe without refreshes.
+    resident_mode_ = env_int("GOL_RESIDENT", 0);
+    resident_k_ = std::min(16, std::max(1, env_int("GOL_RES_K", 8)));
+    resident_D_ = env_int("GOL_RES_D", 0);
+    resident_probe_ = env_int("GOL_RES_PROBE", 0);
     u8_pipe_ = env_int("GOL_U8_PIPE", 1) != 0;
     // Linked launches: consecutive grouped launches of an epoch overlap on
     // two streams, ordered by per-group completion words (LifeBlockParams::
@@ -132,6 +155,10 @@ class HipBackend final : public Backend {
     };
   }
   ~HipBackend() override {
+    {
+      std::lock_guard<std::mutex> lk(live_mu());
+      --live_backends()[dev_];
+    }
     DeviceScope device_scope(dev_);
     if (link_.stream[1]) hipStreamSynchronize(link_.stream[1]);
     if (stream_) hipStreamSynchronize(stream_);
@@ -169,7 +196,10 @@ class HipBackend final : public Backend {
     hipk::LifeTuning t = tune_;
     t.chain = chain_mode_;
     return "hip:" + std::to_string(dev_) + ":" + arch_ + " [" + hipk::life_block_variant(Layout::Bits, t) +
-           "; " + hipk::life_block_variant(Layout::U8, t) + "]";
+           "; " + hipk::life_block_variant(Layout::U8, t) + "]" +
+           (resident_mode_ ? " resident=" + std::string(resident_mode_ < 0 ? "auto" : "on") + " k=" +
+                                 std::to_string(resident_k_)
+                           : "");
   }
   int preferred_tmax(Layout l) const override { return hipk::life_block_max_T(l, tune_); }
   bool is_device() const override { return true; }
@@ -391,6 +421,23 @@ class HipBackend final : public Backend {
     if (chain_mode_) {  // chained groups: own stream only, never inside a graph capture
       tune_.chain_ok = (!a.stream || a.stream == stream_) && !capturing && !linkable;
     }
+    if (a.resident) {  // the engine runs this epoch as one resident launch
+      join_streams();
+      ++launches_;
+      hipk::ResidentPlan pl;
+      GOL_REQUIRE(hipk::plan_resident(a, cus_, resident_k_, &pl),
+                  "resident kernel: block of " + std::to_string(a.row_hi - a.row_lo) + " rows x T = " +
+                      std::to_string(a.T) + " does not fit (Backend::resident_epoch)");
+      reserve_resident(a.g);
+      const size_t mb = size_t(a.g.bytes());
+      auto* m0 = reinterpret_cast<uint8_t*>(tune_.chain_mem(5, mb));
+      auto* m1 = reinterpret_cast<uint8_t*>(tune_.chain_mem(6, mb));
+      uint32_t* fl = tune_.chain_mem(7, size_t(pl.ns) * pl.nb * 4);
+      hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
+      const int drift = hipk::launch_life_resident(a, pl, tune_, m0, m1, fl, resident_probe_, s);
+      HIP_CHECK(hipGetLastError());
+      return drift;
+    }
     if (trace_at_ >= 0 && launches_ == trace_at_) {
       join_streams();
       tune_.link = nullptr;
@@ -539,6 +586,39 @@ class HipBackend final : public Backend {
     }
     return k;
   }
+  // Resident epochs: on when forced (GOL_RESIDENT=1) and the plan fits;
+  // auto (-1) also needs the tile to leave the grouped kernel short of four
+  // waves per SIMD (the adder window's occupancy), where the resident launch
+  // measured faster (docs/PERFORMANCE.md, "Resident epochs").
+  int resident_epoch(Layout l, int64_t rows, int64_t cols, int D_req, bool multi) const override {
+    if (resident_mode_ == 0 || l != Layout::Bits || !tune_.wrap || cols % 32 != 0 || tune_.wpl_bits >= 2) return 0;
+    {
+      std::lock_guard<std::mutex> lk(live_mu());
+      if (live_backends()[dev_] > 1) return 0;  // ranks share this GPU: a launch may not get every CU
+    }
+    if (tune_.xlane != hipk::kXlaneAuto && tune_.xlane != hipk::kXlaneAdd) return 0;
+    const int D = D_req > 0 ? D_req : resident_D_ > 0 ? resident_D_ : multi ? 256 : 128;
+    if (D <= 16) return 0;
+    BlockArgs a;
+    a.g = TileGeom::make(Layout::Bits, rows, cols, D, 0);
+    a.row_lo = D;
+    a.row_hi = D + rows;
+    a.T = D;
+    a.full_width = a.allow_drift = true;
+    hipk::ResidentPlan pl;
+    if (!hipk::plan_resident(a, cus_, resident_k_, &pl)) return 0;
+    if (resident_mode_ < 0) {
+      const int64_t strips = ceil_div(ceil_div(cols, int64_t(32)) + 16, int64_t(63));
+      if (strips * (rows / 24) >= int64_t(16) * cus_) return 0;  // the grouped adder kernel fills 4 waves/SIMD
+    }
+    return D;
+  }
+  void reserve_resident(const TileGeom& g) override {
+    const size_t mb = size_t(g.bytes());
+    tune_.chain_mem(5, mb);
+    tune_.chain_mem(6, mb);
+    tune_.chain_mem(7, size_t(cus_) * 4);
+  }
   int64_t min_block_rows(Layout l, int T) const override {
     return l == Layout::U8 && T > 32 ? int64_t(4) * (2 * T + 2) + T - 1 : 1;
   }
@@ -600,6 +680,8 @@ class HipBackend final : public Backend {
                                             std::to_string(err_host_[2]) + "]"
                                       : "";
       fail(std::string(e == 2   ? "life_group kernel (chained groups): a wave gave up waiting for the group below" + diag
+                       : e == 4 ? "life_resident kernel: a workgroup gave up waiting for its neighbours' halo rows "
+                                  "(not every workgroup was resident: another kernel on this GPU?)"
                        : e == 3 ? "life_group kernel (linked launches): a group gave up waiting for the previous "
                                   "launch's rows"
                                 : "life_short kernel: a wave gave up waiting for its neighbour's LDS rows") +
@@ -724,8 +806,11 @@ class HipBackend final : public Backend {
   hipStream_t comm_ = nullptr;
   void* scratch_ = nullptr;  // split-schedule boundary states
   size_t scratch_bytes_ = 0;
-  void* chain_[5] = {};  // chained groups: flags, slots; linked launches: 3 x completion words (chain_mem)
-  size_t chain_bytes_[5] = {};
+  // chain_mem: chained groups' flags, slots; linked launches' 3 x completion
+  // words; resident epochs' two mirrors and per-workgroup flags (5..7).
+  void* chain_[8] = {};
+  size_t chain_bytes_[8] = {};
+  int resident_mode_ = 0, resident_k_ = 8, resident_D_ = 0, resident_probe_ = 0;
   hipk::LinkState link_;  // linked launches (GOL_LINK)
   bool link_on_ = false;
   uint32_t chain_seq_ = 0;

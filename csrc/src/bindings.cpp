@@ -269,6 +269,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("drift", &Engine::drift)
       .def_property_readonly("drifting", &Engine::drifting)
       .def_property_readonly("via_bits", &Engine::via_bits)
+      .def_property_readonly("resident", &Engine::resident)
       .def("normalize", &Engine::normalize, py::call_guard<py::gil_scoped_release>())
       .def("current_buffer", [](const Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })
       .def("load_cells",

@@ -85,10 +85,23 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     if (row_exchange && h >= 2 * int64_t(D_) + 1) min_rows = std::min({h, int64_t(D_), h - 2 * int64_t(D_)});
     while (tmax_ > 1 && be_->min_block_rows(cl, tmax_) > min_rows) tmax_ = pick_T(tmax_ - 1);
   }
+  // Resident epochs (Backend::resident_epoch): a whole-width bit tile small
+  // enough for the register file runs each epoch as one launch (no T <= 16
+  // blocks, no segment triangles); the same decision on every rank (smallest
+  // tile).  Not with the overlapped schedules, which split epochs into blocks.
+  if (cl == Layout::Bits && dec_.Px == 1 && cfg_.W % 32 == 0 && cfg_.overlap != 1 && cfg_.overlap != 2 &&
+      be_->wraps_columns(cl)) {
+    const int Dr = be_->resident_epoch(cl, ceil_div(dec_.H, int64_t(dec_.Py)), cfg_.W, cfg_.epoch, row_exchange);
+    if (Dr > 16 && (dec_.Py == 1 || Dr <= min_tile_rows(dec_))) {
+      resident_ = true;
+      D_ = Dr;
+      tmax_ = Dr;
+    }
+  }
   // A drifting kernel (one-sided window, Backend::drifts) consumes 2 cells of
   // left halo per generation and none on the right; it needs the tile to be
   // the whole torus width so that the drift is a relabeling of columns.
-  drift_ok_ = kc.drift && dec_.Px == 1 && cfg_.W % 32 == 0;
+  drift_ok_ = (kc.drift || resident_) && dec_.Px == 1 && cfg_.W % 32 == 0;  // resident: adder window
   // Whole-width tiles on a backend that wraps column reads (lane_cols in the
   // HIP kernels) never read their halo columns: no column fills.
   cols_filled_ = !(dec_.Px == 1 && cfg_.W % 32 == 0 && be_->wraps_columns(cl));
@@ -135,8 +148,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // epoch), which on the 32768 x 4096 per-rank tile cost 4x more than the
   // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
   const bool interior = min_tile_rows(dec_) >= 2 * int64_t(D_) + 1;  // on every rank
-  overlap_ = row_exchange && cfg_.overlap == 2 && interior && !via_bits_;
-  const bool early_ok = row_exchange && dec_.Px == 1 && interior && !via_bits_;
+  overlap_ = row_exchange && cfg_.overlap == 2 && interior && !via_bits_ && !resident_;
+  const bool early_ok = row_exchange && dec_.Px == 1 && interior && !via_bits_ && !resident_;
   early_ = early_ok && cfg_.overlap == 1;
   // With the early-boundary schedule every transport operation runs on the
   // comm stream (one stream per communicator, in issue order), so the flag
@@ -157,6 +170,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
+  if (resident_) be_->reserve_resident(via_bits_ ? gb_ : g_);  // before any capture
   if (use_graphs_) early_ = comm_route_ = false;  // captured epochs stay on one stream
   // Overlap auto: measure both schedules on the real ranks (see auto_choose).
   // The one-GPU RCCL rehearsal measured the early-boundary schedule slower
@@ -252,6 +266,7 @@ int64_t Engine::alive_count() {
 }
 
 int Engine::pick_T(int64_t remaining) const {
+  if (resident_) return int(std::min<int64_t>(remaining, tmax_));  // any T: one launch per epoch
   for (int t : kTSizes)
     if (t <= tmax_ && t <= remaining) return t;
   return 1;
@@ -591,6 +606,7 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   a.full_width = dec_.Px == 1 && cfg_.W % 32 == 0;
   a.wrap_rows = rows_wrapped_;
   a.stream = stream;
+  a.resident = resident_;
   a.dual_offset = dual_offset;
   a.prio_boost = prio_boost;
   void* t = phase_begin(stream);

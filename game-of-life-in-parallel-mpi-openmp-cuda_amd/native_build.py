@@ -35,9 +35,11 @@ LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp",
                  "u8_w1_carry", "u8_w1_add",
                  *[f"u8_w1_{x}_t{t}" for x in ("dpp", "carry", "add") for t in (24, 32)],  # deep byte passes
                  "u8_w1_dpp_t48"]  # pipelined wave pairs (life_pipe_impl.hpp)
+RESIDENT_TUS = 7  # life_resident_rw0..6.hip: the resident kernel's rows-per-wave instantiations
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
             *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
-            "kernels/tile_ops.hip"]
+            "kernels/tile_ops.hip", "kernels/life_resident.hip",
+            *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)]]
 BIND_SRCS = ["src/bindings.cpp"]
 CLI_MAIN = "tools/gol_main.cpp"
 GEN_MAIN = "tools/gol_gen.cpp"
@@ -121,7 +123,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     todo = [s for s in srcs if force or _needs(objs[s], CSRC / s, hdr)]
     # Longest compiles first (deep byte passes, then the kernel variants), so
     # the pool does not end on one long translation unit.
-    todo.sort(key=lambda s: 0 if any(f"_t{t}" in s for t in (24, 32, 48, 64)) else 1 if "life_block_" in s else 2)
+    todo.sort(key=lambda s: 0 if any(f"_t{t}" in s for t in (24, 32, 48, 64)) else
+              1 if ("life_block_" in s or "life_resident_rw" in s) else 2)
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]

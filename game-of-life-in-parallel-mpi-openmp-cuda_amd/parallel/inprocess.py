@@ -31,10 +31,12 @@ class InProcessGroup:
         devs = list(devices) if devices else [0]
         self.sims: list[Simulation] = []
         self.backends = []
-        for r in range(self.nranks):
-            be = make_backend(engine, devs[r % len(devs)], threads_per_rank)
+        # Every backend before any engine: an engine's schedule may depend on
+        # how many ranks share its device (resident epochs need a whole GPU),
+        # and all ranks must take the same decision.
+        self.backends = [make_backend(engine, devs[r % len(devs)], threads_per_rank) for r in range(self.nranks)]
+        for r, be in enumerate(self.backends):
             tr = C.thread_transport(self.hub, r, be)
-            self.backends.append(be)
             self.sims.append(Simulation(config, transport=tr, backend=be))
 
     def parallel(self, fn: Callable[[Simulation], object]) -> list:

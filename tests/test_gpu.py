@@ -839,3 +839,107 @@ def test_u8_via_bits_graphs_and_chunked_runs(gpu):
         want = life_step_torch(want, n, device="cuda")
         assert (sim.tile() == want).all(), n
     assert graphs > 0
+
+
+# ---- resident epochs (life_resident_impl.hpp) -------------------------------
+
+def _resident_sim(monkeypatch, W, H, k=8, D=0, rccl_self=False, **kw):
+    import gc
+
+    from gol_amd import make_backend, native
+    gc.collect()  # a stale backend on the device would turn resident epochs off
+    monkeypatch.setenv("GOL_RESIDENT", "1")
+    monkeypatch.setenv("GOL_RES_K", str(k))
+    if D:
+        monkeypatch.setenv("GOL_RES_D", str(D))
+    cfg = LifeConfig(W, H, self_exchange=rccl_self, **kw)
+    if rccl_self:  # the multi-rank epoch schedule against a 1-rank RCCL communicator
+        C = native()
+        sim = Simulation(cfg, transport=C.rccl_transport(C.rccl_unique_id(), 0, 1, 0), backend=make_backend("hip", 0))
+    else:
+        sim = Simulation(cfg, engine="hip")
+    assert sim.native_engine.resident, "resident epochs did not engage"
+    return sim
+
+
+@pytest.mark.parametrize("W,H,k,D", [(4096, 1024, 8, 0), (32 * 200, 700, 16, 48), (2048, 333, 4, 64),
+                                     (32768, 512, 8, 128), (96, 70, 8, 40)])
+def test_resident_epochs_vs_torch(gpu, monkeypatch, W, H, k, D):
+    """Whole epochs in one launch with the tile in registers: bands, strips,
+    halo refreshes every k generations and the drifting frame, exact against
+    the fp32 oracle over several epochs (and a partial one)."""
+    g = random_grid(W, H, W + H + k)
+    sim = _resident_sim(monkeypatch, W, H, k=k, D=D, gen_limit=400, check_similarity=False)
+    sim.load(g)
+    sim.advance(301)
+    assert (sim.tile() == life_step_torch(g, 301, device="cuda")).all()
+
+
+def test_resident_chunked_runs_and_rehearsal(gpu, monkeypatch):
+    """Chunked runs (partial epochs at every chunk end) and the multi-rank
+    epoch schedule against a self-exchanging transport (deep halo rows)."""
+    W, H = 8192, 1536
+    g = random_grid(W, H, 5)
+    for self_exchange in (False, True):
+        sim = _resident_sim(monkeypatch, W, H, gen_limit=2000, check_similarity=False, rccl_self=self_exchange)
+        sim.load(g)
+        want = g
+        for n in (300, 517, 96):
+            sim.advance(n)
+            want = life_step_torch(want, n, device="cuda")
+            assert (sim.tile() == want).all(), (self_exchange, n)
+        del sim
+
+
+@pytest.mark.parametrize("case", [c for c in CONVERGING if c[0] % 32 == 0] + [(256, 512, 77, 0.5)])
+def test_resident_termination_matches_reference(gpu, monkeypatch, case):
+    """The per-generation change flags of resident launches (one LDS slot per
+    generation, flushed every 64) give the reference's Generations count."""
+    W, H, seed, density = case
+    g = random_grid(W, H, seed, density)
+    ref, gens, _ = reference_run(g)
+    sim = _resident_sim(monkeypatch, W, H, D=40, poll_gens=80)
+    sim.load(g)
+    rep = sim.run()
+    assert rep.generations == gens
+    assert (sim.tile() == ref).all()
+
+
+def test_resident_termination_large_still_life(gpu, monkeypatch):
+    """A soup that dies out inside a long epoch: the first unchanged
+    generation lies deep inside one resident launch."""
+    W, H = 4096, 2048
+    g = np.zeros((H, W), np.uint8)
+    g[100:102, 200:202] = 1          # block (still life)
+    g[1000, 3000:3003] = 1           # blinker: similarity every 2 generations
+    sim = _resident_sim(monkeypatch, W, H, D=200)
+    sim.load(g)
+    rep = sim.run()
+    ref, gens, _ = reference_run(g)
+    assert rep.generations == gens
+    assert (sim.tile() == ref).all()
+
+
+def test_resident_u8_via_bits_and_graphs(gpu, monkeypatch):
+    monkeypatch.setenv("GOL_U8_VIA_BITS", "1")
+    W, H = 4096, 1024
+    g = random_grid(W, H, 9)
+    for graphs in ("off", "on"):
+        sim = _resident_sim(monkeypatch, W, H, layout="u8", graphs=graphs, gen_limit=1000, check_similarity=False)
+        sim.load(g)
+        sim.advance(700)
+        assert (sim.tile() == life_step_torch(g, 700, device="cuda")).all(), graphs
+        del sim
+
+
+def test_resident_off_when_ranks_share_the_gpu(gpu, monkeypatch):
+    """Four in-process ranks on one device: a resident launch could not get
+    every CU, so the engines fall back to the grouped kernels (still exact)."""
+    monkeypatch.setenv("GOL_RESIDENT", "1")
+    W, H = 4096, 1024
+    g = random_grid(W, H, 3)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=300, decomp="1x4", check_similarity=False), 4, engine="hip")
+    assert not any(s.native_engine.resident for s in grp.sims)
+    grp.load(g)
+    grp.parallel(lambda s: s.advance(300))
+    assert (grp.gather() == life_step_torch(g, 300, device="cuda")).all()
