@@ -85,8 +85,20 @@ inline uint32_t owned_mask(const TileGeom& g, int64_t c) {
 
 class CpuBackend final : public Backend {
  public:
-  CpuBackend(int threads, bool drift) : pool_(threads > 0 ? threads : default_host_threads()), drift_(drift) {}
-  std::string name() const override { return drift_ ? "cpu [drift]" : "cpu"; }
+  CpuBackend(int threads, bool drift) : pool_(threads > 0 ? threads : default_host_threads()), drift_(drift) {
+    const char* r = std::getenv("GOL_CPU_RESIDENT");
+    resident_ = r && *r && *r != '0';
+  }
+  std::string name() const override {
+    return std::string(drift_ ? "cpu [drift]" : "cpu") + (resident_ ? " [resident]" : "");
+  }
+  // GOL_CPU_RESIDENT=1: the engine's resident-epoch schedule (one block of
+  // T = D per epoch) on the host, so that path is testable without a GPU;
+  // run_block evaluates any T.
+  int resident_epoch(Layout l, int64_t, int64_t, int D_req, bool multi) const override {
+    if (!resident_ || l != Layout::Bits) return 0;
+    return D_req > 16 ? D_req : multi ? 256 : 128;
+  }
   bool drifts(Layout) const override { return drift_; }
   void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override;
   void convert_rows(const void* src, const TileGeom& gs, void* dst, const TileGeom& gd, int64_t r0,
@@ -153,6 +165,7 @@ class CpuBackend final : public Backend {
   }
   ThreadPool pool_;
   bool drift_ = false;
+  bool resident_ = false;  // GOL_CPU_RESIDENT
 };
 
 int CpuBackend::run_block(const BlockArgs& a) {

@@ -89,8 +89,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // enough for the register file runs each epoch as one launch (no T <= 16
   // blocks, no segment triangles); the same decision on every rank (smallest
   // tile).  Not with the overlapped schedules, which split epochs into blocks.
-  if (cl == Layout::Bits && dec_.Px == 1 && cfg_.W % 32 == 0 && cfg_.overlap != 1 && cfg_.overlap != 2 &&
-      be_->wraps_columns(cl)) {
+  if (cl == Layout::Bits && dec_.Px == 1 && cfg_.W % 32 == 0 && cfg_.overlap != 1 && cfg_.overlap != 2) {
     const int Dr = be_->resident_epoch(cl, ceil_div(dec_.H, int64_t(dec_.Py)), cfg_.W, cfg_.epoch, row_exchange);
     if (Dr > 16 && (dec_.Py == 1 || Dr <= min_tile_rows(dec_))) {
       resident_ = true;
