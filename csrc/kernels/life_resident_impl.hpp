@@ -55,7 +55,8 @@ using lb::kCpolSc1;
 
 constexpr int kM = kResidentWaves;          // waves per workgroup, stacked down the band
 constexpr int kBndWords = 2 * kM * 2 * 64;   // [parity][wave][first/last row][lane]
-constexpr int kFlagWords = 128;              // [window parity][64 generations]
+constexpr int kFlagWords = 128;              // generation flags, a ring (slot = generation & 127)
+constexpr int kCntWords = kM;                // GOL_RES_SYNC=1: per-wave generation counters
 // One workgroup per CU: more than half of the CU's 160 KB LDS (a small RW
 // alone would let the register file take two workgroups).
 constexpr int kLdsWords = 96 * 1024 / 4;
@@ -67,6 +68,14 @@ constexpr int kOOR = int(0x80000000u);       // buffer offset past any record co
 constexpr int kRowFence = GOL_RES_ROW_FENCE;  // rows between scheduling barriers (0: none)
 constexpr int kLoadBatch = 8;                 // refresh loads per batch (two batches in flight)
 constexpr int kTwoBodyMaxRW = 48;             // larger RW: one masked generation body
+// Edge-row hand-off between the waves of a band each generation:
+//   0: one workgroup barrier per generation;
+//   1: per-wave generation counters in LDS: a wave publishes its edge rows,
+//      updates its interior rows, and only then waits for its two neighbours
+//      (no workgroup barrier between refreshes).
+#ifndef GOL_RES_SYNC
+#define GOL_RES_SYNC 0
+#endif
 
 struct HS {
   uint32_t h0, h1, c;
@@ -112,11 +121,54 @@ __device__ __forceinline__ uint32_t gen_rows(uint32_t (&s)[RW], uint32_t above, 
   return acc;
 }
 
-// Wave 0 copies one window of generation flags to the engine's array.
-__device__ __forceinline__ void flush_flags(uint32_t* lflag, uint32_t* changed, int win, int g0, int n, int lane) {
+// The same generation with the edge rows last (GOL_RES_SYNC=1): rows
+// 1..RW-2 need no neighbour, so they run while the waves above and below
+// finish publishing; edges() then returns (above, below).
+template <int RW, bool MASKED, class Edges>
+__device__ __forceinline__ uint32_t gen_rows_split(uint32_t (&s)[RW], int i_lo, int i_hi, const Edges& edges) {
+  static_assert(RW >= 3, "split generation body: at least three rows per wave");
+  uint32_t acc = 0;
+  const auto flag = [&](int i, uint32_t n, uint32_t c) {
+    if constexpr (MASKED) {
+      const uint32_t x = (i >= i_lo && i < i_hi) ? c : n;
+      acc = bop3<tt::OR_XOR>(acc, n, x);
+    } else {
+      acc = bop3<tt::OR_XOR>(acc, n, c);
+    }
+    asm("" : "+v"(acc));
+  };
+  const HS a0 = hs(s[0]), a1 = hs(s[1]);
+  HS prev = a0, cur = a1;
+#pragma unroll
+  for (int i = 1; i < RW - 1; ++i) {
+    const HS nxt = hs(s[i + 1]);
+    const uint32_t n = lb::rule(prev.h0, prev.h1, cur.h0, cur.h1, nxt.h0, nxt.h1, cur.c);
+    flag(i, n, cur.c);
+    s[i] = n;
+    prev = cur;
+    cur = nxt;
+    if constexpr (kRowFence > 0)
+      if (i % kRowFence == 0) __builtin_amdgcn_sched_barrier(0);
+  }
+  uint32_t above, below;
+  edges(above, below);
+  const HS ha = hs(above), hb = hs(below);
+  const uint32_t n0 = lb::rule(ha.h0, ha.h1, a0.h0, a0.h1, a1.h0, a1.h1, a0.c);
+  flag(0, n0, a0.c);
+  const uint32_t nl = lb::rule(prev.h0, prev.h1, cur.h0, cur.h1, hb.h0, hb.h1, cur.c);
+  flag(RW - 1, nl, cur.c);
+  s[0] = n0;
+  s[RW - 1] = nl;
+  return acc;
+}
+
+// Wave 0 copies the flags of generations [g0, g0 + n) (n <= 64) from the
+// LDS ring to the engine's array and clears their slots.
+__device__ __forceinline__ void flush_flags(uint32_t* lflag, uint32_t* changed, int g0, int n, int lane) {
   if (lane < n) {
-    if (lflag[win * 64 + lane]) changed[g0 + lane] = 1u;
-    lflag[win * 64 + lane] = 0u;
+    const int sl = (g0 + lane) & (kFlagWords - 1);
+    if (lflag[sl]) changed[g0 + lane] = 1u;
+    lflag[sl] = 0u;
   }
 }
 
@@ -162,12 +214,18 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
 #pragma unroll
     for (int i = 0; i < RW; ++i) s[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, (eb + i) * ip + vw, 0, 0);
   }
-  if (threadIdx.x < kFlagWords) lflag[threadIdx.x] = 0u;
+  uint32_t* const cntw = lflag + kFlagWords;
+  if (threadIdx.x < kFlagWords + kCntWords) lflag[threadIdx.x] = 0u;
+  __syncthreads();
   uint32_t* changed = p.changed;
   if (changed && p.gen_dev) changed += *p.gen_dev + p.gen_rel;
   const bool rec = changed != nullptr && outw;
 
   for (int t = 0; t < p.T; ++t) {
+    if (t > 0 && t % p.k == 0 && p.probe) {  // timing probe: no exchange, but the flags still flush
+      __syncthreads();
+      if (w == 0 && changed) flush_flags(lflag, changed, t - p.k, p.k, lane);
+    }
     if (t > 0 && t % p.k == 0 && !p.probe) {
       // ---- refresh m: publish, signal, wait for the 8 neighbours, read ----
       const uint32_t m = uint32_t(t / p.k);
@@ -205,6 +263,8 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
           __hip_atomic_store(p.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       __syncthreads();
+      // Every wave has finished generations < t: wave 0 moves their flags out.
+      if (w == 0 && changed) flush_flags(lflag, changed, t - p.k, p.k, lane);
       // Fresh opaque copies: per-row values of the publish loop would stay
       // live across the wait (RW SGPRs and offsets).
       asm volatile("" : "+s"(e0), "+s"(qa), "+s"(nc), "+s"(kk), "+s"(ne), "+s"(ipr));
@@ -247,35 +307,58 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
     uint32_t* const slot = bnd + (t & 1) * (kM * 128);
     slot[w * 128 + lane] = s[0];
     slot[w * 128 + 64 + lane] = s[RW - 1];
-    __syncthreads();
-    if (t > 0 && (t & 63) == 0 && w == 0 && changed) flush_flags(lflag, changed, ((t >> 6) - 1) & 1, t - 64, 64, lane);
-    const uint32_t up = slot[max(w - 1, 0) * 128 + 64 + lane];
-    const uint32_t dn = slot[min(w + 1, kM - 1) * 128 + lane];
-    const uint32_t above = w > 0 ? up : 0u;
-    const uint32_t below = w < kM - 1 ? dn : 0u;
     // Opaque copies: the per-row conditions are re-derived each generation
     // instead of being hoisted out of the loop as RW lane masks (SGPR spills).
     int lo = __builtin_amdgcn_readfirstlane(i_lo), hi = __builtin_amdgcn_readfirstlane(i_hi);
     asm volatile("" : "+s"(lo), "+s"(hi));
+    uint32_t acc;
+#if GOL_RES_SYNC == 1
+    if (lane == 0) __hip_atomic_store(cntw + w, uint32_t(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const auto edges = [&](uint32_t& above, uint32_t& below) {
+      // Bounded wait for the neighbours' generation-t edge rows.
+      const uint32_t want = uint32_t(t + 1);
+      bool ok_up = w == 0, ok_dn = w == kM - 1;
+      for (int it = 0; it < (1 << 22) && !(ok_up && ok_dn); ++it) {
+        if (!ok_up) ok_up = __hip_atomic_load(cntw + w - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= want;
+        if (!ok_dn) ok_dn = __hip_atomic_load(cntw + w + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= want;
+      }
+      if (!(ok_up && ok_dn) && lane == 0 && p.err)
+        __hip_atomic_store(p.err, 5u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t up = slot[max(w - 1, 0) * 128 + 64 + lane];
+      const uint32_t dn = slot[min(w + 1, kM - 1) * 128 + lane];
+      above = w > 0 ? up : 0u;
+      below = w < kM - 1 ? dn : 0u;
+    };
+    if constexpr (RW > kTwoBodyMaxRW) {
+      acc = gen_rows_split<RW, true>(s, lo, hi, edges);
+    } else {
+      acc = partial ? gen_rows_split<RW, true>(s, lo, hi, edges) : gen_rows_split<RW, false>(s, 0, RW, edges);
+    }
+#else
+    __syncthreads();
+    const uint32_t up = slot[max(w - 1, 0) * 128 + 64 + lane];
+    const uint32_t dn = slot[min(w + 1, kM - 1) * 128 + lane];
+    const uint32_t above = w > 0 ? up : 0u;
+    const uint32_t below = w < kM - 1 ? dn : 0u;
     // Two bodies (masked for the few waves whose rows straddle the output
     // range) cost a second copy of the rows in registers; above 48 rows per
     // wave that would spill, so one masked body serves every wave there
     // (one more VALU op per row).
-    uint32_t acc;
     if constexpr (RW > kTwoBodyMaxRW) {
       acc = gen_rows<RW, true>(s, above, below, lo, hi);
     } else {
       acc = partial ? gen_rows<RW, true>(s, above, below, lo, hi) : gen_rows<RW, false>(s, above, below, 0, RW);
     }
+#endif
     if (rec) {
       const bool any = __ballot(own && acc != 0u) != 0;
-      if (any && lane == 0) lflag[((t >> 6) & 1) * 64 + (t & 63)] = 1u;
+      if (any && lane == 0) lflag[t & (kFlagWords - 1)] = 1u;
     }
   }
   __syncthreads();
   if (w == 0 && changed && p.T > 0) {
-    const int g0 = (p.T - 1) & ~63;
-    flush_flags(lflag, changed, ((p.T - 1) >> 6) & 1, g0, p.T - g0, lane);
+    const int g0 = ((p.T - 1) / p.k) * p.k;  // the generations since the last refresh
+    flush_flags(lflag, changed, g0, p.T - g0, lane);
   }
   // Opaque copies again: offsets derived from eb before the loop would stay
   // live through it (RW VGPRs).

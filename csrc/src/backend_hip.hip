@@ -682,6 +682,7 @@ class HipBackend final : public Backend {
       fail(std::string(e == 2   ? "life_group kernel (chained groups): a wave gave up waiting for the group below" + diag
                        : e == 4 ? "life_resident kernel: a workgroup gave up waiting for its neighbours' halo rows "
                                   "(not every workgroup was resident: another kernel on this GPU?)"
+                       : e == 5 ? "life_resident kernel: a wave gave up waiting for its neighbours' edge rows"
                        : e == 3 ? "life_group kernel (linked launches): a group gave up waiting for the previous "
                                   "launch's rows"
                                 : "life_short kernel: a wave gave up waiting for its neighbour's LDS rows") +

@@ -5,7 +5,9 @@ export TMPDIR=/tmp
 O=gpurun_out/res1
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -k resident -v --timeout 120 --timeout-method thread > $O/pytest_resident.log 2>&1
-rc=$?; echo "resident tests rc=$rc"; grep -E "PASSED|FAILED|ERROR|passed|failed" $O/pytest_resident.log | tail -25; [ $rc -eq 0 ] || exit $rc
+rc=$?; echo "resident tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_resident.log | tail -8; [ $rc -eq 0 ] || exit $rc
+GOL_NATIVE_SO=alt_so/sync1/_gol.so timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -k resident -v --timeout 120 --timeout-method thread > $O/pytest_resident_sync1.log 2>&1
+rc=$?; echo "resident tests (sync1) rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_resident_sync1.log | tail -8; [ $rc -eq 0 ] || exit $rc
 T=$O/tiles.jsonl; : > $T
 run() {  # label, env..., -- bench args
   local label=$1; shift
@@ -20,6 +22,8 @@ run() {  # label, env..., -- bench args
 for H in 4096 8192; do
   run "h$H default" GOL_RESIDENT=0 -- --height $H || exit $?
   run "h$H resident k8" GOL_RESIDENT=1 GOL_RES_K=8 -- --height $H || exit $?
+  run "h$H resident k8 sync1" GOL_NATIVE_SO=alt_so/sync1/_gol.so GOL_RESIDENT=1 GOL_RES_K=8 -- --height $H || exit $?
+  run "h$H resident k8 sync1 probe" GOL_NATIVE_SO=alt_so/sync1/_gol.so GOL_RESIDENT=1 GOL_RES_K=8 GOL_RES_PROBE=1 -- --height $H --verify 0 || exit $?
   run "h$H resident k16" GOL_RESIDENT=1 GOL_RES_K=16 -- --height $H || exit $?
   run "h$H resident k8 probe" GOL_RESIDENT=1 GOL_RES_K=8 GOL_RES_PROBE=1 -- --height $H --verify 0 || exit $?
   run "h$H rehearse default" GOL_RESIDENT=0 -- --height $H --rehearse-rccl || exit $?
