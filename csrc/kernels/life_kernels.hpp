@@ -209,7 +209,13 @@ struct ResidentParams {
   int nreg;               // ns * nb workgroups
   int spin_log2;
   int probe;              // timing probe: 1 = no refresh waits (wrong rows), 0 = exact
+  // Diagnostics (GOL_RES_TRACE): per region and refresh, s_memrealtime at the
+  // refresh's start, after its stores drained, after the neighbours' flags
+  // arrived and after its loads, then s_memtime (shader clock) at its start
+  // and after its loads: trace[(region * kResTraceRefreshes + m) * 6 + i].
+  uint64_t* trace;
 };
+constexpr int kResTraceRefreshes = 64;
 
 struct ResidentPlan {
   int ns = 0, sw = 0, nb = 0, band_rows = 0, band_rem = 0, rw = 0, k = 0;
@@ -220,12 +226,16 @@ struct ResidentPlan {
 extern const int kResidentRW[];
 extern const int kResidentRWCount;
 constexpr int kResidentWaves = 16;
+// Bytes of one workgroup's exchange record in a resident mirror
+// (life_resident_impl.hpp kRecBytes): 2 x 16 rows of 64 words + 16 x 88 words.
+constexpr int kResidentRecBytes = 2 * 16 * 256 + 4 * kResidentWaves * 88;
 // Plan of a resident launch over a block (false: the tile does not fit the
 // register file at one workgroup per CU, or the block is not eligible).
+// k: refresh period / halo rows (<= 16); 0 = 8, deepened into the slack rows.
 bool plan_resident(const BlockArgs& a, int cus, int k, ResidentPlan* pl);
 // Enqueues the launch (flags zeroed first); returns the drift (T).
 int launch_life_resident(const BlockArgs& a, const ResidentPlan& pl, const LifeTuning& tune, uint8_t* mirror0,
-                         uint8_t* mirror1, uint32_t* flags, int probe, hipStream_t s);
+                         uint8_t* mirror1, uint32_t* flags, int probe, hipStream_t s, uint64_t* trace = nullptr);
 // Per-RW kernels (life_resident_rw*.hip).
 void launch_resident_rw(int rw, const ResidentParams& p, hipStream_t s);
 

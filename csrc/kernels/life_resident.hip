@@ -14,11 +14,13 @@ template <int RW>
 void launch_resident(const ResidentParams& p, hipStream_t s);
 }  // namespace lr
 
-// Rows per wave in VGPRs: dense at the small sizes so the band's slack rows
-// stay few; <= 88 keeps a wave under 128 VGPRs (four waves per SIMD).
-#define GOL_RESIDENT_RW_LIST(X)                                                                               \
-  X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30) X(32) X(34) X(36) X(38) X(40) X(44) \
-      X(48) X(52) X(56) X(60) X(64) X(72) X(80) X(88)
+// Rows per wave in VGPRs: every count up to 48 so the bands' slack rows stay
+// few (the slack goes into deeper halos, see plan_resident); <= 88 keeps a
+// wave under 128 VGPRs (four waves per SIMD).
+#define GOL_RESIDENT_RW_LIST(X) \
+  X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) \
+      X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(33) X(34) X(35) X(36) X(37) X(38) X(39) X(40) X(41) X(42) \
+      X(43) X(44) X(45) X(46) X(47) X(48) X(52) X(56) X(60) X(64) X(72) X(80) X(88)
 
 #define GOL_RW_VALUE(n) n,
 const int kResidentRW[] = {GOL_RESIDENT_RW_LIST(GOL_RW_VALUE)};
@@ -42,10 +44,14 @@ void launch_resident_rw(int rw, const ResidentParams& p, hipStream_t s) {
   }
 }
 
-bool plan_resident(const BlockArgs& a, int cus, int k, ResidentPlan* pl) {
+bool plan_resident(const BlockArgs& a, int cus, int k_req, ResidentPlan* pl) {
   const TileGeom& g = a.g;
   if (g.layout != Layout::Bits || !a.full_width || !a.allow_drift || a.dual_offset != 0 || g.W % 32 != 0)
     return false;
+  // k_req <= 0: plan with 8 halo rows per side, then deepen the halos into
+  // the band's slack rows (up to the halo lane's 16 generations): fewer
+  // refreshes at no cost.
+  const int k = k_req > 0 ? k_req : 8;
   if (k < 1 || k > 16 || a.T < 1 || a.row_lo >= a.row_hi) return false;
   const int64_t ww = g.W / 32;
   const int64_t ns = ceil_div(ww, int64_t(63));
@@ -69,13 +75,14 @@ bool plan_resident(const BlockArgs& a, int cus, int k, ResidentPlan* pl) {
   pl->band_rows = int(band_rows);
   pl->band_rem = int(band_rem);
   pl->rw = rw;
-  pl->k = k;
+  pl->k = k_req > 0 ? k
+                    : int(std::min<int64_t>(16, (int64_t(kResidentWaves) * rw - band_rows - (band_rem ? 1 : 0)) / 2));
   pl->ext_rows = ext;
   return true;
 }
 
 int launch_life_resident(const BlockArgs& a, const ResidentPlan& pl, const LifeTuning& tune, uint8_t* mirror0,
-                         uint8_t* mirror1, uint32_t* flags, int probe, hipStream_t s) {
+                         uint8_t* mirror1, uint32_t* flags, int probe, hipStream_t s, uint64_t* trace) {
   const TileGeom& g = a.g;
   ResidentParams p{};
   p.in = static_cast<const uint8_t*>(a.in);
@@ -106,6 +113,7 @@ int launch_life_resident(const BlockArgs& a, const ResidentPlan& pl, const LifeT
   p.nreg = pl.ns * pl.nb;
   p.spin_log2 = std::min(24, std::max(4, tune.chain_spin_log2 + 4));
   p.probe = probe;
+  p.trace = trace;
   GOL_REQUIRE(p.nreg <= tune.cus, "resident kernel: more workgroups than CUs");
   (void)hipMemsetAsync(flags, 0, size_t(p.nreg) * 4, s);
   launch_resident_rw(pl.rw, p, s);

@@ -61,6 +61,13 @@ constexpr int kCntWords = kM;                // GOL_RES_SYNC=1: per-wave generat
 // alone would let the register file take two workgroups).
 constexpr int kLdsWords = 96 * 1024 / 4;
 constexpr int kOOR = int(0x80000000u);       // buffer offset past any record count: access dropped
+// Per-region exchange record in a mirror (bytes): k <= 16 first rows, k last
+// rows (64 words each), then one halo-lane word per register row.
+constexpr int kRecB = 16 * 256;
+constexpr int kRecC = 2 * 16 * 256;
+constexpr int kRecBytes = kRecC + 4 * kM * 88;
+static_assert(kRecBytes == kResidentRecBytes, "exchange record size");
+static_assert(kBndWords + kFlagWords + kCntWords + 2 * kRecBytes / 4 <= kLdsWords, "LDS layout");
 
 #ifndef GOL_RES_ROW_FENCE
 #define GOL_RES_ROW_FENCE 2
@@ -215,6 +222,8 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
     for (int i = 0; i < RW; ++i) s[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, (eb + i) * ip + vw, 0, 0);
   }
   uint32_t* const cntw = lflag + kFlagWords;
+  uint32_t* const recs = cntw + kCntWords;     // outgoing exchange record
+  uint32_t* const stage = recs + kRecBytes / 4;  // incoming halo rows + halo-lane words
   if (threadIdx.x < kFlagWords + kCntWords) lflag[threadIdx.x] = 0u;
   __syncthreads();
   uint32_t* changed = p.changed;
@@ -225,26 +234,50 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
     if (t > 0 && t % p.k == 0 && p.probe) {  // timing probe: no exchange, but the flags still flush
       __syncthreads();
       if (w == 0 && changed) flush_flags(lflag, changed, t - p.k, p.k, lane);
+      const int m = t / p.k;
+      if (p.trace && m < kResTraceRefreshes && threadIdx.x == 0) {
+        uint64_t* tr = p.trace + (int64_t(j) * kResTraceRefreshes + m) * 6;
+        tr[0] = tr[1] = tr[2] = tr[3] = __builtin_amdgcn_s_memrealtime();
+        tr[4] = tr[5] = __builtin_amdgcn_s_memtime();
+      }
     }
     if (t > 0 && t % p.k == 0 && !p.probe) {
       // ---- refresh m: publish, signal, wait for the 8 neighbours, read ----
       const uint32_t m = uint32_t(t / p.k);
-      // Opaque copies of the row geometry (see the generation step below).
-      int e0 = __builtin_amdgcn_readfirstlane(eb), qa = __builtin_amdgcn_readfirstlane(q0);
-      int nc = __builtin_amdgcn_readfirstlane(cnt), kk = __builtin_amdgcn_readfirstlane(p.k);
-      int ne = __builtin_amdgcn_readfirstlane(p.ext_rows), ipr = ip;
-      asm volatile("" : "+s"(e0), "+s"(qa), "+s"(nc), "+s"(kk), "+s"(ne), "+s"(ipr));
-      const BufRsrc mr = __builtin_amdgcn_make_buffer_rsrc(p.mirror[m & 1] + base, short(0), range, kBufFlags);
+      // Opaque copies of the band geometry (see the generation step below).
+      int r0 = __builtin_amdgcn_readfirstlane(w * RW), nc = __builtin_amdgcn_readfirstlane(cnt);
+      int kk = __builtin_amdgcn_readfirstlane(p.k), qa = __builtin_amdgcn_readfirstlane(q0);
+      int ne = __builtin_amdgcn_readfirstlane(p.ext_rows);
+      asm volatile("" : "+s"(r0), "+s"(nc), "+s"(kk), "+s"(qa), "+s"(ne));
+      // Exchange record of a region (words): its first k owned rows [0, 1024),
+      // its last k owned rows [1024, 2048) (64 lanes each), and its last owned
+      // lane's word of every band row [2048, 2048 + 16 RW).  Staged in LDS so
+      // that the whole workgroup stores / loads it coalesced, all in flight.
+      const BufRsrc mr = __builtin_amdgcn_make_buffer_rsrc(p.mirror[m & 1], short(0), p.nreg * kRecBytes, kBufFlags);
+      uint64_t* const tr = (p.trace && m < kResTraceRefreshes && threadIdx.x == 0)
+                               ? p.trace + (int64_t(j) * kResTraceRefreshes + m) * 6 : nullptr;
+      if (tr) {
+        tr[0] = __builtin_amdgcn_s_memrealtime();
+        tr[4] = __builtin_amdgcn_s_memtime();
+      }
+      constexpr int kRecUsed = kRecC / 4 + kM * RW;  // words of the record this RW fills
 #pragma unroll
       for (int i = 0; i < RW; ++i) {
-        const int q = e0 + i - qa;
-        const bool orow = q >= 0 && q < nc;
-        const bool edge = orow && (q < kk || q >= nc - kk);
-        const bool ok = edge ? own : (orow && last_own);
-        __builtin_amdgcn_raw_buffer_store_b32(s[i], mr, ok ? (e0 + i) * ipr + vw : kOOR, 0, kCpolSc1);
+        const int q = r0 + i - kk;  // owned-row index in the band
+        if (q >= 0 && q < kk) recs[q * 64 + lane] = s[i];
+        if (q >= nc - kk && q < nc && q >= 0) recs[kRecB / 4 + (q - (nc - kk)) * 64 + lane] = s[i];
+        if (lane == own_cnt) recs[kRecC / 4 + r0 + i] = s[i];  // the right neighbour's halo lane
+      }
+      __syncthreads();
+#pragma unroll
+      for (int x0 = 0; x0 < kRecUsed; x0 += 64 * kM) {
+        const int x = x0 + int(threadIdx.x);
+        if (x0 + 64 * kM <= kRecUsed || x < kRecUsed)
+          __builtin_amdgcn_raw_buffer_store_b32(recs[min(x, kRecUsed - 1)], mr, j * kRecBytes + 4 * x, 0, kCpolSc1);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (tr) tr[1] = __builtin_amdgcn_s_memrealtime();
       if (threadIdx.x == 0) __hip_atomic_store(p.flags + j, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (w == 0) {
         const int nn = lane < 4 ? lane : lane + 1;  // 3 x 3 neighbourhood without its centre
@@ -261,46 +294,59 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
         }
         if (!__all(done) && lane == 0 && p.err)
           __hip_atomic_store(p.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
       }
       __syncthreads();
       // Every wave has finished generations < t: wave 0 moves their flags out.
       if (w == 0 && changed) flush_flags(lflag, changed, t - p.k, p.k, lane);
-      // Fresh opaque copies: per-row values of the publish loop would stay
-      // live across the wait (RW SGPRs and offsets).
-      asm volatile("" : "+s"(e0), "+s"(qa), "+s"(nc), "+s"(kk), "+s"(ne), "+s"(ipr));
-      // Loads in batches of kLoadBatch rows, two batches in flight: every
-      // load needs a temporary until its select, and RW of them would not
-      // fit beside the RW rows of state.
-      constexpr int kNB = (RW + kLoadBatch - 1) / kLoadBatch;
-      uint32_t v[kNB][kLoadBatch];
+      // The neighbours' records, staged the same way: halo rows above (the
+      // band above's last k rows, lane 0 from the up-left region) and below
+      // (the band below's first k rows, lane 0 from the down-left region),
+      // then the left region's halo-lane words of every band row.
+      {
+        const int sl = strip > 0 ? strip - 1 : p.ns - 1;  // the strip to the left (torus)
+        const int ocl = min(p.sw, p.ww - sl * p.sw);      // its last owned lane
+        const int hup = band > 0 ? kk : 0, hdn = band < p.nb - 1 ? kk : 0;
+        const int nrows = hup + hdn;
+        const int used = 64 * nrows + kM * RW;
+        uint32_t v[(kRecC / 4 + kM * 88 + 64 * kM - 1) / (64 * kM)];
 #pragma unroll
-      for (int bb = 0; bb <= kNB; ++bb) {
-        if (bb < kNB) {
+        for (int u = 0; u < int(sizeof(v) / 4); ++u) {
+          const int x = u * 64 * kM + int(threadIdx.x);
+          int off = kOOR;
+          if (x < 64 * nrows) {
+            const int r = x >> 6, l = x & 63;
+            const bool upr = r < hup;
+            const int src = (l == 0 ? sl : strip) * p.nb + band + (upr ? -1 : 1);
+            off = src * kRecBytes + 4 * ((upr ? kRecB / 4 + (r + kk - hup) * 64 : (r - hup) * 64) + (l == 0 ? ocl : l));
+          } else if (x < used) {
+            off = (sl * p.nb + band) * kRecBytes + kRecC + 4 * (x - 64 * nrows);
+          }
+          v[u] = __builtin_amdgcn_raw_buffer_load_b32(mr, off, 0, kCpolSc1);
+        }
 #pragma unroll
-          for (int jj = 0; jj < kLoadBatch; ++jj) {
-            const int i = bb * kLoadBatch + jj;
-            if (i < RW) {
-              const int e = e0 + i, q = e - qa;
-              const bool hrow = e >= 0 && e < ne && ((q >= -kk && q < 0) || (q >= nc && q < nc + kk));
-              const bool take = hrow || (q >= 0 && q < nc && lane == 0);
-              v[bb][jj] = __builtin_amdgcn_raw_buffer_load_b32(mr, take ? e * ipr + vw : kOOR, 0, kCpolSc1);
-            }
+        for (int u = 0; u < int(sizeof(v) / 4); ++u) {
+          const int x = u * 64 * kM + int(threadIdx.x);
+          if (x < used) stage[x] = v[u];
+        }
+        __syncthreads();
+        asm volatile("" : "+s"(r0), "+s"(nc), "+s"(kk), "+s"(qa), "+s"(ne));
+#pragma unroll
+        for (int i = 0; i < RW; ++i) {
+          const int q = r0 + i - kk, e = qa + q;
+          if (q < 0 && e >= 0) {
+            s[i] = stage[(q + hup) * 64 + lane];
+          } else if (q >= nc && e < ne) {
+            s[i] = stage[(hup + q - nc) * 64 + lane];
+          } else if (q >= 0 && q < nc) {
+            const uint32_t c = stage[64 * nrows + r0 + i];
+            s[i] = lane == 0 ? c : s[i];
           }
         }
-        __builtin_amdgcn_sched_barrier(0);
-        if (bb > 0) {
-#pragma unroll
-          for (int jj = 0; jj < kLoadBatch; ++jj) {
-            const int i = (bb - 1) * kLoadBatch + jj;
-            if (i < RW) {
-              const int e = e0 + i, q = e - qa;
-              const bool hrow = e >= 0 && e < ne && ((q >= -kk && q < 0) || (q >= nc && q < nc + kk));
-              const bool take = hrow || (q >= 0 && q < nc && lane == 0);
-              s[i] = take ? v[bb - 1][jj] : s[i];
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (tr) {
+        tr[3] = __builtin_amdgcn_s_memrealtime();
+        tr[5] = __builtin_amdgcn_s_memtime();
       }
     }
     // ---- one generation: trade edge rows with the waves above / below ----

@@ -1,7 +1,9 @@
-// Resident epoch kernel instantiations (life_resident_impl.hpp): rows per wave 32, 34, 36, 38.
+// Resident epoch kernel instantiations (life_resident_impl.hpp): rows per wave 26, 27, 28, 29, 30, 31.
 #include "life_resident_impl.hpp"
 
-GOL_RESIDENT_RW(32)
-GOL_RESIDENT_RW(34)
-GOL_RESIDENT_RW(36)
-GOL_RESIDENT_RW(38)
+GOL_RESIDENT_RW(26)
+GOL_RESIDENT_RW(27)
+GOL_RESIDENT_RW(28)
+GOL_RESIDENT_RW(29)
+GOL_RESIDENT_RW(30)
+GOL_RESIDENT_RW(31)

@@ -1,7 +1,9 @@
-// Resident epoch kernel instantiations (life_resident_impl.hpp): rows per wave 40, 44, 48, 52.
+// Resident epoch kernel instantiations (life_resident_impl.hpp): rows per wave 32, 33, 34, 35, 36, 37.
 #include "life_resident_impl.hpp"
 
-GOL_RESIDENT_RW(40)
-GOL_RESIDENT_RW(44)
-GOL_RESIDENT_RW(48)
-GOL_RESIDENT_RW(52)
+GOL_RESIDENT_RW(32)
+GOL_RESIDENT_RW(33)
+GOL_RESIDENT_RW(34)
+GOL_RESIDENT_RW(35)
+GOL_RESIDENT_RW(36)
+GOL_RESIDENT_RW(37)

@@ -1,7 +1,9 @@
-// Resident epoch kernel instantiations (life_resident_impl.hpp): rows per wave 56, 60, 64, 72.
+// Resident epoch kernel instantiations (life_resident_impl.hpp): rows per wave 38, 39, 40, 41, 42, 43.
 #include "life_resident_impl.hpp"
 
-GOL_RESIDENT_RW(56)
-GOL_RESIDENT_RW(60)
-GOL_RESIDENT_RW(64)
-GOL_RESIDENT_RW(72)
+GOL_RESIDENT_RW(38)
+GOL_RESIDENT_RW(39)
+GOL_RESIDENT_RW(40)
+GOL_RESIDENT_RW(41)
+GOL_RESIDENT_RW(42)
+GOL_RESIDENT_RW(43)

@@ -95,9 +95,17 @@ class HipBackend final : public Backend {
     // 1 on where the tile fits; GOL_RES_K refresh period / halo rows (<= 16);
     // GOL_RES_D epoch depth; GOL_RES_PROBE=1 timing probe without refreshes.
     resident_mode_ = env_int("GOL_RESIDENT", 0);
-    resident_k_ = std::min(16, std::max(1, env_int("GOL_RES_K", 8)));
+    resident_k_ = std::min(16, std::max(0, env_int("GOL_RES_K", 0)));  // 0: as deep as the band's slack allows
     resident_D_ = env_int("GOL_RES_D", 0);
     resident_probe_ = env_int("GOL_RES_PROBE", 0);
+    if (const char* t = std::getenv("GOL_RES_TRACE")) {
+      const std::string v(t);
+      const size_t c = v.find(':');
+      if (c != std::string::npos) {
+        res_trace_at_ = std::atoi(v.substr(0, c).c_str());
+        res_trace_path_ = v.substr(c + 1);
+      }
+    }
     u8_pipe_ = env_int("GOL_U8_PIPE", 1) != 0;
     // Linked launches: consecutive grouped launches of an epoch overlap on
     // two streams, ordered by per-group completion words (LifeBlockParams::
@@ -429,13 +437,42 @@ class HipBackend final : public Backend {
                   "resident kernel: block of " + std::to_string(a.row_hi - a.row_lo) + " rows x T = " +
                       std::to_string(a.T) + " does not fit (Backend::resident_epoch)");
       reserve_resident(a.g);
-      const size_t mb = size_t(a.g.bytes());
+      const size_t mb = size_t(cus_) * hipk::kResidentRecBytes;
       auto* m0 = reinterpret_cast<uint8_t*>(tune_.chain_mem(5, mb));
       auto* m1 = reinterpret_cast<uint8_t*>(tune_.chain_mem(6, mb));
       uint32_t* fl = tune_.chain_mem(7, size_t(pl.ns) * pl.nb * 4);
       hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
-      const int drift = hipk::launch_life_resident(a, pl, tune_, m0, m1, fl, resident_probe_, s);
+      // GOL_RES_TRACE=<resident launch>:<csv>: refresh phase timestamps of one launch.
+      const bool traced = res_trace_at_ >= 0 && resident_launches_ == res_trace_at_;
+      ++resident_launches_;
+      uint64_t* tr = nullptr;
+      const size_t tbytes = size_t(pl.ns) * pl.nb * hipk::kResTraceRefreshes * 6 * sizeof(uint64_t);
+      if (traced) {
+        HIP_CHECK(hipStreamSynchronize(s));
+        HIP_CHECK(hipMalloc(&tr, tbytes));
+        HIP_CHECK(hipMemsetAsync(tr, 0, tbytes, s));
+      }
+      const int drift = hipk::launch_life_resident(a, pl, tune_, m0, m1, fl, resident_probe_, s, tr);
       HIP_CHECK(hipGetLastError());
+      if (traced) {
+        std::vector<uint64_t> h(tbytes / sizeof(uint64_t));
+        HIP_CHECK(hipMemcpyAsync(h.data(), tr, tbytes, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        HIP_CHECK(hipFree(tr));
+        std::FILE* f = std::fopen(res_trace_path_.c_str(), "w");
+        GOL_REQUIRE(f != nullptr, "GOL_RES_TRACE: cannot open " + res_trace_path_);
+        std::fprintf(f, "region,strip,band,refresh,t_start,t_stored,t_flags,t_loaded,clk_start,clk_loaded,k,rw,T\n");
+        for (int r = 0; r < pl.ns * pl.nb; ++r)
+          for (int m = 1; m < hipk::kResTraceRefreshes; ++m) {
+            const uint64_t* q = &h[size_t((int64_t(r) * hipk::kResTraceRefreshes + m) * 6)];
+            if (!q[0]) continue;
+            std::fprintf(f, "%d,%d,%d,%d,%llu,%llu,%llu,%llu,%llu,%llu,%d,%d,%d\n", r, r / pl.nb, r % pl.nb, m,
+                         (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[2],
+                         (unsigned long long)q[3], (unsigned long long)q[4], (unsigned long long)q[5], pl.k, pl.rw,
+                         a.T);
+          }
+        std::fclose(f);
+      }
       return drift;
     }
     if (trace_at_ >= 0 && launches_ == trace_at_) {
@@ -613,8 +650,8 @@ class HipBackend final : public Backend {
     }
     return D;
   }
-  void reserve_resident(const TileGeom& g) override {
-    const size_t mb = size_t(g.bytes());
+  void reserve_resident(const TileGeom& /*g*/) override {
+    const size_t mb = size_t(cus_) * hipk::kResidentRecBytes;  // one exchange record per workgroup
     tune_.chain_mem(5, mb);
     tune_.chain_mem(6, mb);
     tune_.chain_mem(7, size_t(cus_) * 4);
@@ -812,6 +849,8 @@ class HipBackend final : public Backend {
   void* chain_[8] = {};
   size_t chain_bytes_[8] = {};
   int resident_mode_ = 0, resident_k_ = 8, resident_D_ = 0, resident_probe_ = 0;
+  int64_t resident_launches_ = 0, res_trace_at_ = -1;
+  std::string res_trace_path_;
   hipk::LinkState link_;  // linked launches (GOL_LINK)
   bool link_on_ = false;
   uint32_t chain_seq_ = 0;

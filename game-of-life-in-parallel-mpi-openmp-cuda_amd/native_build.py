@@ -35,7 +35,7 @@ LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp",
                  "u8_w1_carry", "u8_w1_add",
                  *[f"u8_w1_{x}_t{t}" for x in ("dpp", "carry", "add") for t in (24, 32)],  # deep byte passes
                  "u8_w1_dpp_t48"]  # pipelined wave pairs (life_pipe_impl.hpp)
-RESIDENT_TUS = 7  # life_resident_rw0..6.hip: the resident kernel's rows-per-wave instantiations
+RESIDENT_TUS = 9  # life_resident_rw0..8.hip: the resident kernel's rows-per-wave instantiations
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
             *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
             "kernels/tile_ops.hip", "kernels/life_resident.hip",

@@ -1,13 +1,16 @@
 #!/bin/bash
-# Resident epochs: GPU tests, then the rank tiles against the default kernels.
+# Resident epochs: GPU tests, refresh phase traces and the rank tiles.
 set -uo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/res1
+O=gpurun_out/res2
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -k resident -v --timeout 120 --timeout-method thread > $O/pytest_resident.log 2>&1
 rc=$?; echo "resident tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_resident.log | tail -8; [ $rc -eq 0 ] || exit $rc
-GOL_NATIVE_SO=alt_so/sync1/_gol.so timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -k resident -v --timeout 120 --timeout-method thread > $O/pytest_resident_sync1.log 2>&1
-rc=$?; echo "resident tests (sync1) rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_resident_sync1.log | tail -8; [ $rc -eq 0 ] || exit $rc
+for H in 4096 8192; do
+  GOL_RESIDENT=1 GOL_RES_TRACE=6:$O/trace_h$H.csv timeout -k 10 120 python bench.py --height $H --steps 3 --warmup 1 --prewarm 0 --verify 0 --no-phase-step > $O/h$H.json 2>> $O/err.log
+  rc=$?; echo "trace h$H rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  python scripts/res_trace.py $O/trace_h$H.csv | head -14
+done
 T=$O/tiles.jsonl; : > $T
 run() {  # label, env..., -- bench args
   local label=$1; shift
@@ -22,14 +25,9 @@ run() {  # label, env..., -- bench args
 for H in 4096 8192; do
   run "h$H default" GOL_RESIDENT=0 -- --height $H || exit $?
   run "h$H resident" GOL_RESIDENT=1 -- --height $H || exit $?
-  run "h$H resident sync1" GOL_NATIVE_SO=alt_so/sync1/_gol.so GOL_RESIDENT=1 -- --height $H || exit $?
-  run "h$H resident sync1 probe" GOL_NATIVE_SO=alt_so/sync1/_gol.so GOL_RESIDENT=1 GOL_RES_PROBE=1 -- --height $H --verify 0 || exit $?
   run "h$H resident k8" GOL_RESIDENT=1 GOL_RES_K=8 -- --height $H || exit $?
-  run "h$H resident probe" GOL_RESIDENT=1 GOL_RES_PROBE=1 -- --height $H --verify 0 || exit $?
   run "h$H rehearse default" GOL_RESIDENT=0 -- --height $H --rehearse-rccl || exit $?
-  run "h$H rehearse resident D256" GOL_RESIDENT=1 -- --height $H --rehearse-rccl || exit $?
-  run "h$H rehearse resident D128" GOL_RESIDENT=1 GOL_RES_D=128 -- --height $H --rehearse-rccl || exit $?
+  run "h$H rehearse resident" GOL_RESIDENT=1 -- --height $H --rehearse-rccl || exit $?
 done
 run "h16384 default" GOL_RESIDENT=0 -- --height 16384 || exit $?
 run "h16384 resident" GOL_RESIDENT=1 -- --height 16384 || exit $?
-run "h16384 rehearse resident" GOL_RESIDENT=1 -- --height 16384 --rehearse-rccl || exit $?
