@@ -194,10 +194,17 @@ __device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int 
 // top bit in an SGPR-pair lane mask; s_lshl_b64 moves each mask bit one lane
 // up; v_addc_co_u32 adds it back in as bit 0.  All VALU ops here issue at the
 // full v_bitop3 rate (csrc/tools/ubench_dpp_mix.hip), unlike DPP/v_alignbit.
+#ifndef GOL_ADDER_NOP
+#define GOL_ADDER_NOP 0
+#endif
 __device__ __forceinline__ void adder_window(uint32_t c, uint32_t& l1, uint32_t& l2) {
   // One block so the pair of lane masks never outlives the window (no SGPR
-  // pressure across levels); s_nop 0 where gfx950 wants a wait state between
-  // a carry-writing VALU op and a read of its VGPR result.
+  // pressure across levels).  gfx950 wants a wait state between the last
+  // carry-writing VALU op and a read of its VGPR result; the compiler pads
+  // that hazard after the block itself (an s_nop 0 or an independent op), so
+  // the block no longer ends in its own s_nop (GOL_ADDER_NOP=1 restores it):
+  // one instruction less per level body, 32768^2 10.40-10.48 -> 10.35 ms per
+  // 1000 generations (profiles/r03/adder_nop_ab.jsonl).
   uint32_t t1;
   uint64_t m1, m2;
   asm("v_add_co_u32_e64 %[t1], %[m1], %[c], %[c]\n\t"    // c << 1; carry = bit 31
@@ -205,8 +212,10 @@ __device__ __forceinline__ void adder_window(uint32_t c, uint32_t& l1, uint32_t&
       "v_add_co_u32_e64 %[l2], %[m2], %[t1], %[t1]\n\t"   // carry = bit 30
       "v_addc_co_u32_e64 %[l1], %[m1], %[t1], 0, %[m1]\n\t"
       "s_lshl_b64 %[m2], %[m2], 1\n\t"
-      "v_addc_co_u32_e64 %[l2], %[m2], %[l1], %[l1], %[m2]\n\t"
-      "s_nop 0"
+      "v_addc_co_u32_e64 %[l2], %[m2], %[l1], %[l1], %[m2]"
+#if GOL_ADDER_NOP
+      "\n\ts_nop 0"
+#endif
       : [l1] "=&v"(l1), [l2] "=&v"(l2), [t1] "=&v"(t1), [m1] "=&s"(m1), [m2] "=&s"(m2)
       : [c] "v"(c)
       : "scc");

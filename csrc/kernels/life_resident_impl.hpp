@@ -215,6 +215,12 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
   const int64_t base = p.row0 * p.pitch;
   const int range = int(int64_t(p.ext_rows) * p.pitch);
 
+  // Trace slot 0 (GOL_RES_TRACE): kernel start, state loaded, loop done, end.
+  uint64_t* const tr0 = (p.trace && threadIdx.x == 0) ? p.trace + int64_t(j) * kResTraceRefreshes * 6 : nullptr;
+  if (tr0) {
+    tr0[0] = __builtin_amdgcn_s_memrealtime();
+    tr0[4] = __builtin_amdgcn_s_memtime();
+  }
   uint32_t s[RW];
   {
     const BufRsrc rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.in) + base, short(0), range, kBufFlags);
@@ -226,6 +232,7 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
   uint32_t* const stage = recs + kRecBytes / 4;  // incoming halo rows + halo-lane words
   if (threadIdx.x < kFlagWords + kCntWords) lflag[threadIdx.x] = 0u;
   __syncthreads();
+  if (tr0) tr0[1] = __builtin_amdgcn_s_memrealtime();
   uint32_t* changed = p.changed;
   if (changed && p.gen_dev) changed += *p.gen_dev + p.gen_rel;
   const bool rec = changed != nullptr && outw;
@@ -402,6 +409,7 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
     }
   }
   __syncthreads();
+  if (tr0) tr0[2] = __builtin_amdgcn_s_memrealtime();
   if (w == 0 && changed && p.T > 0) {
     const int g0 = ((p.T - 1) / p.k) * p.k;  // the generations since the last refresh
     flush_flags(lflag, changed, g0, p.T - g0, lane);
@@ -416,6 +424,10 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
   for (int i = 0; i < RW; ++i) {
     const bool ok = own && i >= flo && i < fhi;
     __builtin_amdgcn_raw_buffer_store_b32(s[i], ro, ok ? (ef + i) * ipf + vw : kOOR, 0, 0);
+  }
+  if (tr0) {
+    tr0[3] = __builtin_amdgcn_s_memrealtime();
+    tr0[5] = __builtin_amdgcn_s_memtime();
   }
 }
 

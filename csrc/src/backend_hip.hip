@@ -463,7 +463,7 @@ class HipBackend final : public Backend {
         GOL_REQUIRE(f != nullptr, "GOL_RES_TRACE: cannot open " + res_trace_path_);
         std::fprintf(f, "region,strip,band,refresh,t_start,t_stored,t_flags,t_loaded,clk_start,clk_loaded,k,rw,T\n");
         for (int r = 0; r < pl.ns * pl.nb; ++r)
-          for (int m = 1; m < hipk::kResTraceRefreshes; ++m) {
+          for (int m = 0; m < hipk::kResTraceRefreshes; ++m) {  // m = 0: kernel start / loaded / loop end / end
             const uint64_t* q = &h[size_t((int64_t(r) * hipk::kResTraceRefreshes + m) * 6)];
             if (!q[0]) continue;
             std::fprintf(f, "%d,%d,%d,%d,%llu,%llu,%llu,%llu,%llu,%llu,%d,%d,%d\n", r, r / pl.nb, r % pl.nb, m,

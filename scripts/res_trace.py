@@ -12,6 +12,14 @@ import sys
 
 def main(path: str) -> None:
     rows = list(csv.DictReader(open(path)))
+    k0 = [r for r in rows if r["refresh"] == "0"]
+    rows = [r for r in rows if r["refresh"] != "0"]
+    if k0:  # refresh 0 = the kernel: start, state loaded, loop done, end
+        t = lambda r, c: int(r[c]) * 0.01
+        s0 = min(t(r, "t_start") for r in k0)
+        print(f"kernel: first start -> last start {max(t(r, 't_start') for r in k0) - s0:.2f} us, "
+              f"-> last loaded {max(t(r, 't_stored') for r in k0) - s0:.2f}, -> last loop end "
+              f"{max(t(r, 't_flags') for r in k0) - s0:.2f}, -> last end {max(t(r, 't_loaded') for r in k0) - s0:.2f}")
     by_m: dict[int, list[dict]] = {}
     for r in rows:
         by_m.setdefault(int(r["refresh"]), []).append(r)
@@ -35,7 +43,7 @@ def main(path: str) -> None:
 def compute(path: str) -> None:
     """Per workgroup, the k generations between two refreshes: wall time and
     shader clock (s_memtime cycles / s_memrealtime time)."""
-    rows = list(csv.DictReader(open(path)))
+    rows = [r for r in csv.DictReader(open(path)) if r["refresh"] != "0"]
     by: dict[int, dict[int, dict]] = {}
     for r in rows:
         by.setdefault(int(r["region"]), {})[int(r["refresh"])] = r
