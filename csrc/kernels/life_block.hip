@@ -38,7 +38,8 @@ const char* xlane_name(int x) {
 
 std::string life_block_variant(Layout layout, const LifeTuning& tune) {
   const int w = words_per_lane(layout, tune);
-  if (layout == Layout::U8 && tune.u8_lds) return "u8 lds-tiled single-step";
+  if (layout == Layout::U8 && tune.u8_lds)
+    return tune.lds_T > 1 ? "u8 lds-tiled T=" + std::to_string(tune.lds_T) : std::string("u8 lds-tiled single-step");
   const bool grouped = tune.group != 0 && tune.split == 0 && !tune.skew;
   return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=" + std::to_string(w) + " " +
          xlane_name(xlane_of(layout, w, tune)) + (tune.skew ? " skew" : "") +
@@ -53,7 +54,7 @@ std::string life_block_variant(Layout layout, const LifeTuning& tune) {
 }
 
 int life_block_max_T(Layout layout, const LifeTuning& tune) {
-  if (layout == Layout::U8 && tune.u8_lds) return 1;
+  if (layout == Layout::U8 && tune.u8_lds) return tune.lds_T;
   // Register budget for 2 waves/SIMD (<= 256 VGPRs): T * words-per-lane <= 16.
   return words_per_lane(layout, tune) >= 2 ? 8 : 16;
 }
@@ -98,14 +99,16 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   p.fold_lanes = 64;
   const int64_t rows = a.row_hi - a.row_lo;
   int x = xlane_of(g.layout, w, tune);
-  if (g.layout == Layout::U8 && tune.u8_lds && a.T == 1) {
+  if (g.layout == Layout::U8 && tune.u8_lds && (a.T == 1 || a.T == 2 || a.T == 4 || a.T == 8)) {
     BlockArgs b = a;
     b.dual_offset = 0;
-    launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
-    if (a.dual_offset) {
+    for (int half = 0; half < (a.dual_offset ? 2 : 1); ++half) {
+      if (a.T == 1)
+        launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
+      else
+        launch_life_lds_multi(b, tune.wrap, stream);
       b.row_lo += a.dual_offset;
       b.row_hi += a.dual_offset;
-      launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
     }
     return 0;
   }

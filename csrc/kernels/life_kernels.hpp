@@ -137,6 +137,7 @@ struct LifeTuning {
   int xlane = kXlaneAuto;   // cross-lane primitive
   bool u8_lds = false;      // byte layout: single-step LDS-tiled kernel (T = 1)
   int lds_rows = 32;        // rows per LDS tile (32 or 64)
+  int lds_T = 8;            // generations per launch of the LDS-tiled byte kernel (1, 2, 4, 8)
   int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
   int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
@@ -241,6 +242,9 @@ void launch_resident_rw(int rw, const ResidentParams& p, hipStream_t s);
 
 // Single-generation LDS-tiled byte-layout kernel (life_step_lds.hip).
 void launch_life_step_lds(const BlockArgs& a, int lds_rows, bool wrap, hipStream_t stream);
+// The same with T = 2, 4 or 8 generations per launch through two LDS row
+// buffers (life_step_lds.hip life_lds_multi_kernel).
+void launch_life_lds_multi(const BlockArgs& a, bool wrap, hipStream_t stream);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

@@ -173,7 +173,172 @@ __global__ __launch_bounds__(256) void life_step_lds_kernel(const uint8_t* __res
   if (changed && __ballot(diff != 0u) != 0ull && (tid & 63) == 0) (gen_dev ? changed + *gen_dev : changed)[0] = 1u;
 }
 
+// ---- T generations per launch on an LDS-resident tile ----------------------
+// The same SWAR byte rule on T generations of a tile staged once: a 512-thread
+// workgroup (8 waves) stages 64 rows x 1024 bytes (the 64 - 2T output rows of
+// its tile plus T halo rows per side; 992 owned cells plus one 16-byte halo
+// chunk per side) into LDS, then evaluates generation g = 1..T in place on
+// the rows [g, 64 - g) (the dependence cone shrinks one row and one cell per
+// generation and side), the waves splitting the rows (each saves its
+// neighbours' edge rows before a barrier, then sweeps down its own rows).  Lane l of a wave owns the 16
+// cells of chunk l of a row (lanes 0 and 63 are the halo chunks, evaluated
+// too so that T <= 16 generations stay exact inside); the neighbour words
+// move between lanes with DPP.  The last generation goes to global memory.
+// HBM traffic: the tile once in and once out per T generations (plus the
+// 2T halo rows and 2 halo chunks), instead of per generation.
+constexpr int kMultiRows = 64;                        // LDS rows per buffer
+constexpr int kMultiOwn = 1024 - 2 * kHaloB;          // owned cells per tile (992)
+
+template <int T>
+__global__ __launch_bounds__(512) void life_lds_multi_kernel(const uint8_t* __restrict__ in,
+                                                             uint8_t* __restrict__ out, int64_t pitch,
+                                                             int64_t row_lo, int64_t row_hi, int64_t Wc,
+                                                             int64_t own_c0, int64_t own_c1, uint32_t* changed,
+                                                             const int64_t* gen_dev, int64_t wrap_w, int64_t wrap_h,
+                                                             int64_t row0, int64_t c_first, int64_t c_end) {
+  static_assert(T >= 1 && T <= 16, "one 16-byte halo chunk holds 16 generations of the light cone");
+  constexpr int kTH = kMultiRows - 2 * T;  // output rows per tile
+  constexpr int kRowB = 1024;              // LDS bytes per row: 64 chunks
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kMultiRows * kRowB];  // 64 KB: two workgroups per CU
+  const int64_t r0 = row_lo + int64_t(blockIdx.y) * kTH;          // first output row
+  const int64_t c0 = c_first - kHaloB + int64_t(blockIdx.x) * kMultiOwn;  // first staged cell
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // Stage rows r0 - T .. r0 + kTH + T - 1, cells c0 .. c0 + 1023 (16-byte chunks).
+  constexpr int kPer = kMultiRows * 64 / 512;
+  uint4 v[kPer];
+  bool ok[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int idx = tid + 512 * k;
+    const int lr = idx >> 6, ch = idx & 63;
+    const int64_t gr = r0 - T + lr;
+    const int64_t gc = c0 + 16 * int64_t(ch);
+    int64_t grc = gr < row_hi + T ? gr : row_hi + T - 1;
+    int64_t gcc = gc < 0 ? 0 : (gc + 16 <= pitch ? gc : pitch - 16);
+    if (wrap_h) grc = row0 + (((grc - row0) % wrap_h) + wrap_h) % wrap_h;
+    if (wrap_w) gcc = min(((gc % wrap_w) + wrap_w) % wrap_w, pitch - 16);
+    ok[k] = gr < row_hi + T && (wrap_w ? true : gc >= 0 && gc + 16 <= pitch);
+    v[k] = *reinterpret_cast<const uint4*>(in + grc * pitch + gcc);
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int idx = tid + 512 * k;
+    *reinterpret_cast<uint4*>(buf + idx * 16) = ok[k] ? v[k] : make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+
+  // Owned-cell byte masks for the changed flags (lanes 1..62 of the tile's
+  // owned columns, rows [T, T + kTH) of output rows < row_hi).
+  const int64_t cell = c0 + 16 * int64_t(lane);
+  uint32_t own[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int64_t x = cell + 4 * k + b;
+      if (lane >= 1 && lane <= 62 && x >= own_c0 && x < own_c1) m |= 0xFFu << (8 * b);
+    }
+    own[k] = m;
+  }
+  uint32_t* flags = changed ? (gen_dev ? changed + *gen_dev : changed) : nullptr;
+
+  // Horizontal 3-sums of one row chunk (16 cells per lane); the neighbour
+  // words move between lanes with DPP (lanes 0 and 63 get 0: tile halo).
+  auto hsum = [&](const uint4 x, uint32_t (&h)[4], uint32_t (&c)[4]) {
+    c[0] = x.x;
+    c[1] = x.y;
+    c[2] = x.z;
+    c[3] = x.w;
+    const uint32_t lw = __builtin_amdgcn_mov_dpp(c[3], 0x138, 0xF, 0xF, true);  // wave_shr:1
+    const uint32_t rw = __builtin_amdgcn_mov_dpp(c[0], 0x130, 0xF, 0xF, true);  // wave_shl:1
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t prev = k == 0 ? lw : c[k - 1];
+      const uint32_t next = k == 3 ? rw : c[k + 1];
+      h[k] = __builtin_amdgcn_alignbyte(c[k], prev, 3) + c[k] + __builtin_amdgcn_alignbyte(next, c[k], 1);
+    }
+  };
+
+#pragma unroll 1
+  for (int g = 1; g <= T; ++g) {
+    // Rows [g, kMultiRows - g) split over the 8 waves, contiguous, updated in
+    // place: each wave first saves the old rows just above and below its
+    // range (its neighbours' edge rows), then a barrier, then it sweeps down.
+    const int n = kMultiRows - 2 * g;
+    const int lo = g + (n * w) / 8, hi = g + (n * (w + 1)) / 8;
+    const uint4 up = *reinterpret_cast<const uint4*>(buf + (lo - 1) * kRowB + 16 * lane);
+    const uint4 dn = *reinterpret_cast<const uint4*>(buf + hi * kRowB + 16 * lane);
+    __syncthreads();
+    uint32_t ha[4], hb[4], hc[4], ca[4], cb[4], cc[4];
+    uint32_t diff = 0;
+    if (lo < hi) {
+      hsum(up, ha, ca);
+      hsum(*reinterpret_cast<const uint4*>(buf + lo * kRowB + 16 * lane), hb, cb);
+      for (int i = lo; i < hi; ++i) {
+        hsum(i + 1 < hi ? *reinterpret_cast<const uint4*>(buf + (i + 1) * kRowB + 16 * lane) : dn, hc, cc);
+        uint32_t nx[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nx[k] = rule_bytes(ha[k] + hb[k] + hc[k], cb[k]);
+        const int64_t row = r0 - T + i;
+        const bool counted = i >= T && i < T + kTH && row < row_hi;
+        if (counted) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) diff |= (nx[k] ^ cb[k]) & own[k];
+        }
+        if (g < T) {
+          *reinterpret_cast<uint4*>(buf + i * kRowB + 16 * lane) = make_uint4(nx[0], nx[1], nx[2], nx[3]);
+        } else if (counted && lane >= 1 && lane <= 62 && cell < c_end) {
+          *reinterpret_cast<uint4*>(out + row * pitch + cell) = make_uint4(nx[0], nx[1], nx[2], nx[3]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          ha[k] = hb[k];
+          hb[k] = hc[k];
+          ca[k] = cb[k];
+          cb[k] = cc[k];
+        }
+      }
+    }
+    if (flags && __ballot(diff != 0u) != 0ull && lane == 0) flags[g - 1] = 1u;  // idempotent plain store
+    if (g < T) __syncthreads();
+  }
+}
+
 }  // namespace
+
+int lds_multi_tile_rows(int T) { return kMultiRows - 2 * T; }
+
+void launch_life_lds_multi(const BlockArgs& a, bool wrap, hipStream_t stream) {
+  const TileGeom& g = a.g;
+  GOL_REQUIRE(g.layout == Layout::U8, "life_lds_multi: byte layout only");
+  GOL_REQUIRE(a.T == 2 || a.T == 4 || a.T == 8, "life_lds_multi: T = 2, 4 or 8");
+  GOL_REQUIRE(a.row_lo >= a.T && a.row_hi + a.T <= g.R() && a.row_lo < a.row_hi,
+              "life_lds_multi: row range outside the tile");
+  GOL_REQUIRE(g.pitch % 16 == 0 && g.cell0() % 16 == 0, "life_lds_multi: 16-byte aligned rows and owned cells");
+  const int64_t rows = a.row_hi - a.row_lo;
+  uint32_t* changed = a.changed ? a.changed + (a.gen_dev ? a.gen_rel : a.gen_base + 1 - a.flags_base) : nullptr;
+  const int64_t* gen_dev = a.changed ? a.gen_dev : nullptr;
+  const int64_t wrap_w = wrap && a.full_width && g.hw == 0 && g.W % 16 == 0 ? g.W : 0;
+  const int64_t wrap_h = wrap_w && a.wrap_rows ? g.H : 0;
+  GOL_REQUIRE(!a.wrap_rows || wrap_h, "life_lds_multi: row wrap needs a whole-width tile without halo columns");
+  GOL_REQUIRE(wrap_w || 32 * g.hw >= 16, "life_lds_multi: a tile without halo columns needs column wrap");
+  const int th = lds_multi_tile_rows(a.T);
+  // Wrap: tiles cover the owned cells [cell0, cell0 + W), the chunk staged
+  // left of the first one being the wrapped last chunk.  Halo mode: tiles
+  // cover the whole padded row [0, Wc), halo columns included - a block's
+  // output feeds the next block of the epoch, whose halo columns must be the
+  // evolved ones (valid up to the light cone from the padded row's ends).
+  const int64_t c_first = wrap_w ? g.cell0() : 0;
+  const int64_t c_end = wrap_w ? g.cell0() + g.W : g.Wc();
+  const dim3 grid(unsigned(ceil_div(c_end - c_first, int64_t(kMultiOwn))), unsigned(ceil_div(rows, int64_t(th))));
+  auto k = a.T == 2 ? life_lds_multi_kernel<2> : a.T == 4 ? life_lds_multi_kernel<4> : life_lds_multi_kernel<8>;
+  hipLaunchKernelGGL(k, grid, dim3(512), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
+                     g.pitch, a.row_lo, a.row_hi, g.Wc(), g.cell0(), g.cell0() + g.W, changed, gen_dev, wrap_w, wrap_h,
+                     g.row0(), c_first, c_end);
+}
 
 void launch_life_step_lds(const BlockArgs& a, int lds_rows, bool wrap, hipStream_t stream) {
   const TileGeom& g = a.g;

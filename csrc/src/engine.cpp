@@ -104,11 +104,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // Whole-width tiles on a backend that wraps column reads (lane_cols in the
   // HIP kernels) never read their halo columns: no column fills.
   cols_filled_ = !(dec_.Px == 1 && cfg_.W % 32 == 0 && be_->wraps_columns(cl));
-  // A single-rank torus on a backend that also wraps row reads (the T = 1
-  // LDS kernel): one-generation epochs over the owned rows, no fills at all.
-  rows_wrapped_ = !cols_filled_ && dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && tmax_ == 1 &&
+  // A single-rank torus on a backend that also wraps row reads (the LDS-tiled
+  // byte kernels): one block per epoch over the owned rows, no fills at all.
+  rows_wrapped_ = !cols_filled_ && dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !resident_ &&
                   be_->wraps_rows(cl);
-  if (rows_wrapped_) D_ = 1;
+  if (rows_wrapped_) D_ = tmax_;  // one block per epoch; nothing to fill or exchange
   // Halo columns: none when the kernels wrap (smaller rows to exchange and
   // fill); else D cells per side, 2D on the left for the drifting window.
   int hw = cols_filled_ ? int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32)) : 0;
