@@ -39,7 +39,8 @@ const char* xlane_name(int x) {
 std::string life_block_variant(Layout layout, const LifeTuning& tune) {
   const int w = words_per_lane(layout, tune);
   if (layout == Layout::U8 && tune.u8_lds)
-    return tune.lds_T > 1 ? "u8 lds-tiled T=" + std::to_string(tune.lds_T) : std::string("u8 lds-tiled single-step");
+    return tune.lds_T > 1 ? "u8 lds-tiled T=" + std::to_string(tune.lds_T) + (tune.lds_pack && tune.lds_T >= 8 ? " packed" : "")
+                          : std::string("u8 lds-tiled single-step");
   const bool grouped = tune.group != 0 && tune.split == 0 && !tune.skew;
   return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=" + std::to_string(w) + " " +
          xlane_name(xlane_of(layout, w, tune)) + (tune.skew ? " skew" : "") +
@@ -99,12 +100,17 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   p.fold_lanes = 64;
   const int64_t rows = a.row_hi - a.row_lo;
   int x = xlane_of(g.layout, w, tune);
-  if (g.layout == Layout::U8 && tune.u8_lds && (a.T == 1 || a.T == 2 || a.T == 4 || a.T == 8)) {
+  if (g.layout == Layout::U8 && tune.u8_lds && (a.T == 1 || a.T == 2 || a.T == 4 || a.T == 8 || a.T == 16 || a.T == 32)) {
     BlockArgs b = a;
     b.dual_offset = 0;
+    // Packed tiles need 32-cell aligned rows (pitch) and owned cells.
+    const bool pack = a.T >= 8 && (tune.lds_pack || a.T > 8) && g.pitch % 32 == 0 && g.cell0() % 32 == 0;
+    GOL_REQUIRE(a.T <= 8 || pack, "life_block: LDS-tiled byte passes deeper than 8 need the packed tile");
     for (int half = 0; half < (a.dual_offset ? 2 : 1); ++half) {
       if (a.T == 1)
         launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
+      else if (pack)
+        launch_life_lds_bits(b, tune.wrap, stream);
       else
         launch_life_lds_multi(b, tune.wrap, stream);
       b.row_lo += a.dual_offset;

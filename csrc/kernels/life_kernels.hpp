@@ -137,7 +137,8 @@ struct LifeTuning {
   int xlane = kXlaneAuto;   // cross-lane primitive
   bool u8_lds = false;      // byte layout: single-step LDS-tiled kernel (T = 1)
   int lds_rows = 32;        // rows per LDS tile (32 or 64)
-  int lds_T = 8;            // generations per launch of the LDS-tiled byte kernel (1, 2, 4, 8)
+  int lds_T = 8;            // generations per launch of the LDS-tiled byte kernel (1, 2, 4, 8; 16, 32 packed)
+  bool lds_pack = true;     // LDS-tiled byte kernel evaluates on bit words packed in LDS (T >= 8)
   int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
   int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
@@ -245,6 +246,9 @@ void launch_life_step_lds(const BlockArgs& a, int lds_rows, bool wrap, hipStream
 // The same with T = 2, 4 or 8 generations per launch through two LDS row
 // buffers (life_step_lds.hip life_lds_multi_kernel).
 void launch_life_lds_multi(const BlockArgs& a, bool wrap, hipStream_t stream);
+// The same tile packed to bit words in LDS (T = 8, 16 or 32 generations per
+// launch, bit-sliced rule; life_step_lds.hip life_lds_bits_kernel).
+void launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

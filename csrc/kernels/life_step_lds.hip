@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include "gol/common.hpp"
+#include "life_block_impl.hpp"  // bit-sliced rule, byte <-> bit packing (U8IO)
 #include "life_kernels.hpp"
 
 namespace gol {
@@ -307,9 +308,149 @@ __global__ __launch_bounds__(512) void life_lds_multi_kernel(const uint8_t* __re
   }
 }
 
+// ---- T generations per launch on a bit-packed LDS tile ---------------------
+// Byte-per-cell storage, bit-sliced evaluation: a 512-thread workgroup stages
+// a 128-row x 2048-cell tile of bytes (64 words of 32 cells per row: 62
+// owned words plus one halo word per side; T halo rows per side), packs each
+// 32-byte run into a bit word (v_dot4, U8IO::pack) in LDS (32 KB), evaluates
+// T generations in place with the bit-sliced rule (DPP neighbour words,
+// 15 VALU ops per 32 cells instead of ~60 per 16 with bytes), the eight
+// waves splitting the rows as in the byte kernel, and unpacks the last
+// generation to bytes on the way out.  One halo word holds 32 generations of
+// the symmetric light cone.
+constexpr int kBitRows = 128;                         // LDS rows
+constexpr int kBitOwnWords = 62;                      // owned words per tile row
+constexpr int kBitStageBatch = 4;                     // words staged per thread per batch
+
+template <int T>
+__global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __restrict__ in,
+                                                            uint8_t* __restrict__ out, int64_t pitch,
+                                                            int64_t row_lo, int64_t row_hi, int64_t own_c0,
+                                                            int64_t own_c1, uint32_t* changed,
+                                                            const int64_t* gen_dev, int64_t wrap_w, int64_t wrap_h,
+                                                            int64_t row0, int64_t c_first, int64_t c_end) {
+  static_assert(T >= 1 && T <= 32, "one halo word holds 32 generations of the light cone");
+  constexpr int kTH = kBitRows - 2 * T;
+  using IO = lb::U8IO<1, kXlaneDpp>;
+  __shared__ uint32_t bits[kBitRows * 64];
+  const int64_t r0 = row_lo + int64_t(blockIdx.y) * kTH;                   // first output row
+  const int64_t c0 = c_first - 32 + int64_t(blockIdx.x) * (32 * kBitOwnWords);  // first staged cell
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // Stage: word idx = tid + 512 k (row idx / 64, word idx % 64), 32 bytes each.
+  constexpr int kWords = kBitRows * 64 / 512;
+#pragma unroll
+  for (int k0 = 0; k0 < kWords; k0 += kBitStageBatch) {
+    uint4 v[kBitStageBatch][2];
+    bool ok[kBitStageBatch];
+#pragma unroll
+    for (int kk = 0; kk < kBitStageBatch; ++kk) {
+      const int idx = tid + 512 * (k0 + kk);
+      const int lr = idx >> 6, wl = idx & 63;
+      const int64_t gr = r0 - T + lr;
+      const int64_t gc = c0 + 32 * int64_t(wl);
+      int64_t grc = gr < row_hi + T ? gr : row_hi + T - 1;
+      int64_t gcc = gc < 0 ? 0 : (gc + 32 <= pitch ? gc : pitch - 32);
+      if (wrap_h) grc = row0 + (((grc - row0) % wrap_h) + wrap_h) % wrap_h;
+      if (wrap_w) gcc = min(((gc % wrap_w) + wrap_w) % wrap_w, pitch - 32);
+      ok[kk] = gr < row_hi + T && (wrap_w ? true : gc >= 0 && gc + 32 <= pitch);
+      const uint4* q = reinterpret_cast<const uint4*>(in + grc * pitch + gcc);
+      v[kk][0] = q[0];
+      v[kk][1] = q[1];
+    }
+#pragma unroll
+    for (int kk = 0; kk < kBitStageBatch; ++kk)
+      bits[tid + 512 * (k0 + kk)] = ok[kk] ? IO::pack(v[kk][0], v[kk][1]) : 0u;
+  }
+  __syncthreads();
+
+  // Owned-cell bits of this lane's word (changed flags): lanes 1..62.
+  const int64_t cell = c0 + 32 * int64_t(lane);
+  uint32_t own = 0;
+  if (lane >= 1 && lane <= kBitOwnWords) {
+    const int64_t a = max(own_c0, cell), b = min(own_c1, cell + 32);
+    if (a < b) own = (b - a >= 32 ? 0xFFFFFFFFu : ((1u << (b - a)) - 1u)) << (a - cell);
+  }
+  uint32_t* flags = changed ? (gen_dev ? changed + *gen_dev : changed) : nullptr;
+
+  // Horizontal 3-sums of a row word (cells x-1, x, x+1; DPP neighbour words).
+  auto hsum = [&](uint32_t c, uint32_t& h0, uint32_t& h1) {
+    const uint32_t lw = __builtin_amdgcn_mov_dpp(c, 0x138, 0xF, 0xF, true);  // wave_shr:1 (lane 0: 0)
+    const uint32_t rw = __builtin_amdgcn_mov_dpp(c, 0x130, 0xF, 0xF, true);  // wave_shl:1 (lane 63: 0)
+    const uint32_t l = __builtin_amdgcn_alignbit(c, lw, 31);
+    const uint32_t r = __builtin_amdgcn_alignbit(rw, c, 1);
+    h0 = lb::bop3<tt::XOR3>(l, c, r);
+    h1 = lb::bop3<tt::MAJ>(l, c, r);
+  };
+
+#pragma unroll 1
+  for (int g = 1; g <= T; ++g) {
+    const int n = kBitRows - 2 * g;
+    const int lo = g + (n * w) / 8, hi = g + (n * (w + 1)) / 8;
+    const uint32_t up = bits[(lo - 1) * 64 + lane];
+    const uint32_t dn = bits[hi * 64 + lane];
+    __syncthreads();
+    uint32_t diff = 0;
+    if (lo < hi) {
+      uint32_t a0, a1, b0, b1, c0w, c1w;
+      hsum(up, a0, a1);
+      uint32_t cb = bits[lo * 64 + lane];
+      hsum(cb, b0, b1);
+      for (int i = lo; i < hi; ++i) {
+        const uint32_t cc = i + 1 < hi ? bits[(i + 1) * 64 + lane] : dn;
+        hsum(cc, c0w, c1w);
+        const uint32_t nx = lb::rule(a0, a1, b0, b1, c0w, c1w, cb);
+        const int64_t row = r0 - T + i;
+        const bool counted = i >= T && i < T + kTH && row < row_hi;
+        if (counted) diff |= (nx ^ cb) & own;
+        if (g < T) {
+          bits[i * 64 + lane] = nx;
+        } else if (counted && lane >= 1 && lane <= kBitOwnWords && cell < c_end) {
+          uint4* o = reinterpret_cast<uint4*>(out + row * pitch + cell);
+          o[0] = make_uint4(IO::spread(nx, 0), IO::spread(nx, 1), IO::spread(nx, 2), IO::spread(nx, 3));
+          o[1] = make_uint4(IO::spread(nx, 4), IO::spread(nx, 5), IO::spread(nx, 6), IO::spread(nx, 7));
+        }
+        a0 = b0;
+        a1 = b1;
+        b0 = c0w;
+        b1 = c1w;
+        cb = cc;
+      }
+    }
+    if (flags && __ballot(diff != 0u) != 0ull && lane == 0) flags[g - 1] = 1u;  // idempotent plain store
+    if (g < T) __syncthreads();
+  }
+}
+
 }  // namespace
 
 int lds_multi_tile_rows(int T) { return kMultiRows - 2 * T; }
+
+void launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream) {
+  const TileGeom& g = a.g;
+  GOL_REQUIRE(g.layout == Layout::U8, "life_lds_bits: byte layout only");
+  GOL_REQUIRE(a.T == 8 || a.T == 16 || a.T == 32, "life_lds_bits: T = 8, 16 or 32");
+  GOL_REQUIRE(a.row_lo >= a.T && a.row_hi + a.T <= g.R() && a.row_lo < a.row_hi,
+              "life_lds_bits: row range outside the tile");
+  GOL_REQUIRE(g.pitch % 32 == 0 && g.cell0() % 32 == 0, "life_lds_bits: 32-byte aligned rows and owned cells");
+  const int64_t rows = a.row_hi - a.row_lo;
+  uint32_t* changed = a.changed ? a.changed + (a.gen_dev ? a.gen_rel : a.gen_base + 1 - a.flags_base) : nullptr;
+  const int64_t* gen_dev = a.changed ? a.gen_dev : nullptr;
+  const int64_t wrap_w = wrap && a.full_width && g.hw == 0 && g.W % 32 == 0 ? g.W : 0;
+  const int64_t wrap_h = wrap_w && a.wrap_rows ? g.H : 0;
+  GOL_REQUIRE(!a.wrap_rows || wrap_h, "life_lds_bits: row wrap needs a whole-width tile without halo columns");
+  GOL_REQUIRE(wrap_w || 32 * g.hw >= a.T, "life_lds_bits: a tile without column wrap needs T halo cells");
+  // Tiles as in launch_life_lds_multi: owned cells (wrap) or the padded row.
+  const int64_t c_first = wrap_w ? g.cell0() : 0;
+  const int64_t c_end = wrap_w ? g.cell0() + g.W : g.Wc();
+  const int th = kBitRows - 2 * a.T;
+  const dim3 grid(unsigned(ceil_div(c_end - c_first, int64_t(32 * kBitOwnWords))), unsigned(ceil_div(rows, int64_t(th))));
+  auto k = a.T == 8 ? life_lds_bits_kernel<8> : a.T == 16 ? life_lds_bits_kernel<16> : life_lds_bits_kernel<32>;
+  hipLaunchKernelGGL(k, grid, dim3(512), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
+                     g.pitch, a.row_lo, a.row_hi, g.cell0(), g.cell0() + g.W, changed, gen_dev, wrap_w, wrap_h,
+                     g.row0(), c_first, c_end);
+}
 
 void launch_life_lds_multi(const BlockArgs& a, bool wrap, hipStream_t stream) {
   const TileGeom& g = a.g;

@@ -266,6 +266,11 @@ int64_t Engine::alive_count() {
 
 int Engine::pick_T(int64_t remaining) const {
   if (resident_) return int(std::min<int64_t>(remaining, tmax_));  // any T: one launch per epoch
+  if (rows_wrapped_) {  // the LDS-tiled byte kernels: T = 1, 2, 4, ... (powers of two)
+    int t = 1;
+    while (2 * t <= tmax_ && 2 * t <= remaining) t *= 2;
+    return t;
+  }
   for (int t : kTSizes)
     if (t <= tmax_ && t <= remaining) return t;
   return 1;

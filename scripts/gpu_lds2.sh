@@ -19,7 +19,10 @@ run() {
 }
 for S in 8192 32768; do
   st=20; [ $S = 32768 ] && st=3
-  for t in 1 2 4 8; do
-    run "lds T$t $S" GOL_U8_KERNEL=lds GOL_LDS_T=$t -- --size $S --steps $st --warmup 1 || exit $?
+  for t in 8; do
+    run "lds bytes T$t $S" GOL_U8_KERNEL=lds GOL_LDS_PACK=0 GOL_LDS_T=$t -- --size $S --steps $st --warmup 1 || exit $?
+  done
+  for t in 8 16 32; do
+    run "lds packed T$t $S" GOL_U8_KERNEL=lds GOL_LDS_PACK=1 GOL_LDS_T=$t -- --size $S --steps $st --warmup 1 || exit $?
   done
 done
