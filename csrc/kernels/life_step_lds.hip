@@ -318,7 +318,10 @@ __global__ __launch_bounds__(512) void life_lds_multi_kernel(const uint8_t* __re
 // waves splitting the rows as in the byte kernel, and unpacks the last
 // generation to bytes on the way out.  One halo word holds 32 generations of
 // the symmetric light cone.
-constexpr int kBitRows = 128;                         // LDS rows
+#ifndef GOL_LDS_BIT_ROWS
+#define GOL_LDS_BIT_ROWS 128
+#endif
+constexpr int kBitRows = GOL_LDS_BIT_ROWS;            // LDS rows (128: 32 KB, four workgroups per CU)
 constexpr int kBitOwnWords = 62;                      // owned words per tile row
 constexpr int kBitStageBatch = 4;                     // words staged per thread per batch
 

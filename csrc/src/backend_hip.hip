@@ -83,7 +83,8 @@ class HipBackend final : public Backend {
     if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
     tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
     tune_.lds_pack = env_int("GOL_LDS_PACK", 1) != 0;
-    tune_.lds_T = env_int("GOL_LDS_T", tune_.lds_pack ? 16 : 8);  // bytes 8192^2: T = 1 26.6, 2 24.9, 4 20.4, 8 17.9 us/gen
+    // 8192^2 per generation: bytes T = 1 26.6, 2 24.9, 4 20.4, 8 17.9 us; packed T = 8 6.5, 16 4.9, 32 4.7
+    tune_.lds_T = env_int("GOL_LDS_T", tune_.lds_pack ? 32 : 8);
     GOL_REQUIRE(tune_.lds_T == 1 || tune_.lds_T == 2 || tune_.lds_T == 4 || tune_.lds_T == 8 ||
                     (tune_.lds_pack && (tune_.lds_T == 16 || tune_.lds_T == 32)),
                 "GOL_LDS_T must be 1, 2, 4 or 8 (16 or 32 with the packed tile, GOL_LDS_PACK=1)");
