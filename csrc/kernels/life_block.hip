@@ -106,17 +106,18 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
     // Packed tiles need 32-cell aligned rows (pitch) and owned cells.
     const bool pack = a.T >= 8 && (tune.lds_pack || a.T > 8) && g.pitch % 32 == 0 && g.cell0() % 32 == 0;
     GOL_REQUIRE(a.T <= 8 || pack, "life_block: LDS-tiled byte passes deeper than 8 need the packed tile");
+    int drift = 0;
     for (int half = 0; half < (a.dual_offset ? 2 : 1); ++half) {
       if (a.T == 1)
         launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
       else if (pack)
-        launch_life_lds_bits(b, tune.wrap, stream);
+        drift = launch_life_lds_bits(b, tune.wrap, stream);
       else
         launch_life_lds_multi(b, tune.wrap, stream);
       b.row_lo += a.dual_offset;
       b.row_hi += a.dual_offset;
     }
-    return 0;
+    return drift;
   }
   // The adder window drifts the storage frame by T cells (see kXlaneAdd); the
   // engine allows that only for whole-width tiles of 32-cell words, and the

@@ -247,8 +247,10 @@ void launch_life_step_lds(const BlockArgs& a, int lds_rows, bool wrap, hipStream
 // buffers (life_step_lds.hip life_lds_multi_kernel).
 void launch_life_lds_multi(const BlockArgs& a, bool wrap, hipStream_t stream);
 // The same tile packed to bit words in LDS (T = 8, 16 or 32 generations per
-// launch, bit-sliced rule; life_step_lds.hip life_lds_bits_kernel).
-void launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream);
+// launch, bit-sliced rule; life_step_lds.hip life_lds_bits_kernel).  Returns
+// the drift of the stored frame (T with the adder window, which it runs
+// where BlockArgs::allow_drift and the tile wraps its columns; else 0).
+int launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

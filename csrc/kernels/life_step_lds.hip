@@ -325,19 +325,26 @@ constexpr int kBitRows = GOL_LDS_BIT_ROWS;            // LDS rows (128: 32 KB, f
 constexpr int kBitOwnWords = 62;                      // owned words per tile row
 constexpr int kBitStageBatch = 4;                     // words staged per thread per batch
 
-template <int T>
+// ADD: the adder window (life_block_impl.hpp kXlaneAdd: no DPP / v_alignbit
+// in the level body, the stored frame drifts one cell right per generation;
+// whole-width torus tiles only).  Its light cone is one-sided, 2 cells per
+// generation on the left, so the tile keeps ceil(2T / 32) halo words on the
+// left and none on the right.
+template <int T, bool ADD>
 __global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __restrict__ in,
                                                             uint8_t* __restrict__ out, int64_t pitch,
                                                             int64_t row_lo, int64_t row_hi, int64_t own_c0,
                                                             int64_t own_c1, uint32_t* changed,
                                                             const int64_t* gen_dev, int64_t wrap_w, int64_t wrap_h,
                                                             int64_t row0, int64_t c_first, int64_t c_end) {
-  static_assert(T >= 1 && T <= 32, "one halo word holds 32 generations of the light cone");
+  static_assert(T >= 1 && T <= 32, "at most 32 generations of the light cone per launch");
   constexpr int kTH = kBitRows - 2 * T;
+  constexpr int kHL = ADD ? (2 * T + 31) / 32 : 1, kHR = ADD ? 0 : 1;  // halo words left / right
+  constexpr int kOwn = 64 - kHL - kHR;                                   // owned words per tile row
   using IO = lb::U8IO<1, kXlaneDpp>;
   __shared__ uint32_t bits[kBitRows * 64];
-  const int64_t r0 = row_lo + int64_t(blockIdx.y) * kTH;                   // first output row
-  const int64_t c0 = c_first - 32 + int64_t(blockIdx.x) * (32 * kBitOwnWords);  // first staged cell
+  const int64_t r0 = row_lo + int64_t(blockIdx.y) * kTH;                          // first output row
+  const int64_t c0 = c_first - 32 * kHL + int64_t(blockIdx.x) * (32 * kOwn);    // first staged cell
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -368,23 +375,34 @@ __global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __res
   }
   __syncthreads();
 
-  // Owned-cell bits of this lane's word (changed flags): lanes 1..62.
+  // Owned-cell bits of this lane's word (changed flags).
   const int64_t cell = c0 + 32 * int64_t(lane);
+  const bool own_lane = lane >= kHL && lane < 64 - kHR;
   uint32_t own = 0;
-  if (lane >= 1 && lane <= kBitOwnWords) {
+  if (own_lane) {
     const int64_t a = max(own_c0, cell), b = min(own_c1, cell + 32);
     if (a < b) own = (b - a >= 32 ? 0xFFFFFFFFu : ((1u << (b - a)) - 1u)) << (a - cell);
   }
   uint32_t* flags = changed ? (gen_dev ? changed + *gen_dev : changed) : nullptr;
 
-  // Horizontal 3-sums of a row word (cells x-1, x, x+1; DPP neighbour words).
-  auto hsum = [&](uint32_t c, uint32_t& h0, uint32_t& h1) {
-    const uint32_t lw = __builtin_amdgcn_mov_dpp(c, 0x138, 0xF, 0xF, true);  // wave_shr:1 (lane 0: 0)
-    const uint32_t rw = __builtin_amdgcn_mov_dpp(c, 0x130, 0xF, 0xF, true);  // wave_shl:1 (lane 63: 0)
-    const uint32_t l = __builtin_amdgcn_alignbit(c, lw, 31);
-    const uint32_t r = __builtin_amdgcn_alignbit(rw, c, 1);
-    h0 = lb::bop3<tt::XOR3>(l, c, r);
-    h1 = lb::bop3<tt::MAJ>(l, c, r);
+  // Horizontal 3-sums of a row word and the centre the rule uses: cells
+  // x-1, x, x+1 (DPP neighbour words), or with ADD x-2, x-1, x (centre x-1).
+  auto hsum = [&](uint32_t c, uint32_t& h0, uint32_t& h1, uint32_t& ctr) {
+    if constexpr (ADD) {
+      uint32_t l1, l2;
+      lb::adder_window(c, l1, l2);
+      h0 = lb::bop3<tt::XOR3>(l2, l1, c);
+      h1 = lb::bop3<tt::MAJ>(l2, l1, c);
+      ctr = l1;
+    } else {
+      const uint32_t lw = __builtin_amdgcn_mov_dpp(c, 0x138, 0xF, 0xF, true);  // wave_shr:1 (lane 0: 0)
+      const uint32_t rw = __builtin_amdgcn_mov_dpp(c, 0x130, 0xF, 0xF, true);  // wave_shl:1 (lane 63: 0)
+      const uint32_t l = __builtin_amdgcn_alignbit(c, lw, 31);
+      const uint32_t r = __builtin_amdgcn_alignbit(rw, c, 1);
+      h0 = lb::bop3<tt::XOR3>(l, c, r);
+      h1 = lb::bop3<tt::MAJ>(l, c, r);
+      ctr = c;
+    }
   };
 
 #pragma unroll 1
@@ -396,20 +414,19 @@ __global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __res
     __syncthreads();
     uint32_t diff = 0;
     if (lo < hi) {
-      uint32_t a0, a1, b0, b1, c0w, c1w;
-      hsum(up, a0, a1);
-      uint32_t cb = bits[lo * 64 + lane];
-      hsum(cb, b0, b1);
+      uint32_t a0, a1, actr, b0, b1, bctr, c0w, c1w, cctr;
+      hsum(up, a0, a1, actr);
+      hsum(bits[lo * 64 + lane], b0, b1, bctr);
       for (int i = lo; i < hi; ++i) {
         const uint32_t cc = i + 1 < hi ? bits[(i + 1) * 64 + lane] : dn;
-        hsum(cc, c0w, c1w);
-        const uint32_t nx = lb::rule(a0, a1, b0, b1, c0w, c1w, cb);
+        hsum(cc, c0w, c1w, cctr);
+        const uint32_t nx = lb::rule(a0, a1, b0, b1, c0w, c1w, bctr);
         const int64_t row = r0 - T + i;
         const bool counted = i >= T && i < T + kTH && row < row_hi;
-        if (counted) diff |= (nx ^ cb) & own;
+        if (counted) diff |= (nx ^ bctr) & own;
         if (g < T) {
           bits[i * 64 + lane] = nx;
-        } else if (counted && lane >= 1 && lane <= kBitOwnWords && cell < c_end) {
+        } else if (counted && own_lane && cell < c_end) {
           uint4* o = reinterpret_cast<uint4*>(out + row * pitch + cell);
           o[0] = make_uint4(IO::spread(nx, 0), IO::spread(nx, 1), IO::spread(nx, 2), IO::spread(nx, 3));
           o[1] = make_uint4(IO::spread(nx, 4), IO::spread(nx, 5), IO::spread(nx, 6), IO::spread(nx, 7));
@@ -418,7 +435,7 @@ __global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __res
         a1 = b1;
         b0 = c0w;
         b1 = c1w;
-        cb = cc;
+        bctr = cctr;
       }
     }
     if (flags && __ballot(diff != 0u) != 0ull && lane == 0) flags[g - 1] = 1u;  // idempotent plain store
@@ -430,7 +447,7 @@ __global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __res
 
 int lds_multi_tile_rows(int T) { return kMultiRows - 2 * T; }
 
-void launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream) {
+int launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream) {
   const TileGeom& g = a.g;
   GOL_REQUIRE(g.layout == Layout::U8, "life_lds_bits: byte layout only");
   GOL_REQUIRE(a.T == 8 || a.T == 16 || a.T == 32, "life_lds_bits: T = 8, 16 or 32");
@@ -444,15 +461,23 @@ void launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream) {
   const int64_t wrap_h = wrap_w && a.wrap_rows ? g.H : 0;
   GOL_REQUIRE(!a.wrap_rows || wrap_h, "life_lds_bits: row wrap needs a whole-width tile without halo columns");
   GOL_REQUIRE(wrap_w || 32 * g.hw >= a.T, "life_lds_bits: a tile without column wrap needs T halo cells");
+  // The adder window where the engine allows a drifting frame (whole-width
+  // torus rows, read modulo the width); the DPP window elsewhere.
+  const bool add = a.allow_drift && wrap_w != 0;
   // Tiles as in launch_life_lds_multi: owned cells (wrap) or the padded row.
   const int64_t c_first = wrap_w ? g.cell0() : 0;
   const int64_t c_end = wrap_w ? g.cell0() + g.W : g.Wc();
   const int th = kBitRows - 2 * a.T;
-  const dim3 grid(unsigned(ceil_div(c_end - c_first, int64_t(32 * kBitOwnWords))), unsigned(ceil_div(rows, int64_t(th))));
-  auto k = a.T == 8 ? life_lds_bits_kernel<8> : a.T == 16 ? life_lds_bits_kernel<16> : life_lds_bits_kernel<32>;
+  const int own_words = add ? 64 - (2 * a.T + 31) / 32 : 62;
+  const dim3 grid(unsigned(ceil_div(c_end - c_first, int64_t(32 * own_words))), unsigned(ceil_div(rows, int64_t(th))));
+  auto k = add ? (a.T == 8 ? life_lds_bits_kernel<8, true> : a.T == 16 ? life_lds_bits_kernel<16, true>
+                                                                       : life_lds_bits_kernel<32, true>)
+               : (a.T == 8 ? life_lds_bits_kernel<8, false> : a.T == 16 ? life_lds_bits_kernel<16, false>
+                                                                        : life_lds_bits_kernel<32, false>);
   hipLaunchKernelGGL(k, grid, dim3(512), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
                      g.pitch, a.row_lo, a.row_hi, g.cell0(), g.cell0() + g.W, changed, gen_dev, wrap_w, wrap_h,
                      g.row0(), c_first, c_end);
+  return add ? a.T : 0;
 }
 
 void launch_life_lds_multi(const BlockArgs& a, bool wrap, hipStream_t stream) {

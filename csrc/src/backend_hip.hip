@@ -83,6 +83,7 @@ class HipBackend final : public Backend {
     if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
     tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
     tune_.lds_pack = env_int("GOL_LDS_PACK", 1) != 0;
+    lds_add_ = env_int("GOL_LDS_ADD", 0) != 0;  // packed LDS tile: adder window (drifting frame)
     // 8192^2 per generation: bytes T = 1 26.6, 2 24.9, 4 20.4, 8 17.9 us; packed T = 8 6.5, 16 4.9, 32 4.7
     tune_.lds_T = env_int("GOL_LDS_T", tune_.lds_pack ? 32 : 8);
     GOL_REQUIRE(tune_.lds_T == 1 || tune_.lds_T == 2 || tune_.lds_T == 4 || tune_.lds_T == 8 ||
@@ -576,6 +577,9 @@ class HipBackend final : public Backend {
     return e;
   }
   bool drifts(Layout l) const override {
+    if (l == Layout::U8 && tune_.u8_lds)  // the packed LDS tile (adder window), not the byte kernels
+      return lds_add_ && tune_.lds_pack && tune_.lds_T >= 8 &&
+             (tune_.xlane == hipk::kXlaneAuto || tune_.xlane == hipk::kXlaneAdd);
     return tune_.xlane == hipk::kXlaneAdd && (l == Layout::Bits ? tune_.wpl_bits < 2 : true);
   }
   // The adder window (kXlaneAdd) beats the DPP window only at four resident
@@ -618,7 +622,12 @@ class HipBackend final : public Backend {
           }
     }
     const bool one_word = l == Layout::U8 || tune_.wpl_bits < 2;
-    if (tune_.xlane == hipk::kXlaneAdd && one_word) {
+    // The packed LDS-tiled byte kernel runs the adder window (drifting frame)
+    // wherever the engine allows it (whole-width torus rows).
+    if (l == Layout::U8 && tune_.u8_lds && lds_add_ && tune_.lds_pack && k.tmax >= 8 &&
+        (tune_.xlane == hipk::kXlaneAuto || tune_.xlane == hipk::kXlaneAdd))
+      k.drift = true;
+    if (tune_.xlane == hipk::kXlaneAdd && one_word && !(l == Layout::U8 && tune_.u8_lds)) {
       k.drift = true;
       if (tmax_req <= 0) k.tmax = 12;
     } else if (tune_.xlane == hipk::kXlaneAuto && l == Layout::Bits && one_word && !tune_.skew &&
@@ -855,6 +864,7 @@ class HipBackend final : public Backend {
   void* chain_[8] = {};
   size_t chain_bytes_[8] = {};
   int resident_mode_ = 0, resident_k_ = 8, resident_D_ = 0, resident_probe_ = 0;
+  bool lds_add_ = false;  // GOL_LDS_ADD
   int64_t resident_launches_ = 0, res_trace_at_ = -1;
   std::string res_trace_path_;
   hipk::LinkState link_;  // linked launches (GOL_LINK)

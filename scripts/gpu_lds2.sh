@@ -6,6 +6,8 @@ O=gpurun_out/lds2
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu.py -m gpu -k "lds" -q --timeout 120 --timeout-method thread > $O/pytest_lds.log 2>&1
 rc=$?; echo "lds tests rc=$rc"; grep -E "^FAILED|passed|failed" $O/pytest_lds.log | tail -8; [ $rc -eq 0 ] || exit $rc
+GOL_LDS_ADD=1 timeout -k 10 600 python -u -m pytest tests/test_gpu.py -m gpu -k "lds" -q --timeout 120 --timeout-method thread > $O/pytest_lds_add.log 2>&1
+rc=$?; echo "lds tests (adder) rc=$rc"; grep -E "^FAILED|passed|failed" $O/pytest_lds_add.log | tail -8; [ $rc -eq 0 ] || exit $rc
 T=$O/lds.jsonl; : > $T
 run() {
   local label=$1; shift
@@ -22,7 +24,8 @@ for S in 8192 32768; do
   for t in 8; do
     run "lds bytes T$t $S" GOL_U8_KERNEL=lds GOL_LDS_PACK=0 GOL_LDS_T=$t -- --size $S --steps $st --warmup 1 || exit $?
   done
-  for t in 8 16 32; do
+  for t in 16 32; do
     run "lds packed T$t $S" GOL_U8_KERNEL=lds GOL_LDS_PACK=1 GOL_LDS_T=$t -- --size $S --steps $st --warmup 1 || exit $?
+    run "lds packed adder T$t $S" GOL_U8_KERNEL=lds GOL_LDS_ADD=1 GOL_LDS_PACK=1 GOL_LDS_T=$t -- --size $S --steps $st --warmup 1 || exit $?
   done
 done
