@@ -319,9 +319,13 @@ __global__ __launch_bounds__(512) void life_lds_multi_kernel(const uint8_t* __re
 // generation to bytes on the way out.  One halo word holds 32 generations of
 // the symmetric light cone.
 #ifndef GOL_LDS_BIT_ROWS
-#define GOL_LDS_BIT_ROWS 128
+#define GOL_LDS_BIT_ROWS 160
 #endif
-constexpr int kBitRows = GOL_LDS_BIT_ROWS;            // LDS rows (128: 32 KB, four workgroups per CU)
+// LDS rows: 160 (40 KB) still fits four workgroups in a CU's 160 KB and
+// recomputes fewer light-cone rows per owned row than 128 (T = 32: 1.32x vs
+// 1.48x); measured +1 % at 8192^2, +12 % at 32768^2, 192 rows (three per CU)
+// slower (profiles/r03/lds_packed_rows_160.jsonl).
+constexpr int kBitRows = GOL_LDS_BIT_ROWS;
 constexpr int kBitOwnWords = 62;                      // owned words per tile row
 constexpr int kBitStageBatch = 4;                     // words staged per thread per batch
 
