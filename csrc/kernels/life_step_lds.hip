@@ -326,8 +326,14 @@ __global__ __launch_bounds__(512) void life_lds_multi_kernel(const uint8_t* __re
 // 1.48x); measured +1 % at 8192^2, +12 % at 32768^2, 192 rows (three per CU)
 // slower (profiles/r03/lds_packed_rows_160.jsonl).
 constexpr int kBitRows = GOL_LDS_BIT_ROWS;
+#ifndef GOL_LDS_BIT_WAVES
+#define GOL_LDS_BIT_WAVES 8
+#endif
+constexpr int kBitWaves = GOL_LDS_BIT_WAVES;           // waves per workgroup
+constexpr int kBitThreads = 64 * kBitWaves;
 constexpr int kBitOwnWords = 62;                      // owned words per tile row
-constexpr int kBitStageBatch = 4;                     // words staged per thread per batch
+// words staged per thread per batch
+constexpr int kBitStageBatch = (kBitRows * 64 / kBitThreads) % 4 == 0 ? 4 : (kBitRows * 64 / kBitThreads) % 2 == 0 ? 2 : 1;
 
 // ADD: the adder window (life_block_impl.hpp kXlaneAdd: no DPP / v_alignbit
 // in the level body, the stored frame drifts one cell right per generation;
@@ -335,7 +341,7 @@ constexpr int kBitStageBatch = 4;                     // words staged per thread
 // generation on the left, so the tile keeps ceil(2T / 32) halo words on the
 // left and none on the right.
 template <int T, bool ADD>
-__global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(kBitThreads) void life_lds_bits_kernel(const uint8_t* __restrict__ in,
                                                             uint8_t* __restrict__ out, int64_t pitch,
                                                             int64_t row_lo, int64_t row_hi, int64_t own_c0,
                                                             int64_t own_c1, uint32_t* changed,
@@ -352,15 +358,16 @@ __global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __res
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  // Stage: word idx = tid + 512 k (row idx / 64, word idx % 64), 32 bytes each.
-  constexpr int kWords = kBitRows * 64 / 512;
+  // Stage: word idx = tid + kBitThreads k (row idx / 64, word idx % 64), 32 bytes each.
+  static_assert(kBitRows * 64 % kBitThreads == 0, "whole staging passes");
+  constexpr int kWords = kBitRows * 64 / kBitThreads;
 #pragma unroll
   for (int k0 = 0; k0 < kWords; k0 += kBitStageBatch) {
     uint4 v[kBitStageBatch][2];
     bool ok[kBitStageBatch];
 #pragma unroll
     for (int kk = 0; kk < kBitStageBatch; ++kk) {
-      const int idx = tid + 512 * (k0 + kk);
+      const int idx = tid + kBitThreads * (k0 + kk);
       const int lr = idx >> 6, wl = idx & 63;
       const int64_t gr = r0 - T + lr;
       const int64_t gc = c0 + 32 * int64_t(wl);
@@ -375,7 +382,7 @@ __global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __res
     }
 #pragma unroll
     for (int kk = 0; kk < kBitStageBatch; ++kk)
-      bits[tid + 512 * (k0 + kk)] = ok[kk] ? IO::pack(v[kk][0], v[kk][1]) : 0u;
+      bits[tid + kBitThreads * (k0 + kk)] = ok[kk] ? IO::pack(v[kk][0], v[kk][1]) : 0u;
   }
   __syncthreads();
 
@@ -412,7 +419,7 @@ __global__ __launch_bounds__(512) void life_lds_bits_kernel(const uint8_t* __res
 #pragma unroll 1
   for (int g = 1; g <= T; ++g) {
     const int n = kBitRows - 2 * g;
-    const int lo = g + (n * w) / 8, hi = g + (n * (w + 1)) / 8;
+    const int lo = g + (n * w) / kBitWaves, hi = g + (n * (w + 1)) / kBitWaves;
     const uint32_t up = bits[(lo - 1) * 64 + lane];
     const uint32_t dn = bits[hi * 64 + lane];
     __syncthreads();
@@ -478,7 +485,7 @@ int launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream) {
                                                                        : life_lds_bits_kernel<32, true>)
                : (a.T == 8 ? life_lds_bits_kernel<8, false> : a.T == 16 ? life_lds_bits_kernel<16, false>
                                                                         : life_lds_bits_kernel<32, false>);
-  hipLaunchKernelGGL(k, grid, dim3(512), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
+  hipLaunchKernelGGL(k, grid, dim3(kBitThreads), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
                      g.pitch, a.row_lo, a.row_hi, g.cell0(), g.cell0() + g.W, changed, gen_dev, wrap_w, wrap_h,
                      g.row0(), c_first, c_end);
   return add ? a.T : 0;
