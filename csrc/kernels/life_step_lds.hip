@@ -346,15 +346,32 @@ __global__ __launch_bounds__(kBitThreads) void life_lds_bits_kernel(const uint8_
                                                             int64_t row_lo, int64_t row_hi, int64_t own_c0,
                                                             int64_t own_c1, uint32_t* changed,
                                                             const int64_t* gen_dev, int64_t wrap_w, int64_t wrap_h,
-                                                            int64_t row0, int64_t c_first, int64_t c_end) {
+                                                            int64_t row0, int64_t c_first, int64_t c_end,
+                                                            int ny, int xcd_order) {
   static_assert(T >= 1 && T <= 32, "at most 32 generations of the light cone per launch");
   constexpr int kTH = kBitRows - 2 * T;
+  // Tile of this workgroup.  Workgroups go round-robin to the 8 XCDs (block
+  // b to XCD b % 8), so with xcd_order (GOL_LDS_XCD=1) each XCD takes a contiguous run of
+  // tiles in column-major order: vertically adjacent tiles, whose staged
+  // rows overlap by 2T, read them through the same L2.  Otherwise row-major.
+  const int nblk = int(gridDim.x), b = int(blockIdx.x);
+  int bx, by;
+  if (xcd_order) {
+    const int q = nblk / 8, r = nblk % 8, xcd = b % 8;
+    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+    bx = L / ny;
+    by = L % ny;
+  } else {
+    const int nx = nblk / ny;
+    bx = b % nx;
+    by = b / nx;
+  }
   constexpr int kHL = ADD ? (2 * T + 31) / 32 : 1, kHR = ADD ? 0 : 1;  // halo words left / right
   constexpr int kOwn = 64 - kHL - kHR;                                   // owned words per tile row
   using IO = lb::U8IO<1, kXlaneDpp>;
   __shared__ uint32_t bits[kBitRows * 64];
-  const int64_t r0 = row_lo + int64_t(blockIdx.y) * kTH;                          // first output row
-  const int64_t c0 = c_first - 32 * kHL + int64_t(blockIdx.x) * (32 * kOwn);    // first staged cell
+  const int64_t r0 = row_lo + int64_t(by) * kTH;                          // first output row
+  const int64_t c0 = c_first - 32 * kHL + int64_t(bx) * (32 * kOwn);    // first staged cell
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -458,7 +475,7 @@ __global__ __launch_bounds__(kBitThreads) void life_lds_bits_kernel(const uint8_
 
 int lds_multi_tile_rows(int T) { return kMultiRows - 2 * T; }
 
-int launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream) {
+int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, hipStream_t stream) {
   const TileGeom& g = a.g;
   GOL_REQUIRE(g.layout == Layout::U8, "life_lds_bits: byte layout only");
   GOL_REQUIRE(a.T == 8 || a.T == 16 || a.T == 32, "life_lds_bits: T = 8, 16 or 32");
@@ -480,14 +497,16 @@ int launch_life_lds_bits(const BlockArgs& a, bool wrap, hipStream_t stream) {
   const int64_t c_end = wrap_w ? g.cell0() + g.W : g.Wc();
   const int th = kBitRows - 2 * a.T;
   const int own_words = add ? 64 - (2 * a.T + 31) / 32 : 62;
-  const dim3 grid(unsigned(ceil_div(c_end - c_first, int64_t(32 * own_words))), unsigned(ceil_div(rows, int64_t(th))));
+  const int64_t nx = ceil_div(c_end - c_first, int64_t(32 * own_words)), ny = ceil_div(rows, int64_t(th));
+  GOL_REQUIRE(nx * ny < (int64_t(1) << 31), "life_lds_bits: grid too large");
+  const dim3 grid(unsigned(nx * ny));
   auto k = add ? (a.T == 8 ? life_lds_bits_kernel<8, true> : a.T == 16 ? life_lds_bits_kernel<16, true>
                                                                        : life_lds_bits_kernel<32, true>)
                : (a.T == 8 ? life_lds_bits_kernel<8, false> : a.T == 16 ? life_lds_bits_kernel<16, false>
                                                                         : life_lds_bits_kernel<32, false>);
   hipLaunchKernelGGL(k, grid, dim3(kBitThreads), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
                      g.pitch, a.row_lo, a.row_hi, g.cell0(), g.cell0() + g.W, changed, gen_dev, wrap_w, wrap_h,
-                     g.row0(), c_first, c_end);
+                     g.row0(), c_first, c_end, int(ny), xcd_order ? 1 : 0);
   return add ? a.T : 0;
 }
 
