@@ -111,7 +111,7 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
       if (a.T == 1)
         launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
       else if (pack)
-        drift = launch_life_lds_bits(b, tune.wrap, tune.lds_xcd, stream);
+        drift = launch_life_lds_bits(b, tune.wrap, tune.lds_xcd, tune.lds_waves, tune.cus, stream);
       else
         launch_life_lds_multi(b, tune.wrap, stream);
       b.row_lo += a.dual_offset;

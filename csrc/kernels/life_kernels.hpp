@@ -140,6 +140,7 @@ struct LifeTuning {
   int lds_T = 8;            // generations per launch of the LDS-tiled byte kernel (1, 2, 4, 8; 16, 32 packed)
   bool lds_pack = true;     // LDS-tiled byte kernel evaluates on bit words packed in LDS (T >= 8)
   bool lds_xcd = false;     // packed LDS tiles: XCD-aware workgroup order (column-major runs per XCD)
+  int lds_waves = 0;        // packed LDS tiles: waves per workgroup (8, 16; 0 = by grid size)
   int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
   int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
@@ -251,7 +252,7 @@ void launch_life_lds_multi(const BlockArgs& a, bool wrap, hipStream_t stream);
 // launch, bit-sliced rule; life_step_lds.hip life_lds_bits_kernel).  Returns
 // the drift of the stored frame (T with the adder window, which it runs
 // where BlockArgs::allow_drift and the tile wraps its columns; else 0).
-int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, hipStream_t stream);
+int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, int waves, int cus, hipStream_t stream);
 
 // Tile utility kernels (tile_ops.hip).
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s);

@@ -27,6 +27,7 @@
 // blocking kernel (life_block_impl.hpp) is the fast path.  This one is kept
 // as the single-step u8 baseline ("8192^2 LDS-tiled u8 kernel")
 // and selected with GOL_U8_KERNEL=lds (forces T = 1).
+#include <type_traits>
 #include <hip/hip_runtime.h>
 
 #include "gol/common.hpp"
@@ -326,22 +327,20 @@ __global__ __launch_bounds__(512) void life_lds_multi_kernel(const uint8_t* __re
 // 1.48x); measured +1 % at 8192^2, +12 % at 32768^2, 192 rows (three per CU)
 // slower (profiles/r03/lds_packed_rows_160.jsonl).
 constexpr int kBitRows = GOL_LDS_BIT_ROWS;
-#ifndef GOL_LDS_BIT_WAVES
-#define GOL_LDS_BIT_WAVES 8
-#endif
-constexpr int kBitWaves = GOL_LDS_BIT_WAVES;           // waves per workgroup
-constexpr int kBitThreads = 64 * kBitWaves;
-constexpr int kBitOwnWords = 62;                      // owned words per tile row
-// words staged per thread per batch
-constexpr int kBitStageBatch = (kBitRows * 64 / kBitThreads) % 4 == 0 ? 4 : (kBitRows * 64 / kBitThreads) % 2 == 0 ? 2 : 1;
+// Words staged per thread per batch (NW waves per workgroup).
+template <int NW>
+constexpr int bit_stage_batch() {
+  constexpr int words = kBitRows * 64 / (64 * NW);
+  return words % 4 == 0 ? 4 : words % 2 == 0 ? 2 : 1;
+}
 
 // ADD: the adder window (life_block_impl.hpp kXlaneAdd: no DPP / v_alignbit
 // in the level body, the stored frame drifts one cell right per generation;
 // whole-width torus tiles only).  Its light cone is one-sided, 2 cells per
 // generation on the left, so the tile keeps ceil(2T / 32) halo words on the
 // left and none on the right.
-template <int T, bool ADD>
-__global__ __launch_bounds__(kBitThreads) void life_lds_bits_kernel(const uint8_t* __restrict__ in,
+template <int T, bool ADD, int NW>
+__global__ __launch_bounds__(64 * NW) void life_lds_bits_kernel(const uint8_t* __restrict__ in,
                                                             uint8_t* __restrict__ out, int64_t pitch,
                                                             int64_t row_lo, int64_t row_hi, int64_t own_c0,
                                                             int64_t own_c1, uint32_t* changed,
@@ -375,16 +374,17 @@ __global__ __launch_bounds__(kBitThreads) void life_lds_bits_kernel(const uint8_
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  // Stage: word idx = tid + kBitThreads k (row idx / 64, word idx % 64), 32 bytes each.
-  static_assert(kBitRows * 64 % kBitThreads == 0, "whole staging passes");
-  constexpr int kWords = kBitRows * 64 / kBitThreads;
+  // Stage: word idx = tid + kThreads k (row idx / 64, word idx % 64), 32 bytes each.
+  constexpr int kThreads = 64 * NW, kBitStageBatch = bit_stage_batch<NW>();
+  static_assert(kBitRows * 64 % kThreads == 0, "whole staging passes");
+  constexpr int kWords = kBitRows * 64 / kThreads;
 #pragma unroll
   for (int k0 = 0; k0 < kWords; k0 += kBitStageBatch) {
     uint4 v[kBitStageBatch][2];
     bool ok[kBitStageBatch];
 #pragma unroll
     for (int kk = 0; kk < kBitStageBatch; ++kk) {
-      const int idx = tid + kBitThreads * (k0 + kk);
+      const int idx = tid + kThreads * (k0 + kk);
       const int lr = idx >> 6, wl = idx & 63;
       const int64_t gr = r0 - T + lr;
       const int64_t gc = c0 + 32 * int64_t(wl);
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(kBitThreads) void life_lds_bits_kernel(const uint8_
     }
 #pragma unroll
     for (int kk = 0; kk < kBitStageBatch; ++kk)
-      bits[tid + kBitThreads * (k0 + kk)] = ok[kk] ? IO::pack(v[kk][0], v[kk][1]) : 0u;
+      bits[tid + kThreads * (k0 + kk)] = ok[kk] ? IO::pack(v[kk][0], v[kk][1]) : 0u;
   }
   __syncthreads();
 
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(kBitThreads) void life_lds_bits_kernel(const uint8_
 #pragma unroll 1
   for (int g = 1; g <= T; ++g) {
     const int n = kBitRows - 2 * g;
-    const int lo = g + (n * w) / kBitWaves, hi = g + (n * (w + 1)) / kBitWaves;
+    const int lo = g + (n * w) / NW, hi = g + (n * (w + 1)) / NW;
     const uint32_t up = bits[(lo - 1) * 64 + lane];
     const uint32_t dn = bits[hi * 64 + lane];
     __syncthreads();
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(kBitThreads) void life_lds_bits_kernel(const uint8_
 
 int lds_multi_tile_rows(int T) { return kMultiRows - 2 * T; }
 
-int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, hipStream_t stream) {
+int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, int waves, int cus, hipStream_t stream) {
   const TileGeom& g = a.g;
   GOL_REQUIRE(g.layout == Layout::U8, "life_lds_bits: byte layout only");
   GOL_REQUIRE(a.T == 8 || a.T == 16 || a.T == 32, "life_lds_bits: T = 8, 16 or 32");
@@ -500,11 +500,21 @@ int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, hipStrea
   const int64_t nx = ceil_div(c_end - c_first, int64_t(32 * own_words)), ny = ceil_div(rows, int64_t(th));
   GOL_REQUIRE(nx * ny < (int64_t(1) << 31), "life_lds_bits: grid too large");
   const dim3 grid(unsigned(nx * ny));
-  auto k = add ? (a.T == 8 ? life_lds_bits_kernel<8, true> : a.T == 16 ? life_lds_bits_kernel<16, true>
-                                                                       : life_lds_bits_kernel<32, true>)
-               : (a.T == 8 ? life_lds_bits_kernel<8, false> : a.T == 16 ? life_lds_bits_kernel<16, false>
-                                                                        : life_lds_bits_kernel<32, false>);
-  hipLaunchKernelGGL(k, grid, dim3(kBitThreads), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
+  // 16 waves per workgroup when the grid fits the GPU in one round at 8
+  // (small grids: 8192^2 +6 %), 8 otherwise (32768^2: 16 waves -19 %;
+  // profiles/r03/lds_packed_waves_xcd.jsonl, lds_packed_waves_auto.jsonl).
+  const int nw = waves == 8 || waves == 16 ? waves : (nx * ny <= int64_t(4) * cus ? 16 : 8);
+  using K = void (*)(const uint8_t*, uint8_t*, int64_t, int64_t, int64_t, int64_t, int64_t, uint32_t*,
+                     const int64_t*, int64_t, int64_t, int64_t, int64_t, int64_t, int, int);
+  const auto pick = [&](auto nw_c) -> K {
+    constexpr int NW = decltype(nw_c)::value;
+    return add ? (a.T == 8 ? life_lds_bits_kernel<8, true, NW> : a.T == 16 ? life_lds_bits_kernel<16, true, NW>
+                                                                           : life_lds_bits_kernel<32, true, NW>)
+               : (a.T == 8 ? life_lds_bits_kernel<8, false, NW> : a.T == 16 ? life_lds_bits_kernel<16, false, NW>
+                                                                            : life_lds_bits_kernel<32, false, NW>);
+  };
+  const K k = nw == 16 ? pick(std::integral_constant<int, 16>{}) : pick(std::integral_constant<int, 8>{});
+  hipLaunchKernelGGL(k, grid, dim3(64 * nw), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),
                      g.pitch, a.row_lo, a.row_hi, g.cell0(), g.cell0() + g.W, changed, gen_dev, wrap_w, wrap_h,
                      g.row0(), c_first, c_end, int(ny), xcd_order ? 1 : 0);
   return add ? a.T : 0;

@@ -84,6 +84,8 @@ class HipBackend final : public Backend {
     tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
     tune_.lds_pack = env_int("GOL_LDS_PACK", 1) != 0;
     tune_.lds_xcd = env_int("GOL_LDS_XCD", 0) != 0;
+    tune_.lds_waves = env_int("GOL_LDS_WAVES", 0);
+    GOL_REQUIRE(tune_.lds_waves == 0 || tune_.lds_waves == 8 || tune_.lds_waves == 16, "GOL_LDS_WAVES: 0, 8 or 16");
     lds_add_ = env_int("GOL_LDS_ADD", 0) != 0;  // packed LDS tile: adder window (drifting frame)
     // 8192^2 per generation: bytes T = 1 26.6, 2 24.9, 4 20.4, 8 17.9 us; packed T = 8 6.5, 16 4.9, 32 4.7
     tune_.lds_T = env_int("GOL_LDS_T", tune_.lds_pack ? 32 : 8);

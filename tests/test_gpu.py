@@ -416,18 +416,21 @@ def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H, lds_rows):
 
 @pytest.mark.parametrize("W,H", [(1, 1), (5, 3), (100, 70), (1023, 65), (1025, 200), (3000, 129), (32, 40),
                                  (2048, 333), (3072, 97), (8192, 130), (992, 56), (1984, 113)])
-@pytest.mark.parametrize("lds_T,pack", [(2, 0), (4, 0), (8, 0), (8, 1), (16, 1), (32, 1), (32, 2)])
+@pytest.mark.parametrize("lds_T,pack", [(2, 0), (4, 0), (8, 0), (8, 1), (16, 1), (32, 1), (32, 2),
+                                         (8, 3), (32, 3)])
 def test_u8_lds_multi_generation_kernel_vs_torch(gpu, monkeypatch, W, H, lds_T, pack):
     """The LDS-tiled byte kernel with T generations per launch: on the bytes
     (992-cell tiles with a 16-byte halo chunk per side) or packed to bit words
     in LDS (1984-cell tiles with a halo word per side); torus-wrap tiles
     (width % 32 == 0) and halo-column tiles, 45 generations (partial blocks
-    at the end).  pack == 2: packed, with the XCD-aware tile order
-    (GOL_LDS_XCD=1)."""
+    at the end).  Packed tiles run 16-wave workgroups on these small grids;
+    pack == 2: with the XCD-aware tile order (GOL_LDS_XCD=1), pack == 3:
+    8-wave workgroups (the large-grid choice)."""
     monkeypatch.setenv("GOL_U8_KERNEL", "lds")
     monkeypatch.setenv("GOL_LDS_T", str(lds_T))
     monkeypatch.setenv("GOL_LDS_PACK", str(min(pack, 1)))
     monkeypatch.setenv("GOL_LDS_XCD", str(int(pack == 2)))
+    monkeypatch.setenv("GOL_LDS_WAVES", "8" if pack == 3 else "0")
     g = random_grid(W, H, W * 3 + H + lds_T)
     want = life_step_torch(g, 45, device="cuda")
     assert (life_step(g, 45, engine="hip", layout="u8") == want).all()
