@@ -58,6 +58,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "cell-updates/sec (whole node), 32768^2 x 1000 gens; scaling at 1/2/4/8 GPUs"
+HEADLINE = (32768, 32768, 1000)  # BASELINE.json's grid and GEN_LIMIT
 # no published numbers; best reference run measured there is
 # game_mpi_collective/async.c, 4 ranks, 2048^2: ~8.9e8 cell-updates/s.
 BASELINE_VALUE = 8.9e8
@@ -108,6 +109,39 @@ def _launch_ranks(ngpus: int, argv: list[str], out_fd: int) -> int:
         log(f"bench.py: the rank processes printed {lines} result lines, expected 1")
         return 1
     return rc
+
+
+def metric_label(S: int, Hg: int, gps: int) -> tuple[str, bool, int | None]:
+    """(metric, headline, config_id) of a run.  Only the BASELINE.json grid and
+    generation count carry the headline metric string; any other grid names
+    itself.  config_id is the BASELINE.json config the grid belongs to (1-5:
+    256^2 CPU plumbing, 8192^2 byte tile, 32768^2 node, 65536^2 bits,
+    1048576^2 bytes), None for an experiment's grid."""
+    headline = (S, Hg, gps) == HEADLINE
+    if headline:
+        metric = METRIC
+    else:
+        grid = f"{S}^2" if S == Hg else f"{S}x{Hg}"
+        metric = f"cell-updates/sec (whole node), {grid} x {gps} gens"
+    ids = {256: 1, 8192: 2, 32768: 3, 65536: 4, 1048576: 5}
+    return metric, headline, (ids.get(S) if S == Hg else None)
+
+
+def check_ranks(world: int, shared: bool, comm_count: int, infos: list[dict]) -> str | None:
+    """What RCCL saw must be what the bench reports (the reference's
+    MPI_Comm_size, src/game_mpi.c:159): the communicator holds `world` ranks,
+    every rank reported in, and without --share-gpus no two ranks ran on the
+    same physical GPU (PCI bus id).  Returns the reason to refuse, or None."""
+    if comm_count != world:
+        return f"the halo communicator has {comm_count} ranks, but {world} rank processes were launched"
+    if len(infos) != world or sorted(i["rank"] for i in infos) != list(range(world)):
+        return f"{len(infos)} of {world} ranks reported their device"
+    if not shared:
+        buses = [i["pci_bus_id"] for i in infos if i.get("pci_bus_id")]
+        dup = sorted({b for b in buses if buses.count(b) > 1})
+        if dup:
+            return f"ranks share GPU(s) {dup} without --share-gpus: n_gpus would overstate the GPUs used"
+    return None
 
 
 def parse_args(argv=None):
@@ -201,13 +235,33 @@ def main() -> int:
     if world > 1:
         from gol_amd.parallel.dist import init_process_group, make_transport  # noqa: PLC0415
 
-        dist = init_process_group("nccl" if on_gpu and not shared else "gloo")
+        # torch.distributed over RCCL on the GPU, shared-device rehearsals
+        # included: every rank has its own NCCL_HOSTID, so torch's own RCCL
+        # communicator (gather_grid, the MAX of the rank timings) runs the
+        # same code path as on the node.
+        dist = init_process_group("nccl" if on_gpu else "gloo")
         transport = make_transport(a.comm, backend, local)
     elif a.rehearse_rccl and on_gpu:
         C = native()
         transport = C.rccl_transport(C.rccl_unique_id(), 0, 1, local)
     else:
         transport = native().self_transport()
+
+    # Which communicator size and which physical GPU every rank saw.
+    comm_count = transport.comm_count()
+    me = {"rank": rank, "local_rank": local, "host": socket.gethostname(),
+          "device": (int(backend.device()) if on_gpu else "cpu"),
+          "pci_bus_id": (native().hip_pci_bus_id(int(backend.device())) if on_gpu else None),
+          "comm_device": transport.comm_device()}
+    if dist is not None:
+        infos = [None] * world
+        dist.all_gather_object(infos, me)
+    else:
+        infos = [me]
+    why = check_ranks(world, shared, comm_count, infos)
+    if why:
+        log(f"bench.py: {why}; refusing to report a number")
+        return 2
 
     S = a.size
     Hg = a.height or S
@@ -305,9 +359,10 @@ def main() -> int:
             dist.barrier()
 
     desc = sim.describe()
+    metric, headline, config_id = metric_label(S, Hg, gps)
     if rank == 0:
         rec = {
-            "metric": METRIC,
+            "metric": metric,
             "value": value,
             "unit": "cell-updates/s",
             "n_gpus": world,
@@ -321,6 +376,10 @@ def main() -> int:
             "dtype": "u1 bit-packed cells (exact boolean B3/S23; reference stores u8 chars)"
                      if a.layout == "bits" else "u8 byte-per-cell (exact)",
             "data": "synthetic: on-device counter-based RNG random grid, density 0.5 (generate.sh distribution)",
+            "headline": headline,
+            "config_id": config_id,
+            "rccl_nranks": comm_count,
+            "devices": infos,
             "config": {
                 "model": f"Game of Life B3/S23 torus {S}x{Hg}",
                 "global_batch": 1,

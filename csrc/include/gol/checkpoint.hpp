@@ -17,7 +17,7 @@
 // Crash safety: a new checkpoint never touches the files of the committed
 // one.  Its grid goes to a fresh file name, is fsync'ed, and only then is
 // meta.json replaced (write + fsync + rename + directory fsync); the old grid
-// file is deleted after that.  A crash at any point leaves either the old
+// file is deleted after that, with any orphan of an interrupted checkpoint.  A crash at any point leaves either the old
 // checkpoint or the new one, complete.  (Format v1 checkpoints without a
 // "grid" key use grid.txt.)
 #pragma once
@@ -46,6 +46,11 @@ inline int sim_phase_at(int64_t gen, int64_t start_gen, int phase, int freq) {
   return int(((gen - start_gen + phase) % freq + freq) % freq);
 }
 
+// Whether `name` may be a checkpoint's grid file: the plain basename
+// grid-<digits>[b].txt or the legacy grid.txt - never a path, "..", or
+// meta.json (a tampered meta.json must not make --resume read, or a commit
+// delete, anything else).  Mirrored by utils/checkpoint.py:grid_name_ok.
+bool checkpoint_grid_name_ok(const std::string& name);
 // Grid file of the committed checkpoint in `dir` (reads meta.json).
 std::string checkpoint_grid_path(const std::string& dir);
 // Creates the directory (if needed) and a sized grid file for generation
@@ -55,7 +60,8 @@ std::string checkpoint_grid_path(const std::string& dir);
 std::string checkpoint_begin(const std::string& dir, int64_t W, int64_t H, int64_t generation);
 // After every rank's tile is on disk: fsyncs the grid file `grid_path`
 // (from checkpoint_begin), publishes meta.json for it atomically, then
-// removes the previous checkpoint's grid file.
+// removes the previous checkpoint's grid file and any grid file an
+// interrupted checkpoint left behind.
 void checkpoint_commit(const std::string& dir, const std::string& grid_path, CheckpointMeta m);
 // Reads meta.json (throws on a missing file, a different format or missing keys).
 CheckpointMeta checkpoint_load(const std::string& dir);

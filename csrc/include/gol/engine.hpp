@@ -228,6 +228,7 @@ class Engine {
   void epoch_overlapped(int64_t d);
   void run_epoch(int64_t d);
   void release_graphs();
+  int graph_key() const { return via_bits_ ? 2 * cur_ + bpar_ : cur_; }
   // Overlap auto trial (EngineConfig::overlap == -1): picks the schedule of
   // the next full epoch, records its start, and decides once enough epochs
   // of both schedules have been timed (at the same epoch on every rank).
@@ -264,9 +265,13 @@ class Engine {
   bool use_graphs_ = false, capturing_ = false;
   int64_t* gen_dev_ = nullptr;        // device: (epoch start - flags_base_) for graph replays
   int64_t epoch_start_ = 0;
-  void* graph_[2] = {nullptr, nullptr};  // by buffer parity at epoch start
-  int graph_flip_[2] = {0, 0};
-  int64_t graph_kernels_[2] = {0, 0};
+  // Captured epochs, keyed by graph_key(): the parity of the buffer pair the
+  // epochs alternate over and, for the byte layout on bit words, the byte
+  // buffer the bit scratch lives in (bit_scratch depends on cur_, which
+  // normalize() flips between runs).
+  void* graph_[4] = {nullptr, nullptr, nullptr, nullptr};
+  int graph_flip_[4] = {0, 0, 0, 0};
+  int64_t graph_kernels_[4] = {0, 0, 0, 0};
   uint32_t* graph_flags_ = nullptr;   // flags buffer the graphs were captured with
   int64_t graph_runs_ = 0;
   int64_t halo_bytes_ = 0;
@@ -285,7 +290,7 @@ class Engine {
   int bpar_ = 0;             // bit_scratch(bpar_) holds the current generation during a run
   bool poll_side_ = false;   // termination polls reduce on the comm stream (Transport::side_reduce)
   int64_t drift_ = 0;
-  int64_t graph_drift_[2] = {0, 0};
+  int64_t graph_drift_[4] = {0, 0, 0, 0};
   // Overlap auto trial.
   bool auto_overlap_ = false;       // trial still running
   bool auto_decided_ = false;

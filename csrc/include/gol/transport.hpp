@@ -25,6 +25,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 namespace gol {
@@ -61,6 +62,12 @@ class Transport {
   // enqueued on another stream than exchange() and run concurrently with it
   // (the engine then reduces termination flags beside the compute stream).
   virtual bool side_reduce() const { return false; }
+  // Ranks the underlying communicator reports (RCCL: ncclCommCount; the
+  // reference's MPI_Comm_size, src/game_mpi.c:159) and the device it is
+  // bound to (ncclCommCuDevice; -1 for host transports).  bench.py checks
+  // them against WORLD_SIZE and the rank's own device.
+  virtual int comm_count() const { return size(); }
+  virtual int comm_device() const { return -1; }
 };
 
 // Single rank: nothing to exchange with.
@@ -131,5 +138,7 @@ std::unique_ptr<Transport> make_rccl_transport(const std::vector<uint8_t>& uniqu
                                                int nranks, int device);
 std::vector<uint8_t> rccl_unique_id();
 bool rccl_available();
+// PCI bus id ("0000:05:00.0") of a HIP device: which physical GPU a rank ran on.
+std::string hip_pci_bus_id(int device);
 
 }  // namespace gol

@@ -133,11 +133,14 @@ PYBIND11_MODULE(_gol, m) {
   m.def("hip_backend", [](int device) { return std::shared_ptr<Backend>(make_hip_backend(device)); },
         py::arg("device") = 0);
   m.def("hip_available", &hip_available);
+  m.def("hip_pci_bus_id", &hip_pci_bus_id);
 
   py::class_<Transport, std::shared_ptr<Transport>>(m, "Transport")
       .def("rank", &Transport::rank)
       .def("size", &Transport::size)
       .def("name", &Transport::name)
+      .def("comm_count", &Transport::comm_count)
+      .def("comm_device", &Transport::comm_device)
       .def("barrier", &Transport::barrier, py::call_guard<py::gil_scoped_release>())
       // Raw access for plumbing tests: ops = [(send, peer, address, bytes)],
       // addresses in the transport's address space (device memory for rccl).

@@ -1,5 +1,6 @@
 #include "gol/checkpoint.hpp"
 
+#include <dirent.h>
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -10,6 +11,7 @@
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <vector>
 
 #include "gol/common.hpp"
 #include "gol/io.hpp"
@@ -59,6 +61,21 @@ int64_t need_int(const std::string& js, const std::string& key, const std::strin
 }
 
 }  // namespace
+
+bool checkpoint_grid_name_ok(const std::string& name) {
+  if (name == "grid.txt") return true;  // legacy single-file checkpoints
+  // grid-<digits>[b].txt: a plain basename, never meta.json or a path.
+  const std::string pre = "grid-", suf = ".txt";
+  if (name.size() <= pre.size() + suf.size() || name.compare(0, pre.size(), pre) != 0 ||
+      name.compare(name.size() - suf.size(), suf.size(), suf) != 0)
+    return false;
+  std::string mid = name.substr(pre.size(), name.size() - pre.size() - suf.size());
+  if (!mid.empty() && mid.back() == 'b') mid.pop_back();
+  if (mid.empty()) return false;
+  for (char c : mid)
+    if (c < '0' || c > '9') return false;
+  return true;
+}
 
 std::string checkpoint_grid_path(const std::string& dir) { return dir + "/" + checkpoint_load(dir).grid; }
 
@@ -115,8 +132,18 @@ void checkpoint_commit(const std::string& dir, const std::string& grid_path, Che
   if (std::rename(tmp.c_str(), fin.c_str()) != 0)
     fail("cannot publish checkpoint metadata '" + fin + "': " + std::strerror(errno));
   fsync_path(dir, true);
-  // The committed checkpoint no longer needs the previous grid.
+  // The committed checkpoint no longer needs the previous grid, nor any grid
+  // an interrupted checkpoint left behind (crash between begin and commit).
   if (!previous.empty() && previous != m.grid) std::remove((dir + "/" + previous).c_str());
+  if (DIR* d = ::opendir(dir.c_str())) {
+    std::vector<std::string> orphans;
+    while (const dirent* e = ::readdir(d)) {
+      const std::string n = e->d_name;
+      if (n != m.grid && n.compare(0, 5, "grid-") == 0 && checkpoint_grid_name_ok(n)) orphans.push_back(n);
+    }
+    ::closedir(d);
+    for (const auto& n : orphans) std::remove((dir + "/" + n).c_str());
+  }
 }
 
 CheckpointMeta checkpoint_load(const std::string& dir) {
@@ -142,8 +169,8 @@ CheckpointMeta checkpoint_load(const std::string& dir) {
   if (!lay.empty()) m.layout = lay;
   const std::string grid = json_field(js, "grid");
   if (!grid.empty()) {
-    GOL_REQUIRE(grid.find('/') == std::string::npos && grid != "." && grid != "..",
-                "checkpoint '" + dir + "': bad grid file name '" + grid + "'");
+    GOL_REQUIRE(checkpoint_grid_name_ok(grid), "checkpoint '" + dir + "': bad grid file name '" + grid +
+                                                   "' (expected grid-<generation>[b].txt)");
     m.grid = grid;
   }
   GOL_REQUIRE(m.W > 0 && m.H > 0 && m.sim_freq > 0 && m.generation >= 0,

@@ -779,9 +779,10 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     if (use_graphs_ && d == D_) {
       // Full epochs replay a captured graph; the only per-epoch input is the
       // device generation offset, advanced by the graph itself.  Graphs are
-      // keyed by the parity of the buffer pair the epochs alternate over.
+      // keyed by the parity of the buffer pair the epochs alternate over and
+      // by the addresses baked into them (graph_key).
       int& cur = via_bits_ ? bpar_ : cur_;
-      const int par = cur;
+      const int par = graph_key();
       if (!graph_[par]) {
         const int64_t k0 = launches_;
         const int64_t dr0 = drift_;
@@ -792,7 +793,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
         be_->i64_async(gen_dev_, D_, /*add=*/true);
         graph_[par] = be_->capture_end();
         capturing_ = false;
-        graph_flip_[par] = cur ^ par;
+        graph_flip_[par] = cur ^ (par & 1);
         graph_kernels_[par] = launches_ - k0;
         graph_drift_[par] = ((drift_ - dr0) % cfg_.W + cfg_.W) % cfg_.W;
         be_->graph_launch(graph_[par]);  // capture only recorded it

@@ -133,6 +133,16 @@ class RcclTransport final : public Transport {
                              static_cast<hipStream_t>(stream)));
   }
   bool side_reduce() const override { return flags_comm_ != nullptr; }
+  int comm_count() const override {
+    int n = 0;
+    NCCL_CHECK(ncclCommCount(comm_, &n));
+    return n;
+  }
+  int comm_device() const override {
+    int d = -1;
+    NCCL_CHECK(ncclCommCuDevice(comm_, &d));
+    return d;
+  }
   void barrier() override {
     DeviceScope on(dev_);
     NCCL_CHECK(ncclAllReduce(barrier_buf_, barrier_buf_, 1, ncclUint32, ncclMax, comm_, barrier_stream_));
@@ -171,6 +181,12 @@ std::vector<uint8_t> rccl_unique_id() {
 }
 
 bool rccl_available() { return true; }
+
+std::string hip_pci_bus_id(int device) {
+  char id[64] = {0};
+  HIP_CHECK(hipDeviceGetPCIBusId(id, int(sizeof(id)), device));
+  return id;
+}
 
 std::unique_ptr<Transport> make_rccl_transport(const std::vector<uint8_t>& uid, int rank, int nranks,
                                                int device) {

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import json
 import os
+import re
 from pathlib import Path
 from typing import Optional
 
@@ -28,12 +29,31 @@ from ..models.life import LifeConfig, RunReport, Simulation
 from .termination import reported_generations, sim_phase_at
 
 
+_GRID_NAME = re.compile(r"grid-[0-9]+b?\.txt")
+
+
+def grid_name_ok(name) -> bool:
+    """Whether ``name`` may be a checkpoint's grid file: the plain basename
+    ``grid-<digits>[b].txt`` or the legacy ``grid.txt`` - never a path, "..",
+    or meta.json, so a tampered meta.json cannot make a resume read, or a
+    commit delete, anything else (checkpoint.cpp:checkpoint_grid_name_ok)."""
+    return isinstance(name, str) and (name == "grid.txt" or _GRID_NAME.fullmatch(name) is not None)
+
+
+def _meta_grid(meta: dict, directory) -> str:
+    name = meta.get("grid", "grid.txt")
+    if not grid_name_ok(name):
+        raise ValueError(f"checkpoint '{directory}': bad grid file name {name!r} "
+                         "(expected grid-<generation>[b].txt)")
+    return name
+
+
 def committed_grid(directory) -> Optional[str]:
     """Grid file name of the committed checkpoint in ``directory`` (None: none)."""
     meta = Path(directory) / "meta.json"
     if not meta.exists():
         return None
-    return json.loads(meta.read_text()).get("grid", "grid.txt")
+    return _meta_grid(json.loads(meta.read_text()), directory)
 
 
 def _fsync(path: Path, directory: bool = False) -> None:
@@ -88,6 +108,10 @@ def save_checkpoint(sim: Simulation, directory: str, is_root: bool = True, barri
         _fsync(d, directory=True)
         if previous and previous != name and (d / previous).exists():
             (d / previous).unlink()
+        # Grids an interrupted checkpoint left behind (crash before commit).
+        for orphan in d.glob("grid-*.txt"):
+            if orphan.name != name and grid_name_ok(orphan.name):
+                orphan.unlink(missing_ok=True)
     if barrier:
         barrier()
     return d
@@ -102,7 +126,7 @@ def load_checkpoint(directory: str, **overrides) -> tuple[LifeConfig, Path]:
                      sim_phase=meta["sim_phase"])
     for k, v in overrides.items():
         setattr(cfg, k, v)
-    return cfg, d / meta.get("grid", "grid.txt")
+    return cfg, d / _meta_grid(meta, d)
 
 
 def run_with_checkpoints(sim: Simulation, every: int, directory: Optional[str], is_root: bool = True,

@@ -59,6 +59,47 @@ def test_bench_gpus_n_launches_n_ranks_itself(native, gpus):
     assert ph["generations"] == 100 and ph["compute_ms"] > 0 and ph["allreduce_ms"] >= 0
     if gpus > 1:
         assert ph["halo_ms"] > 0 and cfg["halo_bytes_per_step"] > 0
+    # What the communicator saw: every rank reported, on the CPU engine.
+    assert rec["rccl_nranks"] == gpus
+    assert sorted(d["rank"] for d in rec["devices"]) == list(range(gpus))
+    assert all(d["device"] == "cpu" for d in rec["devices"])
+    # 256^2 is BASELINE config 1's grid, not the headline metric.
+    assert rec["headline"] is False and rec["config_id"] == 1
+    assert rec["metric"] == "cell-updates/sec (whole node), 256^2 x 100 gens"
+
+
+def _bench_module():
+    import importlib.util  # noqa: PLC0415
+    spec = importlib.util.spec_from_file_location("gol_bench", REPO / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_bench_metric_label_names_the_grid():
+    b = _bench_module()
+    m, head, cid = b.metric_label(32768, 32768, 1000)
+    assert m == b.METRIC and head is True and cid == 3
+    m, head, cid = b.metric_label(8192, 8192, 1000)
+    assert "32768" not in m and "8192^2 x 1000 gens" in m and head is False and cid == 2
+    m, head, cid = b.metric_label(32768, 4096, 1000)
+    assert "32768x4096" in m and head is False and cid is None
+    assert b.metric_label(32768, 32768, 200)[1] is False
+    assert b.metric_label(65536, 65536, 1000)[2] == 4 and b.metric_label(1048576, 1048576, 1000)[2] == 5
+
+
+def test_bench_check_ranks_refuses_what_rccl_did_not_see():
+    """A fake communicator view: the refusal cases of bench.py's rank check
+    (rccl_nranks != WORLD_SIZE, a rank missing, two ranks on one physical GPU
+    without --share-gpus)."""
+    b = _bench_module()
+    infos = [{"rank": r, "pci_bus_id": f"0000:{r + 5:02x}:00.0"} for r in range(8)]
+    assert b.check_ranks(8, False, 8, infos) is None
+    assert "7 ranks" in b.check_ranks(8, False, 7, infos)
+    assert "7 of 8" in b.check_ranks(8, False, 8, infos[:7])
+    same = [dict(i, pci_bus_id="0000:05:00.0") for i in infos]
+    assert "share GPU" in b.check_ranks(8, False, 8, same)
+    assert b.check_ranks(8, True, 8, same) is None  # --share-gpus: a declared rehearsal
 
 
 def test_bench_refuses_a_launcher_with_another_world_size(native):
@@ -168,13 +209,16 @@ def test_python_cli_show_prints_the_vt100_view(native, tmp_path):
 
 
 def test_native_cli_metrics_carry_phases_and_comm(gol_bin, tmp_path):
-    """bin/gol --metrics-json: per-phase device times (implied phase timing),
-    the resolved in-process transport (auto -> thread for CPU ranks) and the
-    overlap mode."""
+    """bin/gol --metrics-json: per-phase device times (with --phase-timing
+    only, so the timed loop carries no events by default), the resolved
+    in-process transport (auto -> thread for CPU ranks) and the overlap mode."""
     m = tmp_path / "m.json"
-    r = subprocess.run([str(gol_bin), "256", "600", "--random", "3", "--engine", "cpu", "--ranks", "3",
-                        "--decomp", "1x3", "--gens", "500", "--tmax", "8", "--epoch", "32", "--output", "none",
-                        "--metrics-json", str(m)], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    args = [str(gol_bin), "256", "600", "--random", "3", "--engine", "cpu", "--ranks", "3", "--decomp", "1x3",
+            "--gens", "500", "--tmax", "8", "--epoch", "32", "--output", "none", "--metrics-json", str(m)]
+    r = subprocess.run(args, cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(m.read_text())["phase_timed"] is False
+    r = subprocess.run(args + ["--phase-timing"], cwd=tmp_path, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     rec = json.loads(m.read_text())
     assert rec["comm"] == "thread" and rec["ranks"] == 3

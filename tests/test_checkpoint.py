@@ -222,3 +222,51 @@ def test_checkpoint_same_generation_twice_uses_alternate_file(native, tmp_path):
     meta = json.loads((tmp_path / "ck" / "meta.json").read_text())
     assert meta["grid"] == "grid-5b.txt"
     assert sorted(p.name for p in (tmp_path / "ck").iterdir()) == ["grid-5b.txt", "meta.json"]
+
+
+@pytest.mark.parametrize("bad", ["../outside.txt", "/etc/hostname", "meta.json", "meta.json.tmp", "..", "grid-1.txt/x",
+                                 "grid-.txt", "grid-12c.txt"])
+def test_tampered_meta_grid_name_is_refused(gol_bin, native, tmp_path, bad):
+    """meta.json's grid name must be a plain grid-<gen>[b].txt basename on both
+    sides: a resume never reads, and a commit never deletes, anything else."""
+    g = random_grid(40, 30, 4)
+    sim = Simulation(LifeConfig(40, 30), engine="cpu")
+    sim.load(g)
+    sim.advance(5)
+    ck = tmp_path / "ck"
+    save_checkpoint(sim, str(ck))
+    meta = json.loads((ck / "meta.json").read_text())
+    meta["grid"] = bad
+    (ck / "meta.json").write_text(json.dumps(meta))
+    with pytest.raises(ValueError, match="bad grid file name"):
+        load_checkpoint(str(ck))
+    with pytest.raises(ValueError, match="bad grid file name"):
+        save_checkpoint(sim, str(ck))
+    assert (ck / "meta.json").exists()
+    r = subprocess.run([str(gol_bin), "--resume", str(ck), "--engine", "cpu", "--output", "none"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "bad grid file name" in r.stderr
+
+
+@pytest.mark.parametrize("writer", ["native", "python"])
+def test_commit_removes_orphans_of_interrupted_checkpoints(gol_bin, native, tmp_path, writer):
+    """Grid files of checkpoints that crashed before their commit (about 1 GiB
+    each at 32768^2) are removed by the next successful commit; files that do
+    not look like checkpoint grids are left alone."""
+    ck = tmp_path / "ck"
+    ck.mkdir()
+    for stray in ("grid-7.txt", "grid-12b.txt"):
+        (ck / stray).write_text("0\n")
+    (ck / "notes.txt").write_text("keep me")
+    W, H = 64, 32
+    if writer == "native":
+        _bin(gol_bin, [W, H, "--random", "3", "--engine", "cpu", "--gens", 60, "--no-similarity",
+                       "--checkpoint-every", 20, "--checkpoint-dir", ck, "--output", "none"], tmp_path)
+        want = "grid-40.txt"
+    else:
+        sim = Simulation(LifeConfig(W, H, check_similarity=False), engine="cpu")
+        sim.load(random_grid(W, H, 3))
+        sim.advance(20)
+        save_checkpoint(sim, str(ck))
+        want = "grid-20.txt"
+    assert sorted(p.name for p in ck.iterdir()) == sorted([want, "meta.json", "notes.txt"])

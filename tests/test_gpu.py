@@ -866,6 +866,31 @@ def test_u8_via_bits_graphs_and_chunked_runs(gpu):
     assert graphs > 0
 
 
+def test_u8_via_bits_graphs_survive_drift_rotation(gpu, monkeypatch):
+    """A drifting (adder-window) kernel leaves the byte tile drifted; every
+    read-out rotates the drift out, which flips the byte buffer pair and so
+    moves the bit scratch.  Equal-length chunks must not replay a graph
+    captured against the other buffer (graphs are keyed by both parities)."""
+    monkeypatch.setenv("GOL_XLANE", "3")  # kXlaneAdd: the drifting adder window
+    W, H = 4096, 1024
+    g = random_grid(W, H, 21)
+    sim = Simulation(LifeConfig(W, H, gen_limit=4000, layout="u8", u8_compute="bits", graphs="on",
+                                check_similarity=False), engine="hip")
+    eng = sim.native_engine
+    assert eng.graphs() and eng.drifting
+    sim.load(g)
+    want = g
+    graphs = 0
+    drifted = 0
+    for _ in range(4):
+        sim.advance(2 * eng.epoch_depth)
+        graphs += sim.last_report.graph_launches
+        drifted += eng.drift != 0
+        want = life_step_torch(want, 2 * eng.epoch_depth, device="cuda")
+        assert (sim.tile() == want).all()
+    assert graphs > 0 and drifted > 0
+
+
 # ---- resident epochs (life_resident_impl.hpp) -------------------------------
 
 def _resident_sim(monkeypatch, W, H, k=8, D=0, rccl_self=False, **kw):

@@ -51,6 +51,9 @@ def _torchrun(nproc, args, timeout=240):
 @pytest.mark.parametrize("nproc,cases", [
     (2, "1x2:bits:auto,1x2:u8:on,2x1:bits:off,1x2:bits:edges"),
     (4, "1x4:bits:auto,2x2:bits:off,2x2:u8:auto,1x4:u8:off"),
+    # The node's rank count (bench.py --gpus 8): 1x8 row strips (the default
+    # split) and 2x4 blocks with column halos, plus termination.
+    (8, "1x8:bits:auto,2x4:u8:auto,1x8:u8:off"),
 ])
 def test_rccl_ranks_sharing_one_gpu(gpu, nproc, cases):
     r = _torchrun(nproc, [str(REPO / "tests" / "mp_rccl_worker.py"), cases])
@@ -70,12 +73,34 @@ def test_bench_launches_its_own_ranks_on_gpu(gpu):
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["verified"] is True
+    assert rec["rccl_nranks"] == 2 and len(rec["devices"]) == 2
+    assert all(d["pci_bus_id"] and d["comm_device"] == d["device"] for d in rec["devices"])
     cfg = rec["config"]
     assert cfg["shared_gpus"] is (_ndev() < 2) and cfg["generations_timed"] == 400
     assert "rccl" in cfg["parallelism"] and cfg["halo_bytes_per_step"] > 0
     assert cfg["overlap_mode"] in ("auto:plain", "auto:early")
     ph = cfg["phase_ms_one_step"]
     assert ph["compute_ms"] > 0 and ph["halo_ms"] > 0 and ph["allreduce_ms"] > 0
+
+
+def test_bench_node_rehearsal_8_ranks_full_grid(gpu):
+    """The driver's N = 8 command at the headline grid, rehearsed on the
+    GPUs present: 8 rank processes, RCCL halos and flag all-reduces, torch's
+    own RCCL process group (timing MAX, all_gather of the 32768^2 grid), the
+    overlap auto trial and the fp32 oracle verify."""
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "8", "--share-gpus", "--steps", "2", "--warmup", "1",
+           "--prewarm", "0", "--verify", "48"]
+    r = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["rccl_nranks"] == 8 and rec["verified"] is True
+    assert rec["headline"] is True and rec["config_id"] == 3
+    assert sorted(d["rank"] for d in rec["devices"]) == list(range(8))
+    cfg = rec["config"]
+    assert cfg["parallelism"].startswith("1x8") and cfg["generations_timed"] == 2000
+    assert cfg["overlap_mode"] in ("auto:plain", "auto:early")
 
 
 def test_bench_refuses_more_ranks_than_gpus_without_share(gpu):
