@@ -179,6 +179,9 @@ std::unique_ptr<Backend> make_cpu_backend(int threads, int drift = -1);
 // Defined in backend_hip.hip; throws if no device or the kernels are missing.
 std::unique_ptr<Backend> make_hip_backend(int device);
 bool hip_available();
+// Whether the HIP kernels were built with GOL_EXPERIMENTAL (the measured-
+// slower variants and schedules; docs/PERFORMANCE.md).
+bool experimental_build();
 
 // Counter-based RNG used by init_random (host and device agree bit-for-bit).
 GOL_HD inline uint64_t splitmix64(uint64_t x) {

@@ -134,6 +134,7 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
     (g.layout == Layout::U8 ? launch_u8_w1_add : launch_bits_w1_add)(p, rows, a.T, tune, stream);
     return a.T;
   }
+#ifdef GOL_EXPERIMENTAL
   if (g.layout == Layout::U8) {
     (x == kXlaneCarry ? launch_u8_w1_carry : launch_u8_w1_dpp)(p, rows, a.T, tune, stream);
   } else if (w == 2) {
@@ -142,6 +143,14 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
     (x == kXlaneCarry ? launch_bits_w1_carry
                       : x == kXlaneBpermute ? launch_bits_w1_bperm : launch_bits_w1_dpp)(p, rows, a.T, tune, stream);
   }
+#else
+  // Default build: the DPP and adder windows, one word per lane (the
+  // bpermute / carry-chain windows and two words per lane measured slower
+  // and are compiled only with GOL_EXPERIMENTAL; HipBackend refuses them).
+  GOL_REQUIRE(w == 1 && x == kXlaneDpp, "life_block: variant '" + life_block_variant(g.layout, tune) +
+                                            "' needs an experimental build (GOL_EXPERIMENTAL=1)");
+  (g.layout == Layout::U8 ? launch_u8_w1_dpp : launch_bits_w1_dpp)(p, rows, a.T, tune, stream);
+#endif
   return 0;
 }
 

@@ -12,7 +12,14 @@
 #pragma once
 
 #include "life_pipe_impl.hpp"
+#ifdef GOL_EXPERIMENTAL
+// Measured-slower schedules (docs/PERFORMANCE.md): short segments, bit-layout
+// level-pipelined pairs, linked launches, the split and skewed schedules are
+// compiled only into experimental builds (GOL_EXPERIMENTAL=1 native_build);
+// the default build keeps the grouped / chained / classic kernels and the
+// byte layout's T = 48 pipelined pass.
 #include "life_short_impl.hpp"
+#endif
 
 namespace gol {
 namespace hipk {
@@ -30,6 +37,7 @@ constexpr int kSplitMaxRowsPerT = 8;
 // stream, after an event recorded just before the previous launch (so it
 // starts no earlier than that one), and waits for its input rows group by
 // group.
+#ifdef GOL_EXPERIMENTAL
 template <int T, class IO>
 bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const LifeTuning& tune, hipStream_t s) {
   using LIO = Sc1IO<IO>;
@@ -85,6 +93,7 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   L.prev_valid = true;
   return true;
 }
+#endif  // GOL_EXPERIMENTAL
 
 template <int T, class IO>
 void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
@@ -115,11 +124,13 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
   // tiles, whose launches alone hold 2 waves per SIMD).  Any other launch
   // first joins the two streams.
   if (tune.link) {
+#ifdef GOL_EXPERIMENTAL
     if constexpr (IO::kBits && IO::W == 1 && (T == 8 || T == 12 || T == 16) &&
                   (IO::XL == kXlaneDpp || IO::XL == kXlaneAdd)) {
       if (tune.group != 0 && tune.split == 0 && !tune.skew && dual == 1 && launch_linked<T, IO>(p, out_rows, simds, tune, s))
         return;
     }
+#endif
     link_join(*tune.link);
   }
   if constexpr (T >= 4) {
@@ -146,6 +157,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       // kernel; the byte layout spills at 4 waves/SIMD): lets small tiles
       // fill 4 waves per SIMD.
       const auto better = [](double a, double b) { return a > 0 && (b < 0 || a <= b); };
+#ifdef GOL_EXPERIMENTAL
       if constexpr (IO::kBits && IO::W == 1 &&
                     ((T == 16 && IO::XL == kXlaneDpp) || (T == 12 && IO::XL == kXlaneAdd))) {
         LifeBlockParams s8 = p;
@@ -173,6 +185,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
             return use8 ? launch_pipe<T1, T2, IO, 8>(p8, s) : launch_pipe<T1, T2, IO, 4>(p4, s);
         }
       }
+#endif  // GOL_EXPERIMENTAL
       // Chained groups (GOL_CHAIN): every group boundary shared through
       // global memory, so no wave carries a redundant triangle but the
       // strip's last.  Stream launches only (the flags count launches, so a
@@ -205,6 +218,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
       if (better(c8, cc)) return launch_group<T, IO, 8>(g8, s);
     }
+#ifdef GOL_EXPERIMENTAL
     // The split kernels address boundary states by padded column: halo mode only.
     bool split = tune.split > 0 && IO::XL != kXlaneAdd && dual == 1 && p.wrap_w == 0;
     if (tune.split < 0 && !tune.skew && IO::XL != kXlaneAdd && dual == 1 && p.wrap_w == 0) {
@@ -229,16 +243,27 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
                            dim3(256), 0, s, p);
       return;
     }
+#endif  // GOL_EXPERIMENTAL
   }
+#ifdef GOL_EXPERIMENTAL
   const int occ = tune.skew ? waves_per_simd<T, IO, true, false>() : waves_per_simd<T, IO, false, false>();
   const bool skew = plan(p, T, out_rows, simds, occ, tune.min_seg_rows, tune.target_waves, -1, nullptr, IO::XL) &&
                     tune.skew;
+#else
+  const bool skew = false;
+  plan(p, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves, -1,
+       nullptr, IO::XL);
+#endif
   const int waves = p.ncolw * p.nseg * dual;
   const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
-  if (skew)
+#ifdef GOL_EXPERIMENTAL
+  if (skew) {
     hipLaunchKernelGGL((life_block_kernel<T, IO, true>), grid, block, 0, s, p);
-  else
-    hipLaunchKernelGGL((life_block_kernel<T, IO, false>), grid, block, 0, s, p);
+    return;
+  }
+#endif
+  (void)skew;
+  hipLaunchKernelGGL((life_block_kernel<T, IO, false>), grid, block, 0, s, p);
 }
 
 // Deep byte-layout passes (T = 24, 32): instantiated in translation units of
@@ -311,14 +336,15 @@ void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const Lif
     case 8: launch_T<8, IO>(p, out_rows, tune, s); break;
     case 12: launch_T<12, IO>(p, out_rows, tune, s); break;
     case 16: launch_T<16, IO>(p, out_rows, tune, s); break;
-    case 24:  // byte layout only: HBM-bound, so a deeper pass pays (one read + write per launch)
-      if constexpr (!IO::kBits) {
+    case 24:  // byte layout only: fewer byte-grid passes per generation
+      // (the adder window never runs T > 16: launch_life_block switches it to DPP)
+      if constexpr (!IO::kBits && IO::XL != kXlaneAdd) {
         launch_deep<24, IO>(p, out_rows, tune, s);
         break;
       }
       [[fallthrough]];
     case 32:
-      if constexpr (!IO::kBits) {
+      if constexpr (!IO::kBits && IO::XL != kXlaneAdd) {
         if (T == 32) {
           launch_deep<32, IO>(p, out_rows, tune, s);
           break;

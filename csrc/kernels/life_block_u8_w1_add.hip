@@ -2,8 +2,6 @@
 // one-sided add-with-carry window, no cross-lane data ops.
 #include "life_block_launch.hpp"
 
-GOL_U8_DEEP(extern, 24, kXlaneAdd)
-GOL_U8_DEEP(extern, 32, kXlaneAdd)
 
 namespace gol {
 namespace hipk {

@@ -176,14 +176,27 @@ int life_block_max_T(Layout layout, const LifeTuning& tune);
 #define GOL_LIFE_VARIANT(name) \
   void name(const LifeBlockParams& p, int64_t out_rows, int T, const LifeTuning& tune, hipStream_t s)
 GOL_LIFE_VARIANT(launch_bits_w1_dpp);
+GOL_LIFE_VARIANT(launch_u8_w1_dpp);
+GOL_LIFE_VARIANT(launch_bits_w1_add);
+GOL_LIFE_VARIANT(launch_u8_w1_add);
+#ifdef GOL_EXPERIMENTAL  // measured slower (docs/PERFORMANCE.md); experimental builds only
 GOL_LIFE_VARIANT(launch_bits_w1_bperm);
 GOL_LIFE_VARIANT(launch_bits_w2_dpp);
 GOL_LIFE_VARIANT(launch_bits_w1_carry);
 GOL_LIFE_VARIANT(launch_bits_w2_carry);
-GOL_LIFE_VARIANT(launch_u8_w1_dpp);
 GOL_LIFE_VARIANT(launch_u8_w1_carry);
-GOL_LIFE_VARIANT(launch_bits_w1_add);
-GOL_LIFE_VARIANT(launch_u8_w1_add);
+#endif
+
+// Whether this build carries the measured-slower variants and schedules
+// (GOL_EXPERIMENTAL=1 native_build): resident epochs, split / skewed / short /
+// linked / bit-layout pipelined schedules, bpermute and carry-chain windows,
+// two words per lane.
+constexpr bool kExperimentalBuild =
+#ifdef GOL_EXPERIMENTAL
+    true;
+#else
+    false;
+#endif
 
 // ---- Resident epoch kernel (life_resident_impl.hpp) ------------------------
 // A whole temporal block of T generations (a full halo epoch) in ONE launch,

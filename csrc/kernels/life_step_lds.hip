@@ -508,10 +508,15 @@ int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, int wave
                      const int64_t*, int64_t, int64_t, int64_t, int64_t, int64_t, int, int);
   const auto pick = [&](auto nw_c) -> K {
     constexpr int NW = decltype(nw_c)::value;
-    return add ? (a.T == 8 ? life_lds_bits_kernel<8, true, NW> : a.T == 16 ? life_lds_bits_kernel<16, true, NW>
-                                                                           : life_lds_bits_kernel<32, true, NW>)
-               : (a.T == 8 ? life_lds_bits_kernel<8, false, NW> : a.T == 16 ? life_lds_bits_kernel<16, false, NW>
-                                                                            : life_lds_bits_kernel<32, false, NW>);
+#ifdef GOL_EXPERIMENTAL  // the adder window in the packed tile (GOL_LDS_ADD): exact, measured slower
+    if (add)
+      return a.T == 8 ? life_lds_bits_kernel<8, true, NW> : a.T == 16 ? life_lds_bits_kernel<16, true, NW>
+                                                                      : life_lds_bits_kernel<32, true, NW>;
+#else
+    GOL_REQUIRE(!add, "life_lds_bits: the adder window (GOL_LDS_ADD) needs an experimental build");
+#endif
+    return a.T == 8 ? life_lds_bits_kernel<8, false, NW> : a.T == 16 ? life_lds_bits_kernel<16, false, NW>
+                                                                     : life_lds_bits_kernel<32, false, NW>;
   };
   const K k = nw == 16 ? pick(std::integral_constant<int, 16>{}) : pick(std::integral_constant<int, 8>{});
   hipLaunchKernelGGL(k, grid, dim3(64 * nw), 0, stream, static_cast<const uint8_t*>(a.in), static_cast<uint8_t*>(a.out),

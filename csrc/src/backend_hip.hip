@@ -127,6 +127,7 @@ class HipBackend final : public Backend {
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
+    if (!hipk::kExperimentalBuild) refuse_experimental();
     tune_log_ = env_int("GOL_TUNE_LOG", 0) != 0;
     tune_.chain_seq = &chain_seq_;
     // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words
@@ -440,6 +441,9 @@ class HipBackend final : public Backend {
       tune_.chain_ok = (!a.stream || a.stream == stream_) && !capturing && !linkable;
     }
     if (a.resident) {  // the engine runs this epoch as one resident launch
+#ifndef GOL_EXPERIMENTAL
+      fail("resident epochs need an experimental build (GOL_EXPERIMENTAL=1)");
+#else
       join_streams();
       ++launches_;
       hipk::ResidentPlan pl;
@@ -484,6 +488,7 @@ class HipBackend final : public Backend {
         std::fclose(f);
       }
       return drift;
+#endif  // GOL_EXPERIMENTAL
     }
     if (trace_at_ >= 0 && launches_ == trace_at_) {
       join_streams();
@@ -646,6 +651,10 @@ class HipBackend final : public Backend {
   // waves per SIMD (the adder window's occupancy), where the resident launch
   // measured faster (docs/PERFORMANCE.md, "Resident epochs").
   int resident_epoch(Layout l, int64_t rows, int64_t cols, int D_req, bool multi) const override {
+#ifndef GOL_EXPERIMENTAL
+    (void)l, (void)rows, (void)cols, (void)D_req, (void)multi;
+    return 0;
+#else
     if (resident_mode_ == 0 || l != Layout::Bits || !tune_.wrap || cols % 32 != 0 || tune_.wpl_bits >= 2) return 0;
     {
       std::lock_guard<std::mutex> lk(live_mu());
@@ -667,8 +676,10 @@ class HipBackend final : public Backend {
       if (strips * (rows / 24) >= int64_t(16) * cus_) return 0;  // the grouped adder kernel fills 4 waves/SIMD
     }
     return D;
+#endif
   }
   void reserve_resident(const TileGeom& /*g*/) override {
+    if (!hipk::kExperimentalBuild) return;
     const size_t mb = size_t(cus_) * hipk::kResidentRecBytes;  // one exchange record per workgroup
     tune_.chain_mem(5, mb);
     tune_.chain_mem(6, mb);
@@ -822,6 +833,27 @@ class HipBackend final : public Backend {
   }
 
  private:
+  // Default builds carry neither the measured-slower variants nor their
+  // schedules (hipk::kExperimentalBuild): an environment asking for one fails
+  // here, loudly, instead of silently running the default kernel.
+  static void refuse_experimental() {
+    struct Knob {
+      const char* name;
+      int dflt;
+    };
+    static const Knob knobs[] = {{"GOL_WPL", 1},  {"GOL_SKEW", 0},     {"GOL_SPLIT", 0}, {"GOL_SHORT", 0},
+                                 {"GOL_PIPE", 0}, {"GOL_LINK", 0},     {"GOL_RESIDENT", 0},
+                                 {"GOL_LDS_ADD", 0}};
+    for (const Knob& k : knobs)
+      if (env_int(k.name, k.dflt) != k.dflt)
+        fail(std::string(k.name) + "=" + std::getenv(k.name) +
+             " selects a measured-slower variant that this build does not carry; rebuild with "
+             "GOL_EXPERIMENTAL=1 python -m gol_amd.native_build");
+    const int x = env_int("GOL_XLANE", hipk::kXlaneAuto);
+    if (x == hipk::kXlaneBpermute || x == hipk::kXlaneCarry)
+      fail("GOL_XLANE=" + std::to_string(x) + " (ds_bpermute / carry-chain window) needs an experimental build "
+           "(GOL_EXPERIMENTAL=1 python -m gol_amd.native_build)");
+  }
   int64_t rows_per_chunk(const TileGeom& g) const {
     const int64_t budget = int64_t(256) << 20;
     return std::max<int64_t>(1, std::min<int64_t>(g.H, budget / std::max<int64_t>(1, g.W)));
@@ -890,6 +922,8 @@ class HipBackend final : public Backend {
 };
 
 }  // namespace
+
+bool experimental_build() { return hipk::kExperimentalBuild; }
 
 bool hip_available() {
   int n = 0;

@@ -24,22 +24,34 @@ from pathlib import Path
 PKG_DIR = Path(__file__).resolve().parent
 REPO = PKG_DIR.parent
 CSRC = REPO / "csrc"
-BUILD = REPO / "build" / "obj"
 BIN = REPO / "bin"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("GOL_OFFLOAD_ARCH", "gfx950")
+# GOL_EXPERIMENTAL=1: also compile the variants and schedules that were
+# measured slower than the defaults (docs/PERFORMANCE.md "What was tried"):
+# resident epochs, split / skewed / short-segment / linked / bit-layout
+# pipelined schedules, the ds_bpermute and carry-chain windows, two words per
+# lane, the packed LDS tile's adder window.  The default build leaves them out
+# (a smaller module and GPU tier); the backend refuses their knobs loudly.
+EXPERIMENTAL = os.environ.get("GOL_EXPERIMENTAL", "0") not in ("", "0")
+BUILD = REPO / "build" / ("obj_exp" if EXPERIMENTAL else "obj")
+MODE_STAMP = PKG_DIR / "_gol.mode"  # which mode _gol.so / bin/* were linked in (travels with the .so)
 
 HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/transport.cpp",
              "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp"]
-LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "bits_w1_add", "u8_w1_dpp",
-                 "u8_w1_carry", "u8_w1_add",
-                 *[f"u8_w1_{x}_t{t}" for x in ("dpp", "carry", "add") for t in (24, 32)],  # deep byte passes
+LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_add", "u8_w1_dpp", "u8_w1_add",
+                 *[f"u8_w1_dpp_t{t}" for t in (24, 32)],  # deep byte passes
                  "u8_w1_dpp_t48"]  # pipelined wave pairs (life_pipe_impl.hpp)
+EXPERIMENTAL_VARIANTS = ["bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "u8_w1_carry",
+                         "u8_w1_carry_t24", "u8_w1_carry_t32"]
 RESIDENT_TUS = 9  # life_resident_rw0..8.hip: the resident kernel's rows-per-wave instantiations
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
             *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
-            "kernels/tile_ops.hip", "kernels/life_resident.hip",
-            *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)]]
+            "kernels/tile_ops.hip"]
+if EXPERIMENTAL:
+    HIP_SRCS += [*[f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS], "kernels/life_resident.hip",
+                 *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)]]
+MODE = "experimental" if EXPERIMENTAL else "default"
 BIND_SRCS = ["src/bindings.cpp"]
 CLI_MAIN = "tools/gol_main.cpp"
 GEN_MAIN = "tools/gol_gen.cpp"
@@ -62,7 +74,7 @@ def _headers_mtime() -> float:
 
 
 def _compile_cmd(src: Path, obj: Path) -> list[str]:
-    inc = [f"-I{CSRC / 'include'}", f"-I{CSRC}"]
+    inc = [f"-I{CSRC / 'include'}", f"-I{CSRC}", *(["-DGOL_EXPERIMENTAL=1"] if EXPERIMENTAL else [])]
     if src.suffix == ".hip":
         extra = []
         if src.name.startswith("life_block_"):
@@ -138,12 +150,14 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         "gol": BIN / "gol",
         "gol_gen": BIN / "gol_gen",
     }
-    relink = bool(todo) or force or any(not p.exists() for p in outs.values())
+    stamp = MODE_STAMP.read_text().strip() if MODE_STAMP.exists() else ""
+    relink = bool(todo) or force or any(not p.exists() for p in outs.values()) or stamp != MODE
     if relink:
         _run([_hipcc(), "-shared", "-fPIC", *core, str(objs[BIND_SRCS[0]]), "-o", str(MODULE), *rocm_libs],
              verbose)
         _run([_hipcc(), *core, str(objs[CLI_MAIN]), "-o", str(outs["gol"]), *rocm_libs], verbose)
         _run([_hipcc(), *core, str(objs[GEN_MAIN]), "-o", str(outs["gol_gen"]), *rocm_libs], verbose)
+        MODE_STAMP.write_text(MODE + "\n")
     return outs
 
 
@@ -180,6 +194,8 @@ def build_selftest(kind: str = "address", verbose: bool = False, jobs: int | Non
 
 def is_built() -> bool:
     if not MODULE.exists():
+        return False
+    if not MODE_STAMP.exists() or MODE_STAMP.read_text().strip() != MODE:
         return False
     hdr = _headers_mtime()
     newest = max([(CSRC / s).stat().st_mtime for s in HOST_SRCS + HIP_SRCS + BIND_SRCS] + [hdr])

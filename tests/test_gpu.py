@@ -11,6 +11,10 @@ from gol_amd.parallel import InProcessGroup
 from golden import CASES, CONVERGING, GLIDER
 
 pytestmark = pytest.mark.gpu
+# Measured-slower variants and schedules: compiled only into experimental
+# builds (GOL_EXPERIMENTAL=1 native_build); skipped when the module lacks them.
+experimental = pytest.mark.experimental
+X = experimental
 
 
 @pytest.fixture(autouse=True)
@@ -55,8 +59,9 @@ def test_every_temporal_block_size(gpu, tmax, layout):
     assert (got == want).all()
 
 
-@pytest.mark.parametrize("wpl,xlane,skew", [(1, 0, 0), (1, 1, 0), (1, 2, 0), (2, 0, 0), (2, 2, 0), (1, 0, 1),
-                                            (1, 2, 1), (2, 0, 1), (1, 3, 0), (1, 3, 1)])
+@pytest.mark.parametrize("wpl,xlane,skew", [(1, 0, 0), (1, 3, 0)] + [
+    pytest.param(*v, marks=X) for v in [(1, 1, 0), (1, 2, 0), (2, 0, 0), (2, 2, 0), (1, 0, 1), (1, 2, 1), (2, 0, 1),
+                                        (1, 3, 1)]])
 @pytest.mark.parametrize("tmax", [1, 4, 8, 12, 16])
 def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
     """Every compiled life_block variant (words/lane x DPP|bpermute|carry x
@@ -79,7 +84,7 @@ def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
         assert (out == ref).all(), seed
 
 
-@pytest.mark.parametrize("xlane", [0, 2, 3])
+@pytest.mark.parametrize("xlane", [0, pytest.param(2, marks=X), 3])
 @pytest.mark.parametrize("tmax", [1, 8, 16])
 def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
     monkeypatch.setenv("GOL_XLANE", str(xlane))
@@ -91,7 +96,7 @@ def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
 
 
 @pytest.mark.parametrize("tmax", [24, 32])
-@pytest.mark.parametrize("xlane", [0, 2, 3])
+@pytest.mark.parametrize("xlane", [0, pytest.param(2, marks=X), 3])
 def test_deep_byte_passes_vs_torch(gpu, monkeypatch, tmax, xlane):
     """T = 24 / 32 byte-layout passes (life_block_u8_w1_*_t24/_t32.hip, the
     HBM-bound layout's deep passes) in every byte variant and schedule,
@@ -195,6 +200,7 @@ def test_grouped_schedule_many_groups_and_termination(gpu, monkeypatch, group):
         assert (out == ref).all(), layout
 
 
+@experimental
 @pytest.mark.parametrize("layout", ["bits", "u8"])  # u8: falls back to the grouped kernel
 @pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
@@ -212,6 +218,7 @@ def test_short_segment_schedule_vs_torch(gpu, monkeypatch, layout, W, H, xlane, 
         assert (life_step(g, 35, engine="hip", layout=layout, tmax=tmax) == want).all(), target
 
 
+@experimental
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
 def test_short_segment_schedule_termination(gpu, monkeypatch, xlane, tmax):
     monkeypatch.setenv("GOL_SHORT", "2")
@@ -227,6 +234,7 @@ def test_short_segment_schedule_termination(gpu, monkeypatch, xlane, tmax):
         assert (out == ref).all(), layout
 
 
+@experimental
 @pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (3, 16), (0, 12)])
 def test_pipe_schedule_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
@@ -247,6 +255,7 @@ def test_pipe_schedule_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
         assert (sim.tile() == want).all(), target
 
 
+@experimental
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
 def test_pipe_schedule_termination(gpu, monkeypatch, xlane, tmax):
     """Exact Generations with the pipelined pairs: both stages raise their
@@ -462,6 +471,7 @@ def test_u8_lds_termination(gpu, monkeypatch, W, H, seed, density):
     assert (out == ref).all()
 
 
+@experimental
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("tmax", [4, 8, 16])
 @pytest.mark.parametrize("W,H", [(4000 - 4000 % 32, 1500), (2048, 333), (96, 100)])
@@ -477,6 +487,7 @@ def test_split_schedule_vs_torch(gpu, monkeypatch, layout, tmax, W, H):
     assert (got == want).all()
 
 
+@experimental
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
 def test_split_schedule_termination(gpu, monkeypatch, W, H, seed, density):
     monkeypatch.setenv("GOL_SPLIT", "1")
@@ -489,6 +500,7 @@ def test_split_schedule_termination(gpu, monkeypatch, W, H, seed, density):
         assert (out == ref).all()
 
 
+@experimental
 def test_split_schedule_tall_grid_flags(gpu, monkeypatch):
     """Many boundaries per launch; the changed flags of both phases must OR
     to the exact per-generation result (compare a run that stops early)."""
@@ -757,6 +769,7 @@ def test_pipelined_byte_pass_t48_termination_and_ranks(gpu):
     assert (grp.gather() == want).all()
 
 
+@experimental
 @pytest.mark.parametrize("W,H", [(32768, 1024), (4096, 700), (2048 * 3, 333), (32 * 100, 1000)])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (0, 8), (3, 12), (0, 12)])
 def test_linked_launches_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
@@ -776,6 +789,7 @@ def test_linked_launches_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
     assert rep.linked_launches > 0
 
 
+@experimental
 def test_linked_launches_termination_and_subdomains(gpu, monkeypatch):
     monkeypatch.setenv("GOL_LINK", "1")
     grid = np.zeros((1024, 2048), dtype=np.uint8)
@@ -912,6 +926,7 @@ def _resident_sim(monkeypatch, W, H, k=8, D=0, rccl_self=False, **kw):
     return sim
 
 
+@experimental
 @pytest.mark.parametrize("W,H,k,D", [(4096, 1024, 8, 0), (32 * 200, 700, 16, 48), (2048, 333, 4, 64),
                                      (32768, 512, 8, 128), (96, 70, 8, 40)])
 def test_resident_epochs_vs_torch(gpu, monkeypatch, W, H, k, D):
@@ -925,6 +940,7 @@ def test_resident_epochs_vs_torch(gpu, monkeypatch, W, H, k, D):
     assert (sim.tile() == life_step_torch(g, 301, device="cuda")).all()
 
 
+@experimental
 def test_resident_chunked_runs_and_rehearsal(gpu, monkeypatch):
     """Chunked runs (partial epochs at every chunk end) and the multi-rank
     epoch schedule against a self-exchanging transport (deep halo rows)."""
@@ -941,6 +957,7 @@ def test_resident_chunked_runs_and_rehearsal(gpu, monkeypatch):
         del sim
 
 
+@experimental
 @pytest.mark.parametrize("case", [c for c in CONVERGING if c[0] % 32 == 0] + [(256, 512, 77, 0.5)])
 def test_resident_termination_matches_reference(gpu, monkeypatch, case):
     """The per-generation change flags of resident launches (one LDS slot per
@@ -955,6 +972,7 @@ def test_resident_termination_matches_reference(gpu, monkeypatch, case):
     assert (sim.tile() == ref).all()
 
 
+@experimental
 def test_resident_termination_large_still_life(gpu, monkeypatch):
     """A soup that dies out inside a long epoch: the first unchanged
     generation lies deep inside one resident launch."""
@@ -970,6 +988,7 @@ def test_resident_termination_large_still_life(gpu, monkeypatch):
     assert (sim.tile() == ref).all()
 
 
+@experimental
 def test_resident_u8_via_bits_and_graphs(gpu, monkeypatch):
     monkeypatch.setenv("GOL_U8_VIA_BITS", "1")
     W, H = 4096, 1024
@@ -982,6 +1001,7 @@ def test_resident_u8_via_bits_and_graphs(gpu, monkeypatch):
         del sim
 
 
+@experimental
 def test_resident_off_when_ranks_share_the_gpu(gpu, monkeypatch):
     """Four in-process ranks on one device: a resident launch could not get
     every CU, so the engines fall back to the grouped kernels (still exact)."""
