@@ -239,7 +239,7 @@ def main() -> int:
         # included: every rank has its own NCCL_HOSTID, so torch's own RCCL
         # communicator (gather_grid, the MAX of the rank timings) runs the
         # same code path as on the node.
-        dist = init_process_group("nccl" if on_gpu else "gloo")
+        dist = init_process_group("nccl" if on_gpu else "gloo", device=local if on_gpu else None)
         transport = make_transport(a.comm, backend, local)
     elif a.rehearse_rccl and on_gpu:
         C = native()

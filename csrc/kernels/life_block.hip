@@ -93,6 +93,7 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   p.wg_trace = tune.wg_trace;
   p.err = tune.err;
   p.chain_spin_log2 = tune.chain_spin_log2;
+  p.chain_acquire = tune.chain_acquire ? 1 : 0;
   p.row_alt = a.dual_offset;
   p.prio_boost = a.prio_boost ? 1 : 0;
   p.wrap_w = a.full_width && tune.wrap && g.W % 32 == 0 ? int(g.W / 32) : 0;

@@ -67,6 +67,9 @@ struct LifeBlockParams {
   uint32_t* chain_flag;
   uint32_t chain_seq;
   int64_t chain_end;
+  // 1: the consumer adds an agent-scope acquire (L1 invalidate) after its
+  // poll matched, on top of the sc1 loads (LifeTuning::chain_acquire).
+  int chain_acquire;
   // Linked launches (LifeTuning::link, life_group_kernel<..., LINK = true>):
   // this launch may run while the previous grouped launch, whose output is
   // its input, still runs.  Group (kcol, grp) first waits until every group
@@ -158,6 +161,7 @@ struct LifeTuning {
   uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
   uint32_t* err = nullptr;       // LifeBlockParams::err (4 words: code, then a give-up's diagnostics)
   int chain_spin_log2 = 16;      // LifeBlockParams::chain_spin_log2
+  bool chain_acquire = true;     // LifeBlockParams::chain_acquire (GOL_CHAIN_ACQUIRE)
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).
   std::function<void*(size_t)> scratch;
 };

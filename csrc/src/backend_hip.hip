@@ -160,6 +160,7 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 4 * sizeof(uint32_t), hipHostMallocMapped));
     for (int i = 0; i < 4; ++i) err_host_[i] = 0;
     tune_.chain_spin_log2 = std::min(24, std::max(4, env_int("GOL_CHAIN_SPIN", 16)));
+    tune_.chain_acquire = env_int("GOL_CHAIN_ACQUIRE", 1) != 0;
     HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&tune_.err), err_host_, 0));
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
@@ -643,6 +644,19 @@ class HipBackend final : public Backend {
       constexpr int64_t kT = 12;
       const int64_t strips = ceil_div(ceil_div(cols, 32) + 16, 63);  // + a deep halo's words
       if (strips * (rows / (2 * kT)) >= int64_t(16) * cus_) k = {int(kT), true};
+    }
+    // DPP window on a small tile: the deepest T whose 2T-row segments still
+    // give every SIMD two waves; below two waves per SIMD a wave's level chain
+    // runs exposed (8192^2: T = 16 2.39-2.41 ms per 1000 generations, 1 wave
+    // per SIMD; T = 12 2.48-2.50; T = 8 2.05-2.08, 2 waves; T = 4 2.97 (twice
+    // the launches); the 8-GPU rank tile 32768 x 4096 keeps T = 16 at 2 waves;
+    // profiles/r04/small_grid_T_sweep.jsonl).
+    if (!k.drift && tmax_req <= 0 && l == Layout::Bits && one_word && tune_.group != 0 && k.tmax == 16) {
+      const int64_t strips = ceil_div(ceil_div(cols, 32) + 16, 63);
+      for (int t : {16, 12, 8}) {
+        k.tmax = t;
+        if (strips * (rows / (2 * t)) >= int64_t(8) * cus_) break;
+      }
     }
     return k;
   }

@@ -109,7 +109,8 @@ def main(argv=None) -> int:
     if world > 1:
         from .parallel.dist import init_process_group, make_transport  # noqa: PLC0415
 
-        init_process_group("nccl" if backend.is_device() else "gloo")
+        init_process_group("nccl" if backend.is_device() else "gloo",
+                           device=int(backend.device()) if backend.is_device() else None)
         transport = make_transport(a.comm, backend, local)
     else:
         from ._native import native  # noqa: PLC0415

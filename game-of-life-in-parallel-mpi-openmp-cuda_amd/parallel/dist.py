@@ -53,8 +53,10 @@ def stdout_to_stderr():
         os.close(saved)
 
 
-def init_process_group(backend: Optional[str] = None, timeout_s: int = 600):
-    """Initialise torch.distributed from the torchrun environment (idempotent)."""
+def init_process_group(backend: Optional[str] = None, timeout_s: int = 600, device: Optional[int] = None):
+    """Initialise torch.distributed from the torchrun environment (idempotent).
+    ``device``: this rank's GPU for the ``nccl`` backend (default LOCAL_RANK;
+    ranks sharing GPUs pass LOCAL_RANK modulo the device count)."""
     import torch  # noqa: PLC0415
     import torch.distributed as dist  # noqa: PLC0415
 
@@ -67,8 +69,9 @@ def init_process_group(backend: Optional[str] = None, timeout_s: int = 600):
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     kw = {}
     if backend == "nccl":
-        torch.cuda.set_device(local)
-        kw["device_id"] = torch.device("cuda", local)
+        dev = local if device is None else int(device)
+        torch.cuda.set_device(dev)
+        kw["device_id"] = torch.device("cuda", dev)
     with stdout_to_stderr():
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
