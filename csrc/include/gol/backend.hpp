@@ -149,6 +149,16 @@ class Backend {
   // deep byte pass plans whole wave-pair groups); the engine keeps every
   // block at least this tall or uses a smaller T.
   virtual int64_t min_block_rows(Layout /*l*/, int /*T*/) const { return 1; }
+  // Row ring (single-rank torus): a tile whose top Dv halo rows are a second
+  // virtual mapping of its last Dv owned rows and whose bottom halo rows map
+  // its first ones, so the periodic row halos are always valid and never
+  // filled.  row_ring_halo() returns the halo rows per side (>= min_halo) a
+  // ring of H rows of `pitch` bytes needs for the mapping granularity, or 0
+  // when the backend cannot build one for that geometry; alloc_row_ring()
+  // returns such a tile (zeroed) for a geometry with that Dv, or nullptr.
+  // release() frees rings too.
+  virtual int row_ring_halo(int64_t /*H*/, int64_t /*pitch*/, int /*min_halo*/) const { return 0; }
+  virtual void* alloc_row_ring(const TileGeom& /*g*/) { return nullptr; }
   // Periodic self-fill of halo regions of a single tile (any tile size):
   // columns (left/right halo words of owned rows) and/or rows (full padded
   // rows of the top/bottom halo, which also fills the corners).

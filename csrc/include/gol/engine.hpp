@@ -165,6 +165,9 @@ class Engine {
   bool via_bits() const { return via_bits_; }
   // Whether every epoch runs as one resident launch (Backend::resident_epoch).
   bool resident() const { return resident_; }
+  // Whether the tile is a row ring (Backend::row_ring_halo): no row fills,
+  // one temporal block per epoch over the owned rows.
+  bool row_ring() const { return rows_ring_; }
   // Rotates the drift out of the current buffer (owned rows); every
   // read-out (store_cells) does this first.
   void normalize();
@@ -283,6 +286,7 @@ class Engine {
   bool drift_ok_ = false;   // whole-width tile of 32-cell words on a drifting backend
   bool cols_filled_ = true; // column halos kept valid by fills (false: the backend wraps column reads)
   bool rows_wrapped_ = false; // single-rank torus read modulo its rows (no fills at all)
+  bool rows_ring_ = false;    // row halos are second mappings of the owned rows (Backend::row_ring_halo)
   bool via_bits_ = false;    // byte layout computed on bit words (epoch_via_bits)
   bool resident_ = false;    // one launch per epoch, tile resident in registers (Backend::resident_epoch)
   TileGeom gb_;              // the tile in the bit layout (same rows, halos, words)

@@ -134,21 +134,25 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
     link_join(*tune.link);
   }
   if constexpr (T >= 4) {
-    if (tune.group != 0 && (tune.split == 0 || dual == 2) && !tune.skew) {
+    // Bit-layout blocks of T <= 8 (small tiles, HipBackend::choose_kernel)
+    // group 4 waves by default: 8192^2 at T = 8 1.99 vs 2.06 ms per 1000
+    // generations with 8-wave groups (profiles/r04/small_grid_ab.jsonl).
+    const int group = (IO::kBits && T <= 8) ? tune.group_small : tune.group;
+    if (group != 0 && (tune.split == 0 || dual == 2) && !tune.skew) {
       // M = 4 or 8 waves per workgroup; auto (-1) takes the cheapest of
       // M = 4, M = 8 and the classic plan under the makespan model (classic
       // charged its redundant triangle, T-1 rows, at the triangles' ILP).
       LifeBlockParams g4 = p, g8 = p;
-      const double c4 = (tune.group == 4 || tune.group < 0)
+      const double c4 = (group == 4 || group < 0)
                             ? plan_group<T, 4>(g4, out_rows, simds, group_waves_per_simd<T, IO, 4>(),
                                                tune.target_waves, IO::XL)
                             : -1.0;
-      const double c8 = (tune.group == 8 || tune.group < 0)
+      const double c8 = (group == 8 || group < 0)
                             ? plan_group<T, 8>(g8, out_rows, simds, group_waves_per_simd<T, IO, 8>(),
                                                tune.target_waves, IO::XL)
                             : -1.0;
       double cc = -1.0;
-      if (tune.group < 0) {
+      if (group < 0) {
         LifeBlockParams q = p;
         plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves,
              1.2 * (T - 1), &cc, IO::XL);
@@ -161,7 +165,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       if constexpr (IO::kBits && IO::W == 1 &&
                     ((T == 16 && IO::XL == kXlaneDpp) || (T == 12 && IO::XL == kXlaneAdd))) {
         LifeBlockParams s8 = p;
-        const double cs = tune.short_seg && dual == 1 && (tune.group == 8 || tune.group < 0)
+        const double cs = tune.short_seg && dual == 1 && (group == 8 || group < 0)
                               ? plan_short<T, 8>(s8, out_rows, simds, short_waves_per_simd<T, IO, 8>(),
                                                  tune.target_waves, IO::XL)
                               : -1.0;
@@ -194,7 +198,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
         LifeBlockParams ch = p;
         ch.fold = 1;
         ch.fold_lanes = 64;
-        const bool m4 = tune.group == 4;  // 4-wave groups: every 4th boundary chained
+        const bool m4 = group == 4;  // 4-wave groups: every 4th boundary chained
         const double cch =
             m4 ? plan_chain<T, 4>(ch, out_rows, simds, group_waves_per_simd<T, IO, 4>(), tune.target_waves, IO::XL)
                : plan_chain<T, 8>(ch, out_rows, simds, group_waves_per_simd<T, IO, 8>(), tune.target_waves, IO::XL);

@@ -146,6 +146,7 @@ struct LifeTuning {
   int lds_waves = 0;        // packed LDS tiles: waves per workgroup (8, 16; 0 = by grid size)
   int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
+  int group_small = 4;      // the same for bit-layout blocks of T <= 8 (GOL_GROUP_SMALL; GOL_GROUP sets both)
   int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
   int pipe = 0;             // level-pipelined wave pairs (life_pipe_impl.hpp): 0 off, 1 by the model, 2 forced
   bool wrap = true;         // wrap mode on whole-width tiles (BlockArgs::full_width, lane_cols)

@@ -7,11 +7,17 @@
 // kernels (the bit-sliced rule written as plain boolean word expressions, not
 // the kernels' v_bitop3 truth tables).  run_block sweeps per-thread row bands
 // with a 3-row window per level, like the GPU kernel's register schedule.
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "gol/backend.hpp"
@@ -88,6 +94,43 @@ class CpuBackend final : public Backend {
   CpuBackend(int threads, bool drift) : pool_(threads > 0 ? threads : default_host_threads()), drift_(drift) {
     const char* r = std::getenv("GOL_CPU_RESIDENT");
     resident_ = r && *r && *r != '0';
+    const char* ring = std::getenv("GOL_CPU_RING");
+    ring_ = ring && *ring && *ring != '0';
+  }
+  ~CpuBackend() override {
+    for (auto& kv : rings_) ::munmap(kv.first, kv.second);
+  }
+  // GOL_CPU_RING=1: the HIP backend's row ring, emulated with a memfd mapped
+  // three times (last owned rows, the owned rows, first owned rows), so the
+  // engine's ring schedule is testable on the CPU.
+  int row_ring_halo(int64_t H, int64_t pitch, int min_halo) const override {
+    if (!ring_) return 0;
+    const int64_t page = ::sysconf(_SC_PAGESIZE);
+    int64_t dv = std::max<int64_t>(1, min_halo);
+    while ((dv * pitch) % page != 0) ++dv;  // pitch is a multiple of 256
+    if ((H * pitch) % page != 0 || H < dv) return 0;
+    return int(dv);
+  }
+  void* alloc_row_ring(const TileGeom& g) override {
+    if (!ring_) return nullptr;
+    const size_t halo = size_t(g.Dv) * size_t(g.pitch), owned = size_t(g.H) * size_t(g.pitch);
+    const int fd = ::memfd_create("gol_row_ring", 0);
+    GOL_REQUIRE(fd >= 0, std::string("row ring: memfd_create failed: ") + std::strerror(errno));
+    GOL_REQUIRE(::ftruncate(fd, off_t(owned)) == 0, "row ring: ftruncate failed");
+    void* va = ::mmap(nullptr, owned + 2 * halo, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    GOL_REQUIRE(va != MAP_FAILED, "row ring: address reservation failed");
+    auto* b = static_cast<uint8_t*>(va);
+    const auto map = [&](uint8_t* at, size_t len, off_t off) {
+      void* r = ::mmap(at, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, fd, off);
+      GOL_REQUIRE(r == at, "row ring: mmap failed");
+    };
+    map(b, halo, off_t(owned - halo));   // top halo  = last owned rows
+    map(b + halo, owned, 0);             // owned rows
+    map(b + halo + owned, halo, 0);      // bottom halo = first owned rows
+    ::close(fd);                         // the mappings keep the memory
+    std::lock_guard<std::mutex> lk(ring_mu_);
+    rings_[va] = owned + 2 * halo;
+    return va;  // memfd pages start zeroed
   }
   std::string name() const override {
     return std::string(drift_ ? "cpu [drift]" : "cpu") + (resident_ ? " [resident]" : "");
@@ -110,8 +153,19 @@ class CpuBackend final : public Backend {
     GOL_REQUIRE(p, "host allocation of " + std::to_string(bytes) + " bytes failed");
     return p;
   }
-  void release(void* p) override { std::free(p); }
-  void* alloc_host(size_t bytes) override { return alloc(bytes); }
+  void release(void* p) override {
+    {
+      std::lock_guard<std::mutex> lk(ring_mu_);
+      auto it = rings_.find(p);
+      if (it != rings_.end()) {
+        ::munmap(it->first, it->second);
+        rings_.erase(it);
+        return;
+      }
+    }
+    std::free(p);
+  }
+  void* alloc_host(size_t bytes) override { return std::calloc(bytes ? bytes : 1, 1); }
   void release_host(void* p) override { std::free(p); }
   void memset_async(void* p, int v, size_t bytes) override { std::memset(p, v, bytes); }
   void copy_h2d(void* d, const void* s, size_t n) override { std::memcpy(d, s, n); }
@@ -166,6 +220,9 @@ class CpuBackend final : public Backend {
   ThreadPool pool_;
   bool drift_ = false;
   bool resident_ = false;  // GOL_CPU_RESIDENT
+  bool ring_ = false;      // GOL_CPU_RING
+  std::mutex ring_mu_;
+  std::map<void*, size_t> rings_;  // row rings: base -> mapped bytes
 };
 
 int CpuBackend::run_block(const BlockArgs& a) {

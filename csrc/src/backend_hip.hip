@@ -68,6 +68,7 @@ class HipBackend final : public Backend {
     GOL_REQUIRE(n > 0, "no HIP device available");
     GOL_REQUIRE(device >= 0 && device < n, "HIP device index out of range");
     check_dev_ = env_int("GOL_CHECK_DEVICE", 0) != 0;
+    ring_on_ = env_int("GOL_ROW_RING", 1) != 0;
     GOL_ON_DEVICE();
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     hipDeviceProp_t prop;
@@ -94,6 +95,7 @@ class HipBackend final : public Backend {
                 "GOL_LDS_T must be 1, 2, 4 or 8 (16 or 32 with the packed tile, GOL_LDS_PACK=1)");
     tune_.split = env_int("GOL_SPLIT", 0);  // measured slower so far (profiles/)
     tune_.group = env_int("GOL_GROUP", 8);  // grouped schedule (life_group_impl.hpp)
+    tune_.group_small = std::getenv("GOL_GROUP") ? tune_.group : env_int("GOL_GROUP_SMALL", 4);
     // Short-segment groups (life_short_impl.hpp): exact, but 10-20 % slower
     // than the grouped kernel on the per-rank tile (profiles/sweep_short_segments.jsonl).
     tune_.short_seg = env_int("GOL_SHORT", 0);
@@ -180,6 +182,8 @@ class HipBackend final : public Backend {
       --live_backends()[dev_];
     }
     DeviceScope device_scope(dev_);
+    if (stream_) hipStreamSynchronize(stream_);
+    for (auto& kv : rings_) release_ring(kv.second);
     if (link_.stream[1]) hipStreamSynchronize(link_.stream[1]);
     if (stream_) hipStreamSynchronize(stream_);
     if (comm_) hipStreamSynchronize(comm_);
@@ -241,7 +245,88 @@ class HipBackend final : public Backend {
     join_streams();
     DeviceScope device_scope(dev_);
     hipStreamSynchronize(stream_);
+    auto it = rings_.find(p);
+    if (it != rings_.end()) {
+      release_ring(it->second);
+      rings_.erase(it);
+      return;
+    }
     hipFree(p);
+  }
+  // Row ring (Backend::row_ring_halo): three physical allocations A (first
+  // Dv owned rows), B (the rest but the last Dv), C (last Dv), mapped as
+  //   [C | A B C | A]
+  // into one reserved virtual range (hipMemMap takes offset 0 only, so every
+  // piece is a handle of its own).  The top halo is then the last owned rows
+  // and the bottom halo the first ones: the single-rank torus never fills its
+  // periodic row halos, and every temporal block runs over exactly the owned
+  // rows (no trapezoid).  A kernel reads one buffer and writes the other, so
+  // no launch reads an alias of what it writes.  GOL_ROW_RING=0: off.
+  size_t ring_granularity() const {
+    if (ring_gran_ == 0) {
+      hipMemAllocationProp prop{};
+      prop.type = hipMemAllocationTypePinned;
+      prop.location.type = hipMemLocationTypeDevice;
+      prop.location.id = dev_;
+      size_t g = 0;
+      if (hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityMinimum) != hipSuccess || g == 0) {
+        (void)hipGetLastError();
+        g = size_t(-1);  // unsupported
+      }
+      ring_gran_ = g;
+    }
+    return ring_gran_;
+  }
+  int row_ring_halo(int64_t H, int64_t pitch, int min_halo) const override {
+    if (!ring_on_) return 0;
+    const size_t gran = ring_granularity();
+    if (gran == size_t(-1) || pitch <= 0) return 0;
+    int64_t dv = std::max<int64_t>(1, min_halo);
+    while ((dv * pitch) % int64_t(gran) != 0) {
+      if (++dv > H) return 0;
+    }
+    if ((H * pitch) % int64_t(gran) != 0 || H < 2 * dv) return 0;
+    return int(dv);
+  }
+  void* alloc_row_ring(const TileGeom& g) override {
+    if (!ring_on_) return nullptr;
+    join_streams();
+    GOL_ON_DEVICE();
+    const size_t halo = size_t(g.Dv) * size_t(g.pitch), owned = size_t(g.H) * size_t(g.pitch);
+    const size_t gran = ring_granularity();
+    GOL_REQUIRE(gran != size_t(-1) && halo % gran == 0 && owned % gran == 0 && owned >= 2 * halo && halo > 0,
+                "row ring: geometry does not fit the mapping granularity (Backend::row_ring_halo)");
+    Ring r;
+    r.bytes = owned + 2 * halo;
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev_;
+    const size_t sizes[3] = {halo, owned - 2 * halo, halo};
+    for (int i = 0; i < 3; ++i)
+      if (sizes[i]) HIP_CHECK(hipMemCreate(&r.h[i], sizes[i], &prop, 0));
+    HIP_CHECK(hipMemAddressReserve(&r.va, r.bytes, gran, nullptr, 0));
+    auto* b = static_cast<uint8_t*>(r.va);
+    // [C | A B C | A]
+    const struct {
+      size_t at;
+      int piece;
+    } maps[5] = {{0, 2}, {halo, 0}, {2 * halo, 1}, {owned, 2}, {owned + halo, 0}};
+    for (const auto& m : maps) {
+      if (!sizes[m.piece]) continue;
+      HIP_CHECK(hipMemMap(b + m.at, sizes[m.piece], 0, r.h[m.piece], 0));
+      r.mapped.push_back({b + m.at, sizes[m.piece]});
+    }
+    hipMemAccessDesc acc{};
+    acc.location.type = hipMemLocationTypeDevice;
+    acc.location.id = dev_;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    HIP_CHECK(hipMemSetAccess(r.va, r.bytes, &acc, 1));
+    HIP_CHECK(hipMemsetAsync(b + halo, 0, owned, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (check_dev_) check_ptr(b + halo, "row ring");
+    rings_[r.va] = r;
+    return r.va;
   }
   void* alloc_host(size_t bytes) override {
     GOL_ON_DEVICE();
@@ -847,6 +932,18 @@ class HipBackend final : public Backend {
   }
 
  private:
+  struct Ring {
+    void* va = nullptr;
+    size_t bytes = 0;
+    hipMemGenericAllocationHandle_t h[3] = {};
+    std::vector<std::pair<void*, size_t>> mapped;
+  };
+  void release_ring(Ring& r) {
+    for (auto& m : r.mapped) (void)hipMemUnmap(m.first, m.second);
+    (void)hipMemAddressFree(r.va, r.bytes);
+    for (auto h : r.h)
+      if (h) (void)hipMemRelease(h);
+  }
   // Default builds carry neither the measured-slower variants nor their
   // schedules (hipk::kExperimentalBuild): an environment asking for one fails
   // here, loudly, instead of silently running the default kernel.
@@ -900,6 +997,9 @@ class HipBackend final : public Backend {
 
   int dev_;
   bool check_dev_ = false;  // GOL_CHECK_DEVICE
+  bool ring_on_ = true;     // GOL_ROW_RING
+  mutable size_t ring_gran_ = 0;
+  std::map<void*, Ring> rings_;
   std::vector<hipEvent_t> timing_pool_;  // timing_mark() events
   hipStream_t stream_ = nullptr;
   std::string arch_;

@@ -272,6 +272,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property("generation", &Engine::generation, &Engine::set_generation)
       .def_property_readonly("drift", &Engine::drift)
       .def_property_readonly("drifting", &Engine::drifting)
+      .def_property_readonly("row_ring", &Engine::row_ring)
       .def_property_readonly("via_bits", &Engine::via_bits)
       .def_property_readonly("resident", &Engine::resident)
       .def("normalize", &Engine::normalize, py::call_guard<py::gil_scoped_release>())

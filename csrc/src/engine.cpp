@@ -113,13 +113,26 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // fill); else D cells per side, 2D on the left for the drifting window.
   int hw = cols_filled_ ? int(ceil_div(drift_ok_ ? 2 * int64_t(D_) : int64_t(D_), 32)) : 0;
   Extent r = rows(), c = cols();
+  // Row ring (Backend::row_ring_halo): a single-rank torus whose row halos
+  // are second mappings of its own owned rows.  Nothing is ever filled, and
+  // every temporal block runs over exactly the owned rows, so an epoch is one
+  // block (D = tmax, unless the configuration sets the epoch).
+  int ring_dv = 0;
+  if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !rows_wrapped_ && !resident_) {
+    const TileGeom probe = TileGeom::make(cl, r.size(), c.size(), 0, hw);
+    ring_dv = be_->row_ring_halo(probe.H, probe.pitch, tmax_);
+  }
   if (via_bits_) {
     // The byte tile is storage only (owned cells, no halos); the epochs run
     // on its bit-word image, which carries the halos.
     g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), 0, 0);
-    gb_ = TileGeom::make(Layout::Bits, r.size(), c.size(), D_, hw);
+    gb_ = TileGeom::make(Layout::Bits, r.size(), c.size(), ring_dv > 0 ? ring_dv : D_, hw);
   } else {
-    g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), D_, hw);
+    g_ = TileGeom::make(cfg_.layout, r.size(), c.size(), ring_dv > 0 ? ring_dv : D_, hw);
+  }
+  if (ring_dv > 0) {
+    rows_ring_ = true;
+    if (cfg_.epoch <= 0) D_ = tmax_;  // an epoch only paces the polls (and column fills) now
   }
   // Experiment knob: extra bytes per padded row (multiple of 256).
   if (const char* pad = std::getenv("GOL_PITCH_PAD")) g_.pitch += 256 * (std::max(0, std::atoi(pad)) / 256);
@@ -128,13 +141,26 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // two windows late.
   poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : (tr_->size() > 1 || cfg_.self_exchange) ? 512 : 256;
 
-  for (auto& b : buf_) b = be_->alloc(size_t(g_.bytes()));
+  if (rows_ring_ && !via_bits_) {
+    for (auto& b : buf_) {
+      b = be_->alloc_row_ring(g_);
+      GOL_REQUIRE(b, "row ring allocation failed");
+    }
+  } else {
+    for (auto& b : buf_) b = be_->alloc(size_t(g_.bytes()));
+  }
   if (via_bits_) {
     // The bit words live in the spare byte buffer (about an eighth of its
     // size per parity) unless a small tile's halo rows or pitch rounding do
-    // not leave room.
-    if (2 * gb_.bytes() > g_.bytes())
+    // not leave room, or they form a row ring.
+    if (rows_ring_) {
+      for (auto& b : bitbuf_) {
+        b = be_->alloc_row_ring(gb_);
+        GOL_REQUIRE(b, "row ring allocation failed");
+      }
+    } else if (2 * gb_.bytes() > g_.bytes()) {
       for (auto& b : bitbuf_) b = be_->alloc(size_t(gb_.bytes()));
+    }
   }
   alive_dev_ = static_cast<uint32_t*>(be_->alloc(64));
   if (dec_.Px > 1) {
@@ -327,6 +353,15 @@ void Engine::halo_exchange_on(void* buf, const TileGeom& g) {
     ++exchanges_;
     return;
   }
+  if (rows_ring_) {  // the row halos alias the owned rows; only column halos (if any) need a fill
+    if (cols_filled_) {
+      void* t = phase_begin(nullptr);
+      be_->fill_periodic(buf, g, /*cols=*/true, /*rows=*/false);
+      phase_end(kFill, t, nullptr);
+    }
+    ++exchanges_;
+    return;
+  }
   if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange) {  // one rank: both periodic fills, one launch
     void* t = phase_begin(nullptr);
     be_->fill_periodic(buf, g, /*cols=*/cols_filled_, /*rows=*/true);
@@ -445,9 +480,12 @@ void* Engine::bit_scratch(int i) const {
 void Engine::epoch_via_bits(int64_t d) {
   trace::Range tr("gol.epoch_via_bits");
   halo_exchange_on(bit_scratch(bpar_), gb_);
-  int64_t a = D_ - d;  // a partial epoch's trapezoid starts d rows outside the owned rows
+  // A partial epoch's trapezoid starts d rows outside the owned rows; a row
+  // ring's blocks all cover exactly the owned rows (a = Dv - T).
+  int64_t a = D_ - d;
   while (d > 0) {
     const int T = pick_T(d);
+    if (rows_ring_) a = gb_.Dv - T;
     add_drift(launch(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
     bpar_ ^= 1;
     gen_ += T;
@@ -500,6 +538,7 @@ void Engine::run_epoch(int64_t d) {
   int64_t a = D_ - d;
   while (d > 0) {
     const int T = pick_T(d);
+    if (rows_ring_) a = g_.Dv - T;  // every block covers exactly the owned rows
     if (d == T && early_ && send_next_ && full)
       last_block_early(T);
     else

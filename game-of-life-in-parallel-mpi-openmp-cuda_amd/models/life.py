@@ -199,6 +199,7 @@ class Simulation:
                 "overlap_trial_ms_plain": self._eng.trial_ms_plain,
                 "overlap_trial_ms_early": self._eng.trial_ms_early,
                 "u8_compute": ("bits" if self._eng.via_bits else "bytes") if self.config.resolved_layout() == "u8" else None,
+                "row_ring": bool(self._eng.row_ring),
                 "kernel": ("resident epochs, adder window (drifting frame)" if self._eng.resident
                            else "adder window (drifting frame)" if self._eng.drifting else "symmetric window")}
 

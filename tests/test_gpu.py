@@ -1013,3 +1013,54 @@ def test_resident_off_when_ranks_share_the_gpu(gpu, monkeypatch):
     grp.load(g)
     grp.parallel(lambda s: s.advance(300))
     assert (grp.gather() == life_step_torch(g, 300, device="cuda")).all()
+
+
+# ---- row ring (Backend::row_ring_halo, hipMemMap'd halos) -------------------
+
+@pytest.mark.parametrize("W,H", [(8192, 4096), (32768, 1024), (16384, 2048), (4096, 8192)])
+@pytest.mark.parametrize("layout", ["bits", "u8"])
+def test_row_ring_vs_torch(gpu, W, H, layout):
+    """Single-rank tiles whose row halos are second mappings of their own
+    owned rows (three physical pieces mapped [C | A B C | A]; B may be empty):
+    no fills, every block over exactly the owned rows.  Chunked runs with
+    read-outs (drift rotations) in between, against the fp32 oracle."""
+    g = random_grid(W, H, W // 32 + H)
+    sim = Simulation(LifeConfig(W, H, layout=layout, gen_limit=1000), engine="hip")
+    d = sim.describe()
+    assert d["row_ring"] is True, d
+    sim.load(g)
+    want = g
+    for n in (45, 100):
+        sim.advance(n)
+        want = life_step_torch(want, n, device="cuda")
+        assert (sim.tile() == want).all(), n
+    assert sim.last_report.exchanges > 0
+
+
+def test_row_ring_termination_and_off_switch(gpu, monkeypatch):
+    """Exact Generations through the ring: a block split by the wrap row is a
+    still life only if the halos alias correctly (reference: 2 generations);
+    a lone cell dies (1).  Same with the ring off."""
+    for ring in ("1", "0"):
+        monkeypatch.setenv("GOL_ROW_RING", ring)
+        for cells, want in (([(4095, 10), (4095, 11), (0, 10), (0, 11)], 2), ([(0, 8191)], 1)):
+            grid = np.zeros((4096, 8192), dtype=np.uint8)
+            for r, c in cells:
+                grid[r, c] = 1
+            sim = Simulation(LifeConfig(8192, 4096, poll_gens=16), engine="hip")
+            assert sim.describe()["row_ring"] is (ring == "1")
+            sim.load(grid)
+            rep = sim.run()
+            assert rep.generations == want, (ring, cells)
+            assert (sim.tile() == (grid if want == 2 else 0)).all(), (ring, cells)
+
+
+def test_row_ring_graphs(gpu):
+    W, H = 8192, 4096
+    g = random_grid(W, H, 77)
+    sim = Simulation(LifeConfig(W, H, gen_limit=400, graphs="on", check_similarity=False), engine="hip")
+    assert sim.describe()["row_ring"] is True and sim.native_engine.graphs()
+    sim.load(g)
+    sim.advance(200)
+    assert sim.last_report.graph_launches > 0
+    assert (sim.tile() == life_step_torch(g, 200, device="cuda")).all()
