@@ -431,9 +431,25 @@ __global__ __launch_bounds__(64 * kM) void life_resident_kernel(ResidentParams p
   }
 }
 
+// Every workgroup waits on its neighbours, so all of them must be resident at
+// once: a cooperative launch, which the runtime refuses (instead of letting
+// the waits time out) when the grid cannot be co-resident.  It does not fence
+// off kernels of other streams or processes (RCCL's, another rank's), which is
+// why the backend turns resident epochs off when ranks share the GPU and why
+// they are experimental.
 template <int RW>
 void launch_resident(const ResidentParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((life_resident_kernel<RW>), dim3(unsigned(p.nreg)), dim3(64 * kM), 0, s, p);
+  static const int per_cu = [] {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, life_resident_kernel<RW>, 64 * kM, 0) != hipSuccess) b = 0;
+    return b;
+  }();
+  GOL_REQUIRE(per_cu >= 1, "resident kernel: a workgroup does not fit a CU");
+  ResidentParams arg = p;
+  void* args[] = {&arg};
+  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&life_resident_kernel<RW>),
+                                                  dim3(unsigned(p.nreg)), dim3(64 * kM), args, 0, s);
+  GOL_REQUIRE(e == hipSuccess, std::string("resident kernel: cooperative launch refused: ") + hipGetErrorString(e));
 }
 
 }  // namespace lr

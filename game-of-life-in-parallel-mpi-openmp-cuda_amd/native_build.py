@@ -161,6 +161,31 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     return outs
 
 
+def compile_experimental(verbose: bool = False, jobs: int | None = None) -> int:
+    """Compile-check the experimental-only translation units (the measured-
+    slower variants and the resident kernel) with -DGOL_EXPERIMENTAL into
+    build/obj_exp, without linking or touching the default module; returns
+    how many were compiled.  __graft_entry__.build() runs it so every HIP
+    source in the tree is compiled for gfx950 each round."""
+    global EXPERIMENTAL, BUILD
+    saved = EXPERIMENTAL, BUILD
+    EXPERIMENTAL, BUILD = True, REPO / "build" / "obj_exp"
+    try:
+        BUILD.mkdir(parents=True, exist_ok=True)
+        srcs = [*[f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS], "kernels/life_resident.hip",
+                *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)], "kernels/life_block.hip",
+                "src/backend_hip.hip", "kernels/life_block_bits_w1_dpp.hip"]
+        objs = {s: BUILD / (s.replace("/", "_") + ".o") for s in srcs}
+        hdr = _headers_mtime()
+        todo = [s for s in srcs if _needs(objs[s], CSRC / s, hdr)]
+        with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
+            for f in [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]:
+                f.result()
+        return len(todo)
+    finally:
+        EXPERIMENTAL, BUILD = saved
+
+
 SELFTEST_MAIN = "tools/gol_selftest.cpp"
 SANITIZERS = {
     "address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
