@@ -200,8 +200,23 @@ class Simulation:
                 "overlap_trial_ms_early": self._eng.trial_ms_early,
                 "u8_compute": ("bits" if self._eng.via_bits else "bytes") if self.config.resolved_layout() == "u8" else None,
                 "row_ring": bool(self._eng.row_ring),
-                "kernel": ("resident epochs, adder window (drifting frame)" if self._eng.resident
-                           else "adder window (drifting frame)" if self._eng.drifting else "symmetric window")}
+                "kernel": self._kernel_name()}
+
+    def _kernel_name(self) -> str:
+        """What the temporal blocks run, for reports (bench.py config.kernel)."""
+        e = self._eng
+        lay = self.config.resolved_layout()
+        be = self.backend.name()
+        if lay == "u8" and not e.via_bits and "lds-tiled" in be:
+            return "LDS-tiled byte kernel (" + be.split("; u8 ")[-1].rstrip("]").strip() + ")"
+        window = ("adder window (drifting frame)" if e.drifting else "symmetric window") if not e.resident \
+            else "resident epochs, adder window (drifting frame)"
+        parts = [f"bit-sliced temporal blocks, T={e.tmax}", window]
+        if lay == "u8":
+            parts.append("byte grid packed to bit words once per run" if e.via_bits else "byte-layout kernels")
+        if e.row_ring:
+            parts.append("row ring (no halo fills)")
+        return ", ".join(parts)
 
     # -- state -----------------------------------------------------------
     def load(self, grid: np.ndarray) -> None:
