@@ -5,6 +5,7 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r04e}
 mkdir -p "$OUT"
+timeout -k 10 120 bin/ubench_vbody 3000 > "$OUT/ubench_vbody.txt" 2>&1 || exit $?
 J="$OUT/tile.jsonl"; : > "$J"
 run() { timeout -k 10 120 env "$@" >> "$J" 2>> "$OUT/err.log" || { echo "FAILED: $*" >> "$OUT/err.log"; return 1; }; }
 B="python bench.py --steps 10 --warmup 2 --verify 0 --no-phase-step"
