@@ -193,6 +193,34 @@ def compile_experimental(verbose: bool = False, jobs: int | None = None) -> int:
         EXPERIMENTAL, BUILD = saved
 
 
+def build_experimental_module(out: Path, verbose: bool = False, jobs: int | None = None) -> Path:
+    """The whole module in experimental mode, linked to `out` (not the default
+    module's path); load it with GOL_NATIVE_SO=<out> to run the experimental
+    GPU tests (pytest -m "gpu and experimental")."""
+    global EXPERIMENTAL, BUILD, HIP_SRCS
+    saved = EXPERIMENTAL, BUILD, HIP_SRCS
+    EXPERIMENTAL, BUILD = True, REPO / "build" / "obj_exp"
+    HIP_SRCS = HIP_SRCS + [f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS] + \
+        ["kernels/life_resident.hip", *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)]]
+    try:
+        BUILD.mkdir(parents=True, exist_ok=True)
+        srcs = HOST_SRCS + HIP_SRCS + BIND_SRCS
+        objs = {s: BUILD / (s.replace("/", "_") + ".o") for s in srcs}
+        hdr = _headers_mtime()
+        todo = [s for s in srcs if _needs(objs[s], CSRC / s, hdr)]
+        with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
+            for f in [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]:
+                f.result()
+        out = Path(out)
+        out.parent.mkdir(parents=True, exist_ok=True)
+        rocm_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx",
+                     f"-Wl,-rpath,{ROCM / 'lib'}", "-pthread"]
+        _run([_hipcc(), "-shared", "-fPIC", *[str(objs[s]) for s in srcs], "-o", str(out), *rocm_libs], verbose)
+        return out
+    finally:
+        EXPERIMENTAL, BUILD, HIP_SRCS = saved
+
+
 SELFTEST_MAIN = "tools/gol_selftest.cpp"
 SANITIZERS = {
     "address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],

@@ -24,3 +24,7 @@ P="--steps 5 --warmup 1 --verify 0 --no-phase-step"
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$OUT/prof_32768" -o run -- python3 bench.py $P > "$OUT/prof_32768.log" 2>&1 || exit 1
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$OUT/prof_8192_u8" -o run -- python3 bench.py $P --size 8192 --layout u8 > "$OUT/prof_8192_u8.log" 2>&1 || exit 1
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$OUT/prof_tile_rehearsal" -o run -- python3 bench.py $P --height 4096 --rehearse-rccl > "$OUT/prof_tile.log" 2>&1 || exit 1
+# The experimental build (variants measured slower, compiled out of the default
+# module) still exact: its GPU tests against the alternate module.
+GOL_NATIVE_SO=exp_so/_gol.so timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  -m "gpu and experimental" tests/test_gpu.py > "$OUT/experimental_tier.log" 2>&1 || exit $?

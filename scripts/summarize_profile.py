@@ -13,7 +13,37 @@ def short(name: str) -> str:
     return n[:110] if keep else n.split("(")[0][:90]
 
 
+def from_db(db_path: str) -> None:
+    """rocprofv3 >= 7 writes a rocpd SQLite database (run_results.db): kernel
+    time per kernel, and the device's busy share of the traced span."""
+    import sqlite3  # noqa: PLC0415
+
+    cur = sqlite3.connect(db_path).cursor()
+    rows = cur.execute("select name, count(*), sum(duration), avg(duration) from kernels group by name "
+                       "order by sum(duration) desc").fetchall()
+    tot = sum(r[2] for r in rows) or 1
+    print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
+    print("| kernel | calls | total ms | avg us | % |")
+    print("|---|---:|---:|---:|---:|")
+    for name, n, s_ns, a_ns in rows:
+        print(f"| `{short(name)}` | {n} | {s_ns / 1e6:.3f} | {a_ns / 1e3:.2f} | {100.0 * s_ns / tot:.2f} |")
+    ks = cur.execute("select start, end from kernels order by start").fetchall()
+    if ks:
+        busy, end = 0, ks[0][0]
+        for a, b in ks:  # union of kernel intervals
+            if b > end:
+                busy += b - max(a, end)
+                end = b
+        span = ks[-1][1] - ks[0][0]
+        print(f"\nDevice busy {100.0 * busy / span:.1f} % of the traced span ({span / 1e6:.2f} ms, "
+              f"{len(ks)} dispatches).\n")
+
+
 def main(d: str) -> None:
+    db = os.path.join(d, "run_results.db")
+    if os.path.exists(db):
+        from_db(db)
+        return
     stats = os.path.join(d, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
         rows = list(csv.DictReader(open(stats)))

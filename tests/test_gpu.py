@@ -779,6 +779,7 @@ def test_linked_launches_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
     rows through per-group completion words; against the fp32 conv oracle,
     with several epochs, the drifting adder window and partial epochs."""
     monkeypatch.setenv("GOL_LINK", "1")
+    monkeypatch.setenv("GOL_ROW_RING", "0")  # ring epochs are single blocks: nothing to link
     monkeypatch.setenv("GOL_XLANE", str(xlane))
     g = random_grid(W, H, W + 3 * H + tmax)
     gens = 10 * tmax + 7
@@ -792,6 +793,7 @@ def test_linked_launches_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
 
 @experimental
 def test_linked_launches_termination_and_subdomains(gpu, monkeypatch):
+    monkeypatch.setenv("GOL_ROW_RING", "0")
     monkeypatch.setenv("GOL_LINK", "1")
     grid = np.zeros((1024, 2048), dtype=np.uint8)
     W, H, seed, density = CONVERGING[5]
