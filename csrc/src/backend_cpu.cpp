@@ -18,6 +18,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "gol/backend.hpp"
@@ -96,6 +97,7 @@ class CpuBackend final : public Backend {
     resident_ = r && *r && *r != '0';
     const char* ring = std::getenv("GOL_CPU_RING");
     ring_ = ring && *ring && *ring != '0';
+    ring_fail_ = ring && std::string(ring) == "fail";  // tests: the mapping fails after the size check
   }
   ~CpuBackend() override {
     for (auto& kv : rings_) ::munmap(kv.first, kv.second);
@@ -112,7 +114,7 @@ class CpuBackend final : public Backend {
     return int(dv);
   }
   void* alloc_row_ring(const TileGeom& g) override {
-    if (!ring_) return nullptr;
+    if (!ring_ || ring_fail_) return nullptr;
     const size_t halo = size_t(g.Dv) * size_t(g.pitch), owned = size_t(g.H) * size_t(g.pitch);
     const int fd = ::memfd_create("gol_row_ring", 0);
     GOL_REQUIRE(fd >= 0, std::string("row ring: memfd_create failed: ") + std::strerror(errno));
@@ -221,6 +223,7 @@ class CpuBackend final : public Backend {
   bool drift_ = false;
   bool resident_ = false;  // GOL_CPU_RESIDENT
   bool ring_ = false;      // GOL_CPU_RING
+  bool ring_fail_ = false;  // GOL_CPU_RING=fail
   std::mutex ring_mu_;
   std::map<void*, size_t> rings_;  // row rings: base -> mapped bytes
 };

@@ -1,6 +1,7 @@
 #include "gol/engine.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -117,10 +118,30 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // are second mappings of its own owned rows.  Nothing is ever filled, and
   // every temporal block runs over exactly the owned rows, so an epoch is one
   // block (D = tmax, unless the configuration sets the epoch).
+  // The rings are allocated here, before any geometry is committed: if the
+  // backend cannot build them after all (address space, driver), the tile
+  // falls back to plain buffers with periodic fills.
   int ring_dv = 0;
-  if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !rows_wrapped_ && !resident_) {
+  void* ring_bufs[2] = {nullptr, nullptr};
+  if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !rows_wrapped_ && !resident_ &&
+      !std::getenv("GOL_PITCH_PAD")) {
     const TileGeom probe = TileGeom::make(cl, r.size(), c.size(), 0, hw);
     ring_dv = be_->row_ring_halo(probe.H, probe.pitch, tmax_);
+    if (ring_dv > 0) {
+      const TileGeom gr = TileGeom::make(cl, r.size(), c.size(), ring_dv, hw);
+      try {
+        for (auto& b : ring_bufs) {
+          b = be_->alloc_row_ring(gr);
+          GOL_REQUIRE(b, "the backend returned no ring");
+        }
+      } catch (const std::exception& e) {
+        for (auto& b : ring_bufs)
+          if (b) be_->release(b);
+        ring_bufs[0] = ring_bufs[1] = nullptr;
+        ring_dv = 0;
+        std::fprintf(stderr, "gol: row ring unavailable (%s); periodic row fills instead\n", e.what());
+      }
+    }
   }
   if (via_bits_) {
     // The byte tile is storage only (owned cells, no halos); the epochs run
@@ -142,10 +163,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : (tr_->size() > 1 || cfg_.self_exchange) ? 512 : 256;
 
   if (rows_ring_ && !via_bits_) {
-    for (auto& b : buf_) {
-      b = be_->alloc_row_ring(g_);
-      GOL_REQUIRE(b, "row ring allocation failed");
-    }
+    for (int i = 0; i < 2; ++i) buf_[i] = ring_bufs[i];
   } else {
     for (auto& b : buf_) b = be_->alloc(size_t(g_.bytes()));
   }
@@ -154,10 +172,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     // size per parity) unless a small tile's halo rows or pitch rounding do
     // not leave room, or they form a row ring.
     if (rows_ring_) {
-      for (auto& b : bitbuf_) {
-        b = be_->alloc_row_ring(gb_);
-        GOL_REQUIRE(b, "row ring allocation failed");
-      }
+      for (int i = 0; i < 2; ++i) bitbuf_[i] = ring_bufs[i];
     } else if (2 * gb_.bytes() > g_.bytes()) {
       for (auto& b : bitbuf_) b = be_->alloc(size_t(gb_.bytes()));
     }

@@ -92,3 +92,16 @@ def test_ring_halo_rows_alias_owned_rows(native):
     assert (a[:Dv] == a[H:H + Dv]).all()          # top halo == last Dv owned rows
     assert (a[Dv + H:] == a[Dv:2 * Dv]).all()     # bottom halo == first Dv owned rows
     assert not (a[Dv:Dv + H] == 0).all()
+
+
+def test_ring_allocation_failure_falls_back_to_fills(native, monkeypatch, capfd):
+    """A backend that promises a ring but cannot map it (GOL_CPU_RING=fail):
+    the engine warns, allocates plain buffers and fills the row halos."""
+    monkeypatch.setenv("GOL_CPU_RING", "fail")
+    sim = _sim(128, 64, tmax=4, gen_limit=100)
+    assert sim.describe()["row_ring"] is False
+    assert "row ring unavailable" in capfd.readouterr().err
+    g = random_grid(128, 64, 3)
+    sim.load(g)
+    sim.advance(50)
+    assert (sim.tile() == life_step_numpy(g, 50)).all()
