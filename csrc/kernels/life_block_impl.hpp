@@ -221,18 +221,52 @@ __device__ __forceinline__ void adder_window(uint32_t c, uint32_t& l1, uint32_t&
       : "scc");
 }
 
+// The adder window for two words per lane (w0 = cells 0..31, w1 = cells
+// 32..63 of the lane's 64): w1's left neighbour is the lane's own w0, so only
+// w0 needs a lane-shifted carry.  6 VALU + 2 SALU for two words instead of
+// 8 + 4: the carry out of (w0 << 1 | cin) is w0's top bit, which is exactly
+// w1's carry in.
+__device__ __forceinline__ void adder_window2(uint32_t w0, uint32_t w1, uint32_t& a0, uint32_t& a1, uint32_t& b0,
+                                              uint32_t& b1) {
+  uint32_t t1, t2;
+  uint64_t m1, m0, m3, m2, mz;
+  asm("v_add_co_u32_e64 %[t1], %[m1], %[w1], %[w1]\n\t"          // m1 = top bits of w1
+      "s_lshl_b64 %[m1], %[m1], 1\n\t"                           // lane j <- lane j-1
+      "v_addc_co_u32_e64 %[a0], %[m0], %[w0], %[w0], %[m1]\n\t"  // a0 = x-1 of w0; m0 = top bits of w0
+      "v_addc_co_u32_e64 %[a1], %[mz], %[w1], %[w1], %[m0]\n\t"  // a1 = x-1 of w1
+      "v_add_co_u32_e64 %[t2], %[m3], %[a1], %[a1]\n\t"          // m3 = top bits of a1
+      "s_lshl_b64 %[m3], %[m3], 1\n\t"
+      "v_addc_co_u32_e64 %[b0], %[m2], %[a0], %[a0], %[m3]\n\t"  // b0 = x-2 of w0
+      "v_addc_co_u32_e64 %[b1], %[mz], %[a1], %[a1], %[m2]"        // b1 = x-2 of w1
+      : [a0] "=&v"(a0), [a1] "=&v"(a1), [b0] "=&v"(b0), [b1] "=&v"(b1), [t1] "=&v"(t1), [t2] "=&v"(t2),
+        [m1] "=&s"(m1), [m0] "=&s"(m0), [m3] "=&s"(m3), [m2] "=&s"(m2), [mz] "=&s"(mz)
+      : [w0] "v"(w0), [w1] "v"(w1)
+      : "scc");
+}
+
 // Horizontal 3-sums (h1:h0) = left + centre + right for every word, and the
 // word of the cells the rule treats as centre (the input word itself, or for
 // the one-sided adder window the word shifted by one cell, ctr = x-1).
 template <int XL, int W>
 __device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1, Vec<W>& ctr) {
   if constexpr (XL == kXlaneAdd) {
-    static_assert(W == 1, "adder window: one word per lane");
-    uint32_t l1, l2;
-    adder_window(c.w[0], l1, l2);
-    h0.w[0] = bop3<tt::XOR3>(l2, l1, c.w[0]);
-    h1.w[0] = bop3<tt::MAJ>(l2, l1, c.w[0]);
-    ctr.w[0] = l1;
+    static_assert(W == 1 || W == 2, "adder window: one or two words per lane");
+    if constexpr (W == 1) {
+      uint32_t l1, l2;
+      adder_window(c.w[0], l1, l2);
+      h0.w[0] = bop3<tt::XOR3>(l2, l1, c.w[0]);
+      h1.w[0] = bop3<tt::MAJ>(l2, l1, c.w[0]);
+      ctr.w[0] = l1;
+    } else {
+      uint32_t a0, a1, b0, b1;
+      adder_window2(c.w[0], c.w[1], a0, a1, b0, b1);
+      h0.w[0] = bop3<tt::XOR3>(b0, a0, c.w[0]);
+      h1.w[0] = bop3<tt::MAJ>(b0, a0, c.w[0]);
+      h0.w[1] = bop3<tt::XOR3>(b1, a1, c.w[1]);
+      h1.w[1] = bop3<tt::MAJ>(b1, a1, c.w[1]);
+      ctr.w[0] = a0;
+      ctr.w[1] = a1;
+    }
     return;
   }
   ctr = c;
