@@ -360,15 +360,18 @@ void Engine::halo_exchange() { halo_exchange_on(buf_[cur_], g_); }
 
 void Engine::halo_exchange_on(void* buf, const TileGeom& g) {
   trace::Range tr("gol.halo_exchange");
-  be_->join_streams();  // transports enqueue on the compute stream directly
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
   const int64_t H = g.H, pitch = g.pitch;
-  if (rows_wrapped_) {  // the kernels read the torus modulo its rows and columns
+  if (rows_wrapped_ || (rows_ring_ && !cols_filled_)) {
+    // Nothing to move: the kernels read the torus modulo its rows, or the
+    // row halos alias the owned rows.  No stream join either, so linked
+    // launches (GOL_LINK) chain across such epochs.
     ++exchanges_;
     return;
   }
-  if (rows_ring_) {  // the row halos alias the owned rows; only column halos (if any) need a fill
+  be_->join_streams();  // transports enqueue on the compute stream directly
+  if (rows_ring_) {  // the row halos alias the owned rows; only column halos need a fill
     if (cols_filled_) {
       void* t = phase_begin(nullptr);
       be_->fill_periodic(buf, g, /*cols=*/true, /*rows=*/false);
