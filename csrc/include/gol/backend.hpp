@@ -131,6 +131,7 @@ class Backend {
   struct KernelChoice {
     int tmax = 16;
     bool drift = false;
+    bool link = false;  // consecutive blocks may run linked (BlockArgs::link)
   };
   virtual KernelChoice choose_kernel(Layout l, int64_t /*rows*/, int64_t /*cols*/, int tmax_req) const {
     return {tmax_req > 0 ? tmax_req : preferred_tmax(l), drifts(l)};

@@ -287,6 +287,7 @@ class Engine {
   bool cols_filled_ = true; // column halos kept valid by fills (false: the backend wraps column reads)
   bool rows_wrapped_ = false; // single-rank torus read modulo its rows (no fills at all)
   bool rows_ring_ = false;    // row halos are second mappings of the owned rows (Backend::row_ring_halo)
+  bool link_ = false;         // blocks may run linked (Backend::KernelChoice::link; ring tiles only)
   bool via_bits_ = false;    // byte layout computed on bit words (epoch_via_bits)
   bool resident_ = false;    // one launch per epoch, tile resident in registers (Backend::resident_epoch)
   TileGeom gb_;              // the tile in the bit layout (same rows, halos, words)

@@ -97,6 +97,10 @@ struct BlockArgs {
   // The engine runs resident epochs (Backend::resident_epoch): any T, one
   // launch that keeps the tile in the register file.
   bool resident = false;
+  // The backend may link this launch to the previous one (run both at once,
+  // ordered by per-group completion words): Backend::KernelChoice::link, on
+  // a single-rank ring tile whose epochs move no data between launches.
+  bool link = false;
 };
 
 }  // namespace gol

@@ -14,7 +14,7 @@
 #include "life_pipe_impl.hpp"
 #ifdef GOL_EXPERIMENTAL
 // Measured-slower schedules (docs/PERFORMANCE.md): short segments, bit-layout
-// level-pipelined pairs, linked launches, the split and skewed schedules are
+// level-pipelined pairs, the split and skewed schedules are
 // compiled only into experimental builds (GOL_EXPERIMENTAL=1 native_build);
 // the default build keeps the grouped / chained / classic kernels and the
 // byte layout's T = 48 pipelined pass.
@@ -37,7 +37,6 @@ constexpr int kSplitMaxRowsPerT = 8;
 // stream, after an event recorded just before the previous launch (so it
 // starts no earlier than that one), and waits for its input rows group by
 // group.
-#ifdef GOL_EXPERIMENTAL
 template <int T, class IO>
 bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const LifeTuning& tune, hipStream_t s) {
   using LIO = Sc1IO<IO>;
@@ -93,7 +92,6 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   L.prev_valid = true;
   return true;
 }
-#endif  // GOL_EXPERIMENTAL
 
 template <int T, class IO>
 void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
@@ -124,13 +122,11 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
   // tiles, whose launches alone hold 2 waves per SIMD).  Any other launch
   // first joins the two streams.
   if (tune.link) {
-#ifdef GOL_EXPERIMENTAL
     if constexpr (IO::kBits && IO::W == 1 && (T == 8 || T == 12 || T == 16) &&
                   (IO::XL == kXlaneDpp || IO::XL == kXlaneAdd)) {
       if (tune.group != 0 && tune.split == 0 && !tune.skew && dual == 1 && launch_linked<T, IO>(p, out_rows, simds, tune, s))
         return;
     }
-#endif
     link_join(*tune.link);
   }
   if constexpr (T >= 4) {

@@ -122,8 +122,11 @@ class HipBackend final : public Backend {
     // Linked launches: consecutive grouped launches of an epoch overlap on
     // two streams, ordered by per-group completion words (LifeBlockParams::
     // link_*): small tiles whose launches alone hold only 2 waves per SIMD.
-    link_on_ = env_int("GOL_LINK", 0) != 0;
-    if (link_on_) {
+    // GOL_LINK: 1 every eligible launch, 0 never, -1 (default) where the
+    // engine passes KernelChoice::link (small single-rank ring tiles).
+    link_mode_ = env_int("GOL_LINK", -1);
+    link_on_ = link_mode_ > 0;
+    if (link_mode_ != 0) {
       link_.stream[0] = stream_;
       HIP_CHECK(hipStreamCreateWithFlags(&link_.stream[1], hipStreamNonBlocking));
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -210,7 +213,7 @@ class HipBackend final : public Backend {
   // Linked launches: everything on the second stream precedes what comes
   // next on the compute stream (every entry point but a linkable run_block).
   void join_streams() override {
-    if (link_on_) {
+    if (link_.stream[1]) {
       DeviceScope device_scope(dev_);
       hipk::link_join(link_);
     }
@@ -520,7 +523,8 @@ class HipBackend final : public Backend {
     const bool capturing = hipStreamIsCapturing(stream_, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
     // A launch may join a linked chain only on the compute stream, outside a
     // capture, for one row range of the bit layout; anything else first joins.
-    const bool linkable = link_on_ && !a.stream && !capturing && a.dual_offset == 0 && a.g.layout == Layout::Bits;
+    const bool linkable = (link_on_ || (a.link && link_mode_ < 0)) && link_.stream[1] && !a.stream && !capturing &&
+                          a.dual_offset == 0 && a.g.layout == Layout::Bits;
     if (!linkable) join_streams();
     tune_.link = linkable ? &link_ : nullptr;
     if (chain_mode_) {  // chained groups: own stream only, never inside a graph capture
@@ -742,6 +746,12 @@ class HipBackend final : public Backend {
         k.tmax = t;
         if (strips * (rows / (2 * t)) >= int64_t(8) * cus_) break;
       }
+      // Such tiles also link consecutive launches where each holds at least
+      // 1.5 waves per SIMD: two launches then fill the SIMDs together (8192^2
+      // 1.93 -> 1.75 ms per 1000 generations; 4096^2, with 0.75 waves per
+      // SIMD, and 4-wave-per-SIMD tiles measured slower linked;
+      // profiles/r04/linked_launches_ring.jsonl).
+      k.link = k.tmax < 16 && strips * (rows / (2 * k.tmax)) >= int64_t(6) * cus_;
     }
     return k;
   }
@@ -953,7 +963,7 @@ class HipBackend final : public Backend {
       int dflt;
     };
     static const Knob knobs[] = {{"GOL_WPL", 1},  {"GOL_SKEW", 0},     {"GOL_SPLIT", 0}, {"GOL_SHORT", 0},
-                                 {"GOL_PIPE", 0}, {"GOL_LINK", 0},     {"GOL_RESIDENT", 0},
+                                 {"GOL_PIPE", 0}, {"GOL_RESIDENT", 0},
                                  {"GOL_LDS_ADD", 0}};
     for (const Knob& k : knobs)
       if (env_int(k.name, k.dflt) != k.dflt)
@@ -1017,7 +1027,8 @@ class HipBackend final : public Backend {
   int64_t resident_launches_ = 0, res_trace_at_ = -1;
   std::string res_trace_path_;
   hipk::LinkState link_;  // linked launches (GOL_LINK)
-  bool link_on_ = false;
+  bool link_on_ = false;  // every eligible launch (GOL_LINK=1)
+  int link_mode_ = -1;
   uint32_t chain_seq_ = 0;
   bool u8_pipe_ = true;  // GOL_U8_PIPE: T = 48 / 64 byte passes
   int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, 2 timing probe, -1 autotuned per launch shape

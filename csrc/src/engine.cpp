@@ -153,6 +153,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   }
   if (ring_dv > 0) {
     rows_ring_ = true;
+    link_ = kc.link && !cols_filled_;  // epochs move no data: consecutive blocks may run linked
     if (cfg_.epoch <= 0) D_ = tmax_;  // an epoch only paces the polls (and column fills) now
   }
   // Experiment knob: extra bytes per padded row (multiple of 256).
@@ -668,6 +669,7 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   a.wrap_rows = rows_wrapped_;
   a.stream = stream;
   a.resident = resident_;
+  a.link = link_;
   a.dual_offset = dual_offset;
   a.prio_boost = prio_boost;
   void* t = phase_begin(stream);

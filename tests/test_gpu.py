@@ -770,7 +770,6 @@ def test_pipelined_byte_pass_t48_termination_and_ranks(gpu):
     assert (grp.gather() == want).all()
 
 
-@experimental
 @pytest.mark.parametrize("W,H", [(32768, 1024), (4096, 700), (2048 * 3, 333), (32 * 100, 1000)])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (0, 8), (3, 12), (0, 12)])
 def test_linked_launches_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
@@ -791,7 +790,6 @@ def test_linked_launches_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
     assert rep.linked_launches > 0
 
 
-@experimental
 def test_linked_launches_termination_and_subdomains(gpu, monkeypatch):
     monkeypatch.setenv("GOL_ROW_RING", "0")
     monkeypatch.setenv("GOL_LINK", "1")
@@ -1067,3 +1065,19 @@ def test_row_ring_graphs(gpu):
     sim.advance(200)
     assert sim.last_report.graph_launches > 0
     assert (sim.tile() == life_step_torch(g, 200, device="cuda")).all()
+
+
+def test_small_ring_tiles_link_launches_by_default(gpu):
+    """Small single-rank ring tiles (the small-tile T rule, >= 1.5 waves per
+    SIMD per launch) run consecutive blocks linked by default
+    (KernelChoice::link): exact against the fp32 oracle, bits and u8."""
+    W = H = 8192
+    g = random_grid(W, H, 88)
+    want = life_step_torch(g, 200, device="cuda")
+    for layout in ("bits", "u8"):
+        sim = Simulation(LifeConfig(W, H, layout=layout, gen_limit=1000), engine="hip")
+        assert sim.describe()["row_ring"] is True and sim.describe()["tmax"] == 8
+        sim.load(g)
+        rep = sim.advance(200)
+        assert rep.linked_launches > 0, layout
+        assert (sim.tile() == want).all(), layout
