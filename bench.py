@@ -137,8 +137,11 @@ def check_ranks(world: int, shared: bool, comm_count: int, infos: list[dict]) ->
     if len(infos) != world or sorted(i["rank"] for i in infos) != list(range(world)):
         return f"{len(infos)} of {world} ranks reported their device"
     if not shared:
-        buses = [i["pci_bus_id"] for i in infos if i.get("pci_bus_id")]
-        dup = sorted({b for b in buses if buses.count(b) > 1})
+        # One logical device per rank: (host, PCI bus id, device ordinal).  The
+        # ordinal is part of the key so that partitions of one physical GPU
+        # (which may share a bus id) still count as distinct devices.
+        keys = [(i.get("host"), i["pci_bus_id"], i.get("device")) for i in infos if i.get("pci_bus_id")]
+        dup = sorted({k[1] for k in keys if keys.count(k) > 1})
         if dup:
             return f"ranks share GPU(s) {dup} without --share-gpus: n_gpus would overstate the GPUs used"
     return None

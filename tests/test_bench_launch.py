@@ -93,13 +93,16 @@ def test_bench_check_ranks_refuses_what_rccl_did_not_see():
     (rccl_nranks != WORLD_SIZE, a rank missing, two ranks on one physical GPU
     without --share-gpus)."""
     b = _bench_module()
-    infos = [{"rank": r, "pci_bus_id": f"0000:{r + 5:02x}:00.0"} for r in range(8)]
+    infos = [{"rank": r, "host": "n0", "device": r, "pci_bus_id": f"0000:{r + 5:02x}:00.0"} for r in range(8)]
     assert b.check_ranks(8, False, 8, infos) is None
     assert "7 ranks" in b.check_ranks(8, False, 7, infos)
     assert "7 of 8" in b.check_ranks(8, False, 8, infos[:7])
-    same = [dict(i, pci_bus_id="0000:05:00.0") for i in infos]
+    same = [dict(i, pci_bus_id="0000:05:00.0", device=0) for i in infos]  # eight ranks on one device
     assert "share GPU" in b.check_ranks(8, False, 8, same)
     assert b.check_ranks(8, True, 8, same) is None  # --share-gpus: a declared rehearsal
+    # Partitions of one physical GPU may share a bus id but are distinct devices.
+    parts = [dict(i, pci_bus_id="0000:05:00.0") for i in infos]
+    assert b.check_ranks(8, False, 8, parts) is None
 
 
 def test_bench_refuses_a_launcher_with_another_world_size(native):
