@@ -1067,10 +1067,12 @@ def test_row_ring_graphs(gpu):
     assert (sim.tile() == life_step_torch(g, 200, device="cuda")).all()
 
 
-def test_small_ring_tiles_link_launches_by_default(gpu):
+def test_small_ring_tiles_link_launches_by_default(gpu, monkeypatch):
     """Small single-rank ring tiles (the small-tile T rule, >= 1.5 waves per
     SIMD per launch) run consecutive blocks linked by default
-    (KernelChoice::link): exact against the fp32 oracle, bits and u8."""
+    (KernelChoice::link): exact against the fp32 oracle, bits and u8 (the
+    GPU default for bytes: computed on bit words)."""
+    monkeypatch.delenv("GOL_U8_VIA_BITS", raising=False)
     W = H = 8192
     g = random_grid(W, H, 88)
     want = life_step_torch(g, 200, device="cuda")
