@@ -404,6 +404,8 @@ def main() -> int:
                 "exchanges_per_step": rs[-1].exchanges if rs else 0,
                 "polls_per_step": rs[-1].polls if rs else 0,
                 "kernel_launches_per_step": rs[-1].kernel_launches if rs else 0,
+                "linked_launches_per_step": rs[-1].linked_launches if rs else 0,
+                "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith("GOL_")},
                 "halo_bytes_per_step": rs[-1].halo_bytes if rs else 0,
                 "overlapped_halo_exchange": bool(rs and rs[-1].overlapped),
                 "overlap_mode": desc["overlap_mode"],
