@@ -197,6 +197,9 @@ __device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int 
 #ifndef GOL_ADDER_NOP
 #define GOL_ADDER_NOP 0
 #endif
+#ifndef GOL_ADDER_DPP
+#define GOL_ADDER_DPP 0
+#endif
 __device__ __forceinline__ void adder_window(uint32_t c, uint32_t& l1, uint32_t& l2) {
   // One block so the pair of lane masks never outlives the window (no SGPR
   // pressure across levels).  gfx950 wants a wait state between the last
@@ -253,7 +256,15 @@ __device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1, Ve
     static_assert(W == 1 || W == 2, "adder window: one or two words per lane");
     if constexpr (W == 1) {
       uint32_t l1, l2;
+#if GOL_ADDER_DPP
+      // Experiment: the same one-sided window from one DPP lane shift and
+      // two funnel shifts (3 half-rate VALU ops instead of the 4 carry ops).
+      const uint32_t lw = __builtin_amdgcn_mov_dpp(c.w[0], 0x138, 0xF, 0xF, true);  // wave_shr:1
+      l1 = __builtin_amdgcn_alignbit(c.w[0], lw, 31);
+      l2 = __builtin_amdgcn_alignbit(c.w[0], lw, 30);
+#else
       adder_window(c.w[0], l1, l2);
+#endif
       h0.w[0] = bop3<tt::XOR3>(l2, l1, c.w[0]);
       h1.w[0] = bop3<tt::MAJ>(l2, l1, c.w[0]);
       ctr.w[0] = l1;

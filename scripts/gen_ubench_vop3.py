@@ -53,6 +53,24 @@ VARIANTS = [
     ("v_addc_co_u32_e64 (sgpr carry in/out)",
      lambda i: f"v_addc_co_u32_e64 {dst(i)}, s[42:43], {v(i % 16)}, {v((i + 1) % 16)}, s[44:45]"),
     ("v_add_u32 (VOP2)", lambda i: f"v_add_u32 {dst(i)}, {v(i % 16)}, {v((i + 1) % 16)}"),
+    ("v_add_co_u32_e32 (vcc carry out)", lambda i: f"v_add_co_u32_e32 {dst(i)}, vcc, {v(i % 16)}, {v((i + 1) % 16)}"),
+    ("v_addc_co_u32_e32 (vcc in/out)", lambda i: f"v_addc_co_u32_e32 {dst(i)}, vcc, {v(i % 16)}, {v((i + 1) % 16)}, vcc"),
+    ("v_addc_co_u32_e32 (vcc in/out, src0 0)", lambda i: f"v_addc_co_u32_e32 {dst(i)}, vcc, 0, {v(i % 16)}, vcc"),
+    ("v_cmp_gt_i32_e32 (vcc)", lambda i: f"v_cmp_gt_i32_e32 vcc, 0, {v(i % 16)}"),
+    ("v_cmp_gt_i32_e64 (sgpr pair)", lambda i: f"v_cmp_gt_i32_e64 s[42:43], 0, {v(i % 16)}"),
+    ("v_cndmask_b32_e32 (vcc)", lambda i: f"v_cndmask_b32_e32 {dst(i)}, {v(i % 16)}, {v((i + 1) % 16)}, vcc"),
+    ("v_cndmask_b32_e64 (sgpr pair)", lambda i: f"v_cndmask_b32_e64 {dst(i)}, {v(i % 16)}, {v((i + 1) % 16)}, s[44:45]"),
+    ("v_lshlrev_b32_e32", lambda i: f"v_lshlrev_b32_e32 {dst(i)}, 1, {v(i % 16)}"),
+    ("v_lshrrev_b32_e32", lambda i: f"v_lshrrev_b32_e32 {dst(i)}, 31, {v(i % 16)}"),
+    ("v_lshl_or_b32 (VOP3 3 src)", lambda i: f"v_lshl_or_b32 {dst(i)}, {v(i % 16)}, 1, {v((i + 1) % 16)}"),
+    ("v_add_u32_e64 with sgpr source", lambda i: f"v_add_u32_e64 {dst(i)}, s40, {v(i % 16)}"),
+    ("v_xor_b32_e32 with sgpr source", lambda i: f"v_xor_b32_e32 {dst(i)}, s40, {v(i % 16)}"),
+    ("v_mov_b32_dpp row_shr:1", lambda i: f"v_mov_b32_dpp {dst(i)}, {v(i % 16)} row_shr:1 row_mask:0xf bank_mask:0xf"),
+    ("v_or_b32_dpp row_shr:1", lambda i: f"v_or_b32_dpp {dst(i)}, {v(i % 16)}, {v((i + 1) % 16)} row_shr:1 row_mask:0xf bank_mask:0xf"),
+    ("v_mov_b32_dpp wave_shr:1", lambda i: f"v_mov_b32_dpp {dst(i)}, {v(i % 16)} wave_shr:1 row_mask:0xf bank_mask:0xf"),
+    ("v_or_b32_dpp wave_shr:1", lambda i: f"v_or_b32_dpp {dst(i)}, {v(i % 16)}, {v((i + 1) % 16)} wave_shr:1 row_mask:0xf bank_mask:0xf"),
+    ("v_mov_b32_dpp row_bcast / quad_perm", lambda i: f"v_mov_b32_dpp {dst(i)}, {v(i % 16)} quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"),
+    ("v_permlane32_swap", lambda i: f"v_permlane32_swap_b32_e32 {v(16 + (2 * i) % 16)}, {v(17 + (2 * i) % 16)}"),
     ("v_and_b32 (VOP2) + v_bitop3 alternating",
      lambda i: (f"v_and_b32 {dst(i)}, {v(i % 16)}, {v((i + 1) % 16)}" if i % 2 == 0 else
                 "v_bitop3_b32 {}, {}, {}, {} bitop3:0x96".format(dst(i), *distinct3(i)))),
@@ -70,6 +88,8 @@ def main() -> None:
         "#include <cstdint>",
         "#include <cstdio>",
         "#include <cstdlib>",
+        "#include <algorithm>",
+        "#include <map>",
         "#include <vector>",
         "",
         "#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf(\"HIP error %s line %d\\n\", "
@@ -77,7 +97,9 @@ def main() -> None:
         "",
         "#define CLOB \"v0\",\"v1\",\"v2\",\"v3\",\"v4\",\"v5\",\"v6\",\"v7\",\"v8\",\"v9\",\"v10\",\"v11\",\"v12\",\"v13\","
         "\"v14\",\"v15\",\"v16\",\"v17\",\"v18\",\"v19\",\"v20\",\"v21\",\"v22\",\"v23\",\"v24\",\"v25\",\"v26\",\"v27\","
-        "\"v28\",\"v29\",\"v30\",\"v31\",\"s40\",\"s42\",\"s43\",\"s44\",\"s45\"",
+        "\"v28\",\"v29\",\"v30\",\"v31\",\"s40\",\"s42\",\"s43\",\"s44\",\"s45\",\"vcc\"",
+        "",
+        "constexpr int kRec = 5;",
         "",
         "template <int V>",
         "__global__ __launch_bounds__(256) void bench(uint64_t* rec, uint32_t* sink, int iters, uint32_t seed) {",
@@ -104,10 +126,16 @@ def main() -> None:
         "  uint32_t acc;",
         "  asm volatile(\"v_bitop3_b32 %0, v16, v17, v18 bitop3:0x96\\n\\tv_bitop3_b32 %0, %0, v19, v31 bitop3:0x96\" : \"=v\"(acc) :: CLOB);",
         "  sink[blockIdx.x * blockDim.x + threadIdx.x] = acc;",
+        "  // Where the wave ran: HW_ID (wave, SIMD, CU, SH, SE) and the XCC.",
+        "  const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));",
+        "  const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));",
         "  if ((threadIdx.x & 63) == 0) {",
         "    const int w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;",
-        "    rec[2 * w] = t1 - t0;",
-        "    rec[2 * w + 1] = r1 - r0;",
+        "    rec[kRec * w + 0] = t0;",
+        "    rec[kRec * w + 1] = t1;",
+        "    rec[kRec * w + 2] = r0;",
+        "    rec[kRec * w + 3] = r1;",
+        "    rec[kRec * w + 4] = (uint64_t(xcc) << 32) | hw;",
         "  }",
         "}",
         "",
@@ -120,20 +148,39 @@ def main() -> None:
         "    const int blocks = cus * w, waves = blocks * 4;",
         "    uint64_t* rec;",
         "    uint32_t* sink;",
-        "    CHK(hipMalloc(&rec, sizeof(uint64_t) * 2 * waves));",
+        "    CHK(hipMalloc(&rec, sizeof(uint64_t) * kRec * waves));",
         "    CHK(hipMalloc(&sink, sizeof(uint32_t) * 256 * blocks));",
         "    hipLaunchKernelGGL(bench<V>, dim3(blocks), dim3(256), 0, 0, rec, sink, iters / 8, 7u);  // warm",
         "    hipLaunchKernelGGL(bench<V>, dim3(blocks), dim3(256), 0, 0, rec, sink, iters, 7u);",
         "    CHK(hipDeviceSynchronize());",
-        "    std::vector<uint64_t> h(2 * waves);",
-        "    CHK(hipMemcpy(h.data(), rec, sizeof(uint64_t) * 2 * waves, hipMemcpyDeviceToHost));",
-        "    double cyc = 0, real = 0;",
-        "    for (int i = 0; i < waves; ++i) cyc += double(h[2 * i]), real += double(h[2 * i + 1]);",
-        "    cyc /= waves;",
-        "    real /= waves;",
-        f"    const double instrs = double(iters) * {N};",
-        "    std::printf(\"%-40s waves/SIMD=%d  %.2f cycles per instruction per SIMD  (clock %.2f GHz)\\n\", kNames[V], w,",
-        "                cyc / (instrs * w), cyc / (real / 100e6) / 1e9);",
+        "    std::vector<uint64_t> h(size_t(kRec) * waves);",
+        "    CHK(hipMemcpy(h.data(), rec, sizeof(uint64_t) * kRec * waves, hipMemcpyDeviceToHost));",
+        "    // Per SIMD (XCC, SE, SH, CU, SIMD): waves it ran, the span from the first",
+        "    // start to the last end (100 MHz realtime), and the clock (memtime ticks",
+        "    // per realtime tick) -> cycles per wave-instruction on that SIMD.",
+        "    struct S { int n = 0; uint64_t r0 = ~0ull, r1 = 0; double clk = 0; int conc = 0; };",
+        "    std::map<uint64_t, S> simds;",
+        "    for (int i = 0; i < waves; ++i) {",
+        "      const uint64_t* q = &h[size_t(kRec) * i];",
+        "      const uint64_t hwid = q[4] & 0xffffffffull, xcc = q[4] >> 32;",
+        "      const uint64_t key = (xcc << 32) | (hwid & 0xff30u);  // SIMD [5:4], CU [11:8], SH/SE [15:12]",
+        "      S& s = simds[key];",
+        "      s.n++;",
+        "      s.r0 = std::min(s.r0, q[2]);",
+        "      s.r1 = std::max(s.r1, q[3]);",
+        "      s.clk += double(q[1] - q[0]) / double(std::max<uint64_t>(1, q[3] - q[2]));",
+        "    }",
+        "    double cpi = 0, clk = 0, nw = 0;",
+        "    for (auto& [k, s] : simds) {",
+        f"      const double instrs = double(iters) * {N} * s.n;",
+        "      const double c = s.clk / s.n;  // memtime ticks per 10 ns",
+        "      cpi += double(s.r1 - s.r0) * c / instrs;",
+        "      clk += c;",
+        "      nw += s.n;",
+        "    }",
+        "    const double ns = double(simds.size());",
+        "    std::printf(\"%-40s waves/SIMD=%d (%4zu SIMDs, %.2f waves each)  %.2f cycles per wave-instruction per SIMD  (clock %.2f GHz)\\n\",",
+        "                kNames[V], w, simds.size(), nw / ns, cpi / ns, clk / ns / 10.0);",
         "    CHK(hipFree(rec));",
         "    CHK(hipFree(sink));",
         "  }",
