@@ -118,18 +118,25 @@ class CpuBackend final : public Backend {
     const size_t halo = size_t(g.Dv) * size_t(g.pitch), owned = size_t(g.H) * size_t(g.pitch);
     const int fd = ::memfd_create("gol_row_ring", 0);
     GOL_REQUIRE(fd >= 0, std::string("row ring: memfd_create failed: ") + std::strerror(errno));
-    GOL_REQUIRE(::ftruncate(fd, off_t(owned)) == 0, "row ring: ftruncate failed");
-    void* va = ::mmap(nullptr, owned + 2 * halo, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    GOL_REQUIRE(va != MAP_FAILED, "row ring: address reservation failed");
-    auto* b = static_cast<uint8_t*>(va);
-    const auto map = [&](uint8_t* at, size_t len, off_t off) {
-      void* r = ::mmap(at, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, fd, off);
-      GOL_REQUIRE(r == at, "row ring: mmap failed");
-    };
-    map(b, halo, off_t(owned - halo));   // top halo  = last owned rows
-    map(b + halo, owned, 0);             // owned rows
-    map(b + halo + owned, halo, 0);      // bottom halo = first owned rows
-    ::close(fd);                         // the mappings keep the memory
+    void* va = MAP_FAILED;
+    try {
+      GOL_REQUIRE(::ftruncate(fd, off_t(owned)) == 0, "row ring: ftruncate failed");
+      va = ::mmap(nullptr, owned + 2 * halo, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      GOL_REQUIRE(va != MAP_FAILED, "row ring: address reservation failed");
+      auto* b = static_cast<uint8_t*>(va);
+      const auto map = [&](uint8_t* at, size_t len, off_t off) {
+        void* r = ::mmap(at, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, fd, off);
+        GOL_REQUIRE(r == at, "row ring: mmap failed");
+      };
+      map(b, halo, off_t(owned - halo));  // top halo  = last owned rows
+      map(b + halo, owned, 0);            // owned rows
+      map(b + halo + owned, halo, 0);     // bottom halo = first owned rows
+    } catch (...) {
+      if (va != MAP_FAILED) ::munmap(va, owned + 2 * halo);  // the whole range, mapped pieces included
+      ::close(fd);
+      throw;
+    }
+    ::close(fd);  // the mappings keep the memory
     std::lock_guard<std::mutex> lk(ring_mu_);
     rings_[va] = owned + 2 * halo;
     return va;  // memfd pages start zeroed

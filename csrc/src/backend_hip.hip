@@ -306,27 +306,36 @@ class HipBackend final : public Backend {
     prop.location.type = hipMemLocationTypeDevice;
     prop.location.id = dev_;
     const size_t sizes[3] = {halo, owned - 2 * halo, halo};
-    for (int i = 0; i < 3; ++i)
-      if (sizes[i]) HIP_CHECK(hipMemCreate(&r.h[i], sizes[i], &prop, 0));
-    HIP_CHECK(hipMemAddressReserve(&r.va, r.bytes, gran, nullptr, 0));
-    auto* b = static_cast<uint8_t*>(r.va);
-    // [C | A B C | A]
-    const struct {
-      size_t at;
-      int piece;
-    } maps[5] = {{0, 2}, {halo, 0}, {2 * halo, 1}, {owned, 2}, {owned + halo, 0}};
-    for (const auto& m : maps) {
-      if (!sizes[m.piece]) continue;
-      HIP_CHECK(hipMemMap(b + m.at, sizes[m.piece], 0, r.h[m.piece], 0));
-      r.mapped.push_back({b + m.at, sizes[m.piece]});
+    auto* b = static_cast<uint8_t*>(nullptr);
+    try {
+      for (int i = 0; i < 3; ++i)
+        if (sizes[i]) HIP_CHECK(hipMemCreate(&r.h[i], sizes[i], &prop, 0));
+      HIP_CHECK(hipMemAddressReserve(&r.va, r.bytes, gran, nullptr, 0));
+      b = static_cast<uint8_t*>(r.va);
+      // [C | A B C | A]
+      const struct {
+        size_t at;
+        int piece;
+      } maps[5] = {{0, 2}, {halo, 0}, {2 * halo, 1}, {owned, 2}, {owned + halo, 0}};
+      for (const auto& m : maps) {
+        if (!sizes[m.piece]) continue;
+        HIP_CHECK(hipMemMap(b + m.at, sizes[m.piece], 0, r.h[m.piece], 0));
+        r.mapped.push_back({b + m.at, sizes[m.piece]});
+      }
+      hipMemAccessDesc acc{};
+      acc.location.type = hipMemLocationTypeDevice;
+      acc.location.id = dev_;
+      acc.flags = hipMemAccessFlagsProtReadWrite;
+      HIP_CHECK(hipMemSetAccess(r.va, r.bytes, &acc, 1));
+      HIP_CHECK(hipMemsetAsync(b + halo, 0, owned, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    } catch (...) {
+      // A partial ring (out of memory or address space) gives back what it
+      // took, so the engine's fallback to plain buffers has it.
+      release_ring(r);
+      (void)hipGetLastError();
+      throw;
     }
-    hipMemAccessDesc acc{};
-    acc.location.type = hipMemLocationTypeDevice;
-    acc.location.id = dev_;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    HIP_CHECK(hipMemSetAccess(r.va, r.bytes, &acc, 1));
-    HIP_CHECK(hipMemsetAsync(b + halo, 0, owned, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
     if (check_dev_) check_ptr(b + halo, "row ring");
     rings_[r.va] = r;
     return r.va;
@@ -950,9 +959,13 @@ class HipBackend final : public Backend {
   };
   void release_ring(Ring& r) {
     for (auto& m : r.mapped) (void)hipMemUnmap(m.first, m.second);
-    (void)hipMemAddressFree(r.va, r.bytes);
-    for (auto h : r.h)
+    r.mapped.clear();
+    if (r.va) (void)hipMemAddressFree(r.va, r.bytes);
+    r.va = nullptr;
+    for (auto& h : r.h) {
       if (h) (void)hipMemRelease(h);
+      h = {};
+    }
   }
   // Default builds carry neither the measured-slower variants nor their
   // schedules (hipk::kExperimentalBuild): an environment asking for one fails
