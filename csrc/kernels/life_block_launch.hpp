@@ -43,12 +43,12 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   constexpr int M = 8;
   LinkState& L = *tune.link;
   if (s != L.stream[0]) return false;
-  LifeBlockParams q = p0;
-  q.fold = 1;
-  q.fold_lanes = 64;
+  LifeBlockParams q = p0;  // keeps launch_T's folded last strip (q.fold): a folded block publishes
+                           // the completion words of all its groups
   if (plan_group<T, M>(q, out_rows, simds, group_waves_per_simd<T, LIO, M>(), tune.target_waves, IO::XL) <= 0)
     return false;
-  const int64_t blocks = int64_t(q.ncolw) * q.nseg;
+  const int64_t blocks = q.fold > 1 ? int64_t(q.ncolw - 1) * q.nseg + ceil_div(int64_t(q.nseg), int64_t(q.fold))
+                                    : int64_t(q.ncolw) * q.nseg;
   static const int per_cu = occupancy_blocks(life_group_kernel<T, LIO, M>, 64 * M);
   const int64_t cap = int64_t(std::max(1, tune.cus)) * per_cu;
   const bool link = L.prev_valid && L.prev_out == q.in && L.prev.ncolw == q.ncolw && L.prev.wrap_w == q.wrap_w &&
@@ -56,7 +56,7 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   // Completion words of this launch: the third buffer back, so neither the
   // previous launch's words (read by this one) nor the ones before it (read by
   // the previous launch, which may still run) are overwritten.
-  const size_t need = size_t(blocks);
+  const size_t need = size_t(q.ncolw) * size_t(q.nseg);  // one word per group
   if (L.flag_words < need) {
     if (!tune.chain_mem) return false;
     for (int i = 0; i < 3; ++i) L.flags[i] = tune.chain_mem(2 + i, need * 4);

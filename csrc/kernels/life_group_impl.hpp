@@ -400,7 +400,9 @@ void life_group_kernel(const LifeBlockParams p) {
   }
 
   if constexpr (IO::kLinked) {  // wait for the previous launch's rows this group reads
-    if (p.link_prev_flag && m == 0) link_wait(p, kcol, G0 - T, G1 + T, lane);
+    // (a folded block: the rows of all its groups)
+    const int64_t Gend = nsub > 1 ? group_end(min(grp + nsub - 1, p.nseg - 1)) : G1;
+    if (p.link_prev_flag && m == 0) link_wait(p, kcol, G0 - T, Gend + T, lane);
     __syncthreads();
   }
   rd.base = p.in + in0 * pitch;  // input row of step k: in0 + k
@@ -463,8 +465,9 @@ void life_group_kernel(const LifeBlockParams p) {
   if constexpr (IO::kLinked) {  // every wave's rows are written through, then one flag
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (p.link_flag && m == 0 && lane == 0)
-      __hip_atomic_store(p.link_flag + (int64_t(kcol) * p.nseg + grp), p.link_seq, __ATOMIC_RELAXED,
+    // One word per group: a folded block publishes each of its groups.
+    if (p.link_flag && m == 0 && lane < nsub && grp + lane < p.nseg)
+      __hip_atomic_store(p.link_flag + (int64_t(kcol) * p.nseg + grp + lane), p.link_seq, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
   if (p.wg_trace) wg_trace_record(p.wg_trace, M, m, lane, t_start);
