@@ -51,6 +51,13 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
                                     : int64_t(q.ncolw) * q.nseg;
   static const int per_cu = occupancy_blocks(life_group_kernel<T, LIO, M>, 64 * M);
   const int64_t cap = int64_t(std::max(1, tune.cus)) * per_cu;
+  // Two such launches never fit beside each other: the plain kernel (no
+  // write-through stores, no completion words) serves the whole chain.
+  if (2 * blocks > cap) {
+    link_join(L);
+    L.prev_valid = false;
+    return false;
+  }
   const bool link = L.prev_valid && L.prev_out == q.in && L.prev.ncolw == q.ncolw && L.prev.wrap_w == q.wrap_w &&
                     L.prev.pitch == q.pitch && L.prev_blocks + blocks <= cap;
   // Completion words of this launch: the third buffer back, so neither the

@@ -757,10 +757,12 @@ class HipBackend final : public Backend {
       }
       // Such tiles also link consecutive launches where each holds at least
       // 1.5 waves per SIMD: two launches then fill the SIMDs together (8192^2
-      // 1.93 -> 1.75 ms per 1000 generations; 4096^2, with 0.75 waves per
-      // SIMD, and 4-wave-per-SIMD tiles measured slower linked;
-      // profiles/r04/linked_launches_ring.jsonl).
-      k.link = k.tmax < 16 && strips * (rows / (2 * k.tmax)) >= int64_t(6) * cus_;
+      // 1.93 -> 1.60 ms per 1000 generations with the folded strip; the 8-GPU
+      // rank tile 2.26 -> 2.24 single-rank, 2.44 -> 2.40 in the multi-rank
+      // schedule; 4096^2, with 0.75 waves per SIMD, measured slower linked;
+      // profiles/r04/linked_*.jsonl).  Launches too large to run two at once
+      // are never linked (launch_linked).
+      k.link = strips * (rows / (2 * k.tmax)) >= int64_t(6) * cus_;
     }
     return k;
   }

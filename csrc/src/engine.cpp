@@ -153,9 +153,12 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   }
   if (ring_dv > 0) {
     rows_ring_ = true;
-    link_ = kc.link && !cols_filled_;  // epochs move no data: consecutive blocks may run linked
     if (cfg_.epoch <= 0) D_ = tmax_;  // an epoch only paces the polls (and column fills) now
   }
+  // Linked launches (Backend::KernelChoice::link): consecutive blocks of an
+  // epoch overlap; anything else on the stream (fills, exchanges, polls)
+  // joins the streams first.  Not with column fills between blocks.
+  link_ = kc.link && !cols_filled_;
   // Experiment knob: extra bytes per padded row (multiple of 256).
   if (const char* pad = std::getenv("GOL_PITCH_PAD")) g_.pitch += 256 * (std::max(0, std::atoi(pad)) / 256);
   // Several ranks: every poll is a flag all-reduce on the compute stream
