@@ -218,8 +218,11 @@ def main() -> int:
             # own "node" (socket transport over loopback).
             shared = True
             os.environ["NCCL_HOSTID"] = f"gol-bench-rank{rank}"
-            # Resident epochs need every CU of the device for one launch.
+            # Resident epochs need every CU of the device for one launch, and
+            # linked launches that two of their launches fit on it at once
+            # (another rank's kernels would stretch a linked wait past its bound).
             os.environ["GOL_RESIDENT"] = "0"
+            os.environ.setdefault("GOL_LINK", "0")
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         local = local % max(1, ndev)
 
