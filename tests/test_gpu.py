@@ -1067,6 +1067,26 @@ def test_row_ring_graphs(gpu):
     assert (sim.tile() == life_step_torch(g, 200, device="cuda")).all()
 
 
+def test_rank_tile_multirank_schedule_links_by_default(gpu):
+    """The 8-GPU rank tile (32768 x 4096) in the multi-rank schedule (row
+    halos through a 1-rank RCCL communicator, epoch trapezoids): the blocks of
+    an epoch run linked by default, every exchange and poll joins the two
+    streams first, and the result is exact against the fp32 oracle."""
+    C = gpu
+    W, H = 32768, 4096
+    g = random_grid(W, H, 17)
+    gens = 600  # past two epochs of 16T = 256 and two termination polls
+    want = life_step_torch(g, gens, device="cuda")
+    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0)
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, self_exchange=True), transport=tr, backend=C.hip_backend(0))
+    d = sim.describe()
+    assert d["tmax"] == 16 and d["row_ring"] is False
+    sim.load(g)
+    rep = sim.advance(gens)
+    assert rep.exchanges >= 2 and rep.linked_launches > 0
+    assert (sim.tile() == want).all()
+
+
 def test_small_ring_tiles_link_launches_by_default(gpu, monkeypatch):
     """Small single-rank ring tiles (the small-tile T rule, >= 1.5 waves per
     SIMD per launch) run consecutive blocks linked by default
