@@ -200,6 +200,9 @@ __device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int 
 #ifndef GOL_ADDER_DPP
 #define GOL_ADDER_DPP 0
 #endif
+#ifndef GOL_ADDER_FAKE
+#define GOL_ADDER_FAKE 0
+#endif
 __device__ __forceinline__ void adder_window(uint32_t c, uint32_t& l1, uint32_t& l2) {
   // One block so the pair of lane masks never outlives the window (no SGPR
   // pressure across levels).  gfx950 wants a wait state between the last
@@ -256,7 +259,12 @@ __device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1, Ve
     static_assert(W == 1 || W == 2, "adder window: one or two words per lane");
     if constexpr (W == 1) {
       uint32_t l1, l2;
-#if GOL_ADDER_DPP
+#if GOL_ADDER_FAKE
+      // Timing probe only (WRONG cells): the window's shifts without the
+      // cross-lane carries, to price them in the level-body microbenchmark.
+      l1 = c.w[0] + c.w[0];
+      l2 = l1 + l1;
+#elif GOL_ADDER_DPP
       // Experiment: the same one-sided window from one DPP lane shift and
       // two funnel shifts (3 half-rate VALU ops instead of the 4 carry ops).
       const uint32_t lw = __builtin_amdgcn_mov_dpp(c.w[0], 0x138, 0xF, 0xF, true);  // wave_shr:1

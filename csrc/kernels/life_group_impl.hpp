@@ -293,10 +293,13 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
 // allocator lands at 123 VGPRs = 4 waves/SIMD for bits T = 16 and at 183 for
 // the byte layout).  Without a cap, an early version with a separate
 // remainder branch took ~400 registers (VGPR + AGPR, one wave per SIMD).
+#ifndef GOL_GROUP_T12_ADD_WAVES
+#define GOL_GROUP_T12_ADD_WAVES 3
+#endif
 template <int T, class IO>
 constexpr int group_min_waves() {
   if constexpr (IO::W >= 2) return T >= 12 ? 2 : T >= 8 ? 3 : 4;
-  if constexpr (IO::XL == kXlaneAdd) return T >= 16 ? GOL_GROUP_T16_ADD_WAVES : T >= 12 ? 3 : 4;
+  if constexpr (IO::XL == kXlaneAdd) return T >= 16 ? GOL_GROUP_T16_ADD_WAVES : T >= 12 ? GOL_GROUP_T12_ADD_WAVES : 4;
   return T >= 16 ? GOL_GROUP_T16_WAVES : T >= 12 ? 3 : 4;
 }
 

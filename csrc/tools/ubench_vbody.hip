@@ -233,6 +233,22 @@ int main(int argc, char** argv) {
     for (int n : {1, 2, 4}) std::printf(" %8.2f", run(k_row2<T, XL>, n, steps, cus, out, 2 * T)); \
     std::printf("\n");                                                                             \
   } while (0)
+  if (argc > 2 && std::atoi(argv[2]) == 1) {  // occupancy sweep of the row-word bodies: 1-8 waves per SIMD
+    std::printf("%-34s %8s %8s %8s %8s %8s\n", "variant", "1 w", "2 w", "4 w", "6 w", "8 w");
+#define ROWN(T, XL, name)                                                                                \
+  do {                                                                                                   \
+    attr(reinterpret_cast<const void*>(&k_row<T, XL>));                                                  \
+    std::printf("%-34s", name);                                                                          \
+    for (int n : {1, 2, 4, 6, 8}) std::printf(" %8.2f", run(k_row<T, XL>, n, steps, cus, out, T));     \
+    std::printf("\n");                                                                                   \
+  } while (0)
+    ROWN(4, kXlaneAdd, "row words, adder window, T=4");
+    ROWN(8, kXlaneAdd, "row words, adder window, T=8");
+    ROWN(12, kXlaneAdd, "row words, adder window, T=12");
+    ROWN(8, kXlaneDpp, "row words, DPP window, T=8");
+    CHK(hipFree(out));
+    return 0;
+  }
   ROW2(8, kXlaneAdd, "row words x2/lane, adder, T=8");
   ROW2(12, kXlaneAdd, "row words x2/lane, adder, T=12");
   ROW2(16, kXlaneAdd, "row words x2/lane, adder, T=16");

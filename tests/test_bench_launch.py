@@ -245,3 +245,23 @@ def test_native_cli_resume_rejects_another_sim_freq(gol_bin, tmp_path):
     r = subprocess.run([str(gol_bin), "--resume", str(ck), "--engine", "cpu", "--sim-freq", "5", "--output", "none"],
                        cwd=tmp_path, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "--sim-freq" in r.stderr
+
+
+def test_band_oracle_matches_whole_grid_oracle():
+    """bench.py checks grids beyond 2^30 cells on row bands with their light
+    cones (no 2^32-element fp32 tensor): each band equals the same rows of the
+    whole-grid fp32 oracle, at the torus's top, middle and bottom."""
+    import numpy as np
+
+    from gol_amd import random_grid
+    from gol_amd.ops.life_ops import life_step_torch_roll
+
+    b = _bench_module()
+    H, W, g = 300, 64, 23
+    snap = random_grid(W, H, 9)
+    want = life_step_torch_roll(snap, g)
+    starts = b.band_starts(H)
+    assert starts[0] == 0 and starts[-1] == H - b.ORACLE_BAND_ROWS and len(starts) == 3
+    for r0 in starts + [7]:
+        rows = np.arange(r0, r0 + b.ORACLE_BAND_ROWS) % H
+        assert np.array_equal(b.band_oracle(snap, r0, g, "cpu"), want[rows]), r0
