@@ -7,16 +7,20 @@
 //
 // What this kernel does instead (CDNA4-first design):
 //   * Cells are processed 32 at a time as bit planes: a lane owns W adjacent
-//     32-cell words of a row; a wave64 owns 64*W adjacent words (the outermost
-//     word on each side is its halo).  The neighbour count is a bit-sliced
-//     adder tree built from v_bitop3_b32 (any 3-input boolean function in ONE
-//     full-rate VALU op on gfx950) and v_alignbit_b32 funnel shifts; the two
-//     bits that cross a lane boundary move with one cross-lane op per side
-//     (DPP wave_shr/wave_shl, or ds_bpermute on the LDS crossbar).  Per word
-//     and generation: 10 bitop3 + 2 alignbit + 2/W cross-lane ops.
-//     Measured on MI355X (csrc/tools/ubench_level.hip): a DPP wave shift costs
-//     ~10 cycles inside a VALU stream vs ~2.5 for bitop3, so the bit layout
-//     uses W=2 words per lane to halve that overhead.
+//     32-cell words of a row (W = 1 in the default build); a wave64 owns 64*W
+//     adjacent words (its outermost word(s) are halo).  The neighbour count is
+//     a bit-sliced adder tree built from v_bitop3_b32 (any 3-input boolean
+//     function in ONE full-rate VALU op on gfx950).  The two bits that cross a
+//     lane boundary come from one of two horizontal windows:
+//       - the adder window (kXlaneAdd, the default wherever a tile fills four
+//         waves per SIMD): one-sided cells x-2, x-1, x from add-with-carry
+//         ops whose lane masks move on the SALU; the storage frame drifts one
+//         cell per generation (adder_window);
+//       - the symmetric DPP window (kXlaneDpp, smaller tiles): DPP wave
+//         shifts and v_alignbit funnel shifts.
+//     Per word and generation: 10 bitop3/AND + 4 carry ops (adder) or
+//     2 DPP + 2 alignbit (DPP).  Issue classes measured per instruction form:
+//     csrc/tools/ubench_vop3.hip (profiles/r04/ubench_vop3.txt).
 //   * Temporal blocking in registers: the wave streams down its column strip
 //     one row at a time and carries T generation levels, each with a 3-row
 //     sliding window of horizontal partial sums.  Every input row is read
