@@ -131,6 +131,9 @@ def metric_label(S: int, Hg: int, gps: int) -> tuple[str, bool, int | None]:
 # grid); larger grids are checked on row bands with their light cones.
 ORACLE_WHOLE_CELLS = 1 << 30
 ORACLE_BAND_ROWS = 128
+# Beyond this the verification step is skipped (host copies of the grid and
+# the byte-layout engine would not fit): 2^34 cells = 16 GiB per byte copy.
+VERIFY_MAX_CELLS = 1 << 34
 
 
 def band_starts(H: int) -> list[int]:
@@ -360,7 +363,12 @@ def main() -> int:
     # continues from its current state; the oracle restarts from a snapshot.
     verify = None
     verified = None
-    if a.verify > 0:
+    if a.verify > 0 and S * Hg > VERIFY_MAX_CELLS:
+        # Host copies of the whole grid (snapshot, result) and a second byte-
+        # layout engine do not fit beside a grid this large.
+        log(f"bench.py: --verify skipped: {S}x{Hg} exceeds {VERIFY_MAX_CELLS} cells")
+        verify = {"skipped": f"grid beyond {VERIFY_MAX_CELLS} cells"}
+    elif a.verify > 0:
         from gol_amd.ops.life_ops import life_step_torch_roll  # noqa: PLC0415
         from gol_amd.parallel.dist import gather_grid  # noqa: PLC0415
 
