@@ -165,7 +165,19 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         _run([_hipcc(), *core, str(objs[CLI_MAIN]), "-o", str(outs["gol"]), *rocm_libs], verbose)
         _run([_hipcc(), *core, str(objs[GEN_MAIN]), "-o", str(outs["gol_gen"]), *rocm_libs], verbose)
         MODE_STAMP.write_text(MODE + "\n")
+    LAST_BUILD.clear()
+    LAST_BUILD.update(compiled=len(todo), up_to_date=len(srcs) - len(todo), relinked=relink, mode=MODE)
     return outs
+
+
+# What the last build() in this process did (compiled vs up-to-date objects).
+LAST_BUILD: dict = {}
+
+
+def gfx950_code_objects(path: Path = MODULE) -> int:
+    """Number of gfx950 device code objects bundled in a built library (the
+    offload bundle entries name their target)."""
+    return path.read_bytes().count(b"amdgcn-amd-amdhsa--" + ARCH.encode())
 
 
 def compile_experimental(verbose: bool = False, jobs: int | None = None) -> int:
