@@ -85,12 +85,23 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
     q.link_prev_nseg = L.prev.nseg;
     q.link_prev_seg_rows = L.prev.seg_rows;
     q.link_prev_seg_rem = L.prev.seg_rem;
-    (void)hipStreamWaitEvent(st, L.before[L.cur], 0);
+    // Only the chain's second launch waits for the first one's start (an
+    // event): the first follows whatever the stream held before it (fills,
+    // an exchange), which may take long, and a linked group's wait is
+    // bounded.  Later launches need no event: each becomes eligible when the
+    // launch two back on its own stream ends, after the previous launch did,
+    // so it never waits long; its groups touch no memory before their
+    // completion-word waits, and two launches fit on the GPU together (cap).
+    // Its stream also orders it after the launch two back, whose completion
+    // words (flags[seq % 3]) it overwrites.
+    if (L.events || L.chain == 1) (void)hipStreamWaitEvent(st, L.before[L.cur], 0);
     ++L.linked;
   } else {
     link_join(L);
+    L.chain = 0;
   }
-  (void)hipEventRecord(L.before[which], st);
+  if (L.events || L.chain == 0) (void)hipEventRecord(L.before[which], st);
+  ++L.chain;
   hipLaunchKernelGGL((life_group_kernel<T, LIO, M>), dim3(unsigned(blocks)), dim3(64 * M), 0, st, q);
   L.cur = which;
   L.prev = q;

@@ -118,6 +118,16 @@ struct LinkState {
   size_t flag_words = 0;
   uint32_t seq = 0;
   int64_t linked = 0;                           // launches that ran linked (diagnostics)
+  // Order every linked launch after the previous one's start with a cross-
+  // stream event (GOL_LINK_EVENTS, default 1).  With 0 only a chain's second
+  // launch does; the completion words still order the data (launch_linked).
+  // An event wait between two streams costs ~10 us of device time on MI355X
+  // (csrc/tools/ubench_launch.hip), yet without them 8192^2 runs slower
+  // (1.81-1.85 vs 1.61 ms per 1000 generations; the early consumers' spinning
+  // waves take the producer's slots), the rank tile the same
+  // (profiles/r04/linked_events_ab.jsonl).
+  bool events = true;
+  int chain = 0;  // launches in the current chain
 };
 
 // Everything enqueued on stream[1] precedes what comes next on stream[0];

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
@@ -130,6 +131,7 @@ class HipBackend final : public Backend {
       link_.stream[0] = stream_;
       HIP_CHECK(hipStreamCreateWithFlags(&link_.stream[1], hipStreamNonBlocking));
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      link_.events = env_int("GOL_LINK_EVENTS", 1) != 0;
     }
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
     if (!hipk::kExperimentalBuild) refuse_experimental();
@@ -158,6 +160,12 @@ class HipBackend final : public Backend {
       if (c != std::string::npos) {
         trace_at_ = std::atoi(v.substr(0, c).c_str());
         trace_path_ = v.substr(c + 1);
+        // "N:path:pair": launches N and N + 1, left linked (overlap evidence).
+        const size_t c2 = trace_path_.rfind(":pair");
+        if (c2 != std::string::npos && c2 + 5 == trace_path_.size()) {
+          trace_pair_ = true;
+          trace_path_ = trace_path_.substr(0, c2);
+        }
       }
     }
     // Kernel error word: fine-grained pinned host memory the kernels write
@@ -184,6 +192,10 @@ class HipBackend final : public Backend {
       std::lock_guard<std::mutex> lk(live_mu());
       --live_backends()[dev_];
     }
+    if (prof_on_ && prof_n_ > 0)
+      std::fprintf(stderr, "gol host profile: %lld blocks; per block: engine between blocks %.2f us, run_block %.2f us "
+                   "(launch call %.2f us)\n", (long long)prof_n_, prof_gap_ / double(std::max<int64_t>(1, prof_n_ - 1)),
+                   prof_in_ / double(prof_n_), prof_launch_ / double(prof_n_));
     DeviceScope device_scope(dev_);
     if (stream_) hipStreamSynchronize(stream_);
     for (auto& kv : rings_) release_ring(kv.second);
@@ -522,7 +534,19 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipStreamWaitEvent(on ? static_cast<hipStream_t>(on) : stream_, static_cast<hipEvent_t>(mark), 0));
   }
 
+  // GOL_HOST_PROFILE=1: host time per block, printed when the backend goes:
+  // the engine between blocks, run_block itself, and its launch call.
   int run_block(const BlockArgs& a) override {
+    if (!prof_on_) return run_block_impl(a);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (prof_n_ > 0) prof_gap_ += std::chrono::duration<double, std::micro>(t0 - prof_exit_).count();
+    const int r = run_block_impl(a);
+    prof_exit_ = std::chrono::steady_clock::now();
+    prof_in_ += std::chrono::duration<double, std::micro>(prof_exit_ - t0).count();
+    ++prof_n_;
+    return r;
+  }
+  int run_block_impl(const BlockArgs& a) {
     GOL_ON_DEVICE();
     if (check_dev_) {
       check_ptr(a.in, "run_block input");
@@ -589,6 +613,8 @@ class HipBackend final : public Backend {
       return drift;
 #endif  // GOL_EXPERIMENTAL
     }
+    if (trace_at_ >= 0 && trace_pair_ && (launches_ == trace_at_ || launches_ == trace_at_ + 1))
+      return run_block_traced_pair(a, linkable);
     if (trace_at_ >= 0 && launches_ == trace_at_) {
       join_streams();
       tune_.link = nullptr;
@@ -600,7 +626,9 @@ class HipBackend final : public Backend {
     if (chain_mode_ < 0 && !linkable) timed = autotune_chain(a);
     if (linkable) tune_.chain = 0;
     if (timed) HIP_CHECK(hipEventRecord(timed->e0, s));
+    const auto l0 = prof_on_ ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
     const int drift = hipk::launch_life_block(a, tune_, s);
+    if (prof_on_) prof_launch_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - l0).count();
     HIP_CHECK(hipGetLastError());
     if (timed) HIP_CHECK(hipEventRecord(timed->e1, s));
     return drift;
@@ -857,6 +885,53 @@ class HipBackend final : public Backend {
     std::fclose(f);
     return drift;
   }
+  // GOL_WG_TRACE=N:path:pair: per-wave records of launches N and N + 1 with
+  // the second one left linked to the first (scripts/wg_trace.py --pair
+  // reports how far they overlapped).  Buffers are set up before launch N.
+  int run_block_traced_pair(const BlockArgs& a, bool linkable) {
+    const size_t bytes = size_t(hipk::kWgTraceWaves) * 4 * sizeof(uint64_t);
+    const int which = int(launches_ - trace_at_);
+    if (which == 0) {
+      join_streams();
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      for (auto& d : pair_trace_) {
+        HIP_CHECK(hipMalloc(&d, bytes));
+        HIP_CHECK(hipMemsetAsync(d, 0, bytes, stream_));
+      }
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      pair_T_ = a.T;
+    }
+    ++launches_;
+    hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
+    if (linkable) tune_.chain = 0;
+    tune_.wg_trace = pair_trace_[which];
+    const int drift = hipk::launch_life_block(a, tune_, s);
+    tune_.wg_trace = nullptr;
+    HIP_CHECK(hipGetLastError());
+    if (which == 1) {
+      join_streams();
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      std::FILE* f = std::fopen(trace_path_.c_str(), "w");
+      GOL_REQUIRE(f != nullptr, "GOL_WG_TRACE: cannot open " + trace_path_);
+      std::fprintf(f, "launch,block,wave,xcc_id,hw_id,t_start,t_end,T,linked\n");
+      std::vector<uint64_t> h(size_t(hipk::kWgTraceWaves) * 4);
+      for (int l = 0; l < 2; ++l) {
+        HIP_CHECK(hipMemcpy(h.data(), pair_trace_[l], bytes, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < hipk::kWgTraceWaves; ++i) {
+          const uint64_t* r = &h[size_t(4 * i)];
+          if (!(r[0] >> 63)) continue;
+          std::fprintf(f, "%d,%llu,%llu,%llu,%llu,%llu,%llu,%d,%d\n", l,
+                       (unsigned long long)((r[0] & ~(1ull << 63)) >> 8), (unsigned long long)(r[0] & 255),
+                       (unsigned long long)(r[1] >> 32), (unsigned long long)(r[1] & 0xFFFFFFFFull),
+                       (unsigned long long)r[2], (unsigned long long)r[3], l ? a.T : pair_T_, int(linkable));
+        }
+        HIP_CHECK(hipFree(pair_trace_[l]));
+        pair_trace_[l] = nullptr;
+      }
+      std::fclose(f);
+    }
+    return drift;
+  }
   void check_device_errors() override {
     const uint32_t e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
     if (e != 0) {
@@ -1052,8 +1127,15 @@ class HipBackend final : public Backend {
   std::deque<Pending> pending_;  // timed trial launches not collected yet
   std::vector<hipEvent_t> free_events_;
   int64_t launches_ = 0;
+  bool prof_on_ = env_int("GOL_HOST_PROFILE", 0) != 0;
+  int64_t prof_n_ = 0;
+  double prof_gap_ = 0, prof_in_ = 0, prof_launch_ = 0;
+  std::chrono::steady_clock::time_point prof_exit_{};
   int64_t trace_at_ = -1;
   std::string trace_path_;
+  bool trace_pair_ = false;
+  uint64_t* pair_trace_[2] = {nullptr, nullptr};
+  int pair_T_ = 0;
   std::array<hipEvent_t, 16> marks_{};
   size_t mark_next_ = 0;
   void* stage_ = nullptr;

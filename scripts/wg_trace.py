@@ -48,6 +48,32 @@ def main(path: str) -> None:
     print(f"mean CU occupancy over the span: {busy / (len(per_cu) * (t1 - t0)):.2f} workgroups")
 
 
+def pair(path: str) -> None:
+    """Two consecutive launches traced with GOL_WG_TRACE=N:path:pair: how far
+    the second (linked) launch overlapped the first."""
+    rows = list(csv.DictReader(open(path)))
+    tick_us = 0.01
+    by = collections.defaultdict(list)
+    for r in rows:
+        by[int(r["launch"])].append((int(r["t_start"]), int(r["t_end"])))
+    t0 = min(s for v in by.values() for s, _ in v)
+    (a, b) = (by[0], by[1])
+    a0, a1 = min(s for s, _ in a) - t0, max(e for _, e in a) - t0
+    b0, b1 = min(s for s, _ in b) - t0, max(e for _, e in b) - t0
+    early = sum(1 for s, _ in b if s - t0 < a1)
+    print(f"{path}: linked={rows[-1]['linked']} T={rows[0]['T']}/{rows[-1]['T']}")
+    print(f"launch 0: {len(a)} waves, {a0 * tick_us:.2f} .. {a1 * tick_us:.2f} us")
+    print(f"launch 1: {len(b)} waves, {b0 * tick_us:.2f} .. {b1 * tick_us:.2f} us")
+    print(f"overlap: launch 1 starts {(a1 - b0) * tick_us:.2f} us before launch 0 ends; "
+          f"{early} of its {len(b)} waves ({100.0 * early / max(1, len(b)):.0f} %) start before that end; "
+          f"two launches in {(b1 - a0) * tick_us:.2f} us vs {((a1 - a0) + (b1 - b0)) * tick_us:.2f} us back to back")
+
+
 if __name__ == "__main__":
-    for p in sys.argv[1:]:
-        main(p)
+    args = sys.argv[1:]
+    if args and args[0] == "--pair":
+        for p in args[1:]:
+            pair(p)
+    else:
+        for p in args:
+            main(p)
