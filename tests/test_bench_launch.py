@@ -265,3 +265,17 @@ def test_band_oracle_matches_whole_grid_oracle():
     for r0 in starts + [7]:
         rows = np.arange(r0, r0 + b.ORACLE_BAND_ROWS) % H
         assert np.array_equal(b.band_oracle(snap, r0, g, "cpu"), want[rows]), r0
+
+
+def test_band_oracle_small_grid_is_whole_grid():
+    """A torus shorter than one band: a single band covering every row."""
+    import numpy as np
+
+    from gol_amd import random_grid
+    from gol_amd.ops.life_ops import life_step_torch_roll
+
+    b = _bench_module()
+    H, W, g = 40, 32, 9
+    snap = random_grid(W, H, 3)
+    assert b.band_starts(H) == [0]
+    assert np.array_equal(b.band_oracle(snap, 0, g, "cpu"), life_step_torch_roll(snap, g))
