@@ -207,6 +207,14 @@ __device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int 
 #ifndef GOL_ADDER_FAKE
 #define GOL_ADDER_FAKE 0
 #endif
+// Timing probes only (a linked launch needs both): Sc1IO's write-through
+// row stores and its L1-bypassing row loads.
+#ifndef GOL_SC1_LOADS
+#define GOL_SC1_LOADS 1
+#endif
+#ifndef GOL_SC1_STORES
+#define GOL_SC1_STORES 1
+#endif
 __device__ __forceinline__ void adder_window(uint32_t c, uint32_t& l1, uint32_t& l2) {
   // One block so the pair of lane masks never outlives the window (no SGPR
   // pressure across levels).  gfx950 wants a wait state between the last
@@ -447,11 +455,12 @@ struct Sc1IO : IO {
     Raw r;
     const BufRsrc rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), short(0), 0x7FFFFFFF, kBufFlags);
 #pragma unroll
-    for (int i = 0; i < W; ++i) r.w[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, off[i] * 4, 0, kCpolSc1);
+    for (int i = 0; i < W; ++i)
+      r.w[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, off[i] * 4, 0, GOL_SC1_LOADS ? kCpolSc1 : 0);
     return r;
   }
   __device__ static __forceinline__ void store_buf(BufRsrc row, int voff, uint32_t w) {
-    __builtin_amdgcn_raw_buffer_store_b32(w, row, voff, 0, kCpolSc1);
+    __builtin_amdgcn_raw_buffer_store_b32(w, row, voff, 0, GOL_SC1_STORES ? kCpolSc1 : 0);
   }
 };
 

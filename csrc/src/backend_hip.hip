@@ -132,6 +132,7 @@ class HipBackend final : public Backend {
       HIP_CHECK(hipStreamCreateWithFlags(&link_.stream[1], hipStreamNonBlocking));
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       link_.events = env_int("GOL_LINK_EVENTS", 1) != 0;
+      tune_.link_force = env_int("GOL_LINK_FORCE", 0) != 0;
     }
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
     if (!hipk::kExperimentalBuild) refuse_experimental();
