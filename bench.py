@@ -454,6 +454,10 @@ def main() -> int:
                 "polls_per_step": rs[-1].polls if rs else 0,
                 "kernel_launches_per_step": rs[-1].kernel_launches if rs else 0,
                 "linked_launches_per_step": rs[-1].linked_launches if rs else 0,
+                "flow": desc["flow"],
+                "flow_launches_per_step": rs[-1].flow_launches if rs else 0,
+                "flow_blocks_per_step": rs[-1].flow_blocks if rs else 0,
+                "flow_plan": desc["flow_plan"],
                 "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith("GOL_")},
                 "halo_bytes_per_step": rs[-1].halo_bytes if rs else 0,
                 "overlapped_halo_exchange": bool(rs and rs[-1].overlapped),

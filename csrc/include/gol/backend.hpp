@@ -100,6 +100,15 @@ class Backend {
   // (BlockArgs::allow_drift): the output's column x holds the cell the input
   // frame had at x - drift.
   virtual int run_block(const BlockArgs& a) = 0;
+  // A run of temporal blocks (FlowArgs) as one launch where the backend has a
+  // persistent dataflow kernel for it (has_flow); returns the total drift.
+  // The default runs the blocks one by one through run_block, with the same
+  // result, so the engine's flow bookkeeping is the same on every backend.
+  virtual int run_flow(const FlowArgs& f);
+  // Whether run_flow of T-generation blocks is one launch for this layout.
+  virtual bool has_flow(Layout /*l*/, int /*T*/) const { return false; }
+  // Description of the last flow launch (kernel plan), or "".
+  virtual std::string flow_desc() const { return ""; }
   // Whether run_block may drift the frame for this layout when allowed
   // (the engine then sizes the left halo for the one-sided light cone).
   virtual bool drifts(Layout) const { return false; }

@@ -103,4 +103,26 @@ struct BlockArgs {
   bool link = false;
 };
 
+// A run of `nblk` temporal blocks of T generations as ONE persistent
+// dataflow launch (Backend::run_flow): block j reads buf[j & 1] and writes
+// buf[(j & 1) ^ 1]; its output rows are [row_lo + j*shrink, row_hi -
+// j*shrink) (shrink = T: the trapezoid of a deep-halo epoch; 0: a row ring,
+// every block over the owned rows, ring = true).  Same semantics as nblk
+// consecutive run_block calls (flags of generation gen_base + 1 + t at
+// changed[gen_base + 1 + t - flags_base]); returns the total drift.
+struct FlowArgs {
+  void* buf[2] = {nullptr, nullptr};
+  TileGeom g;
+  int T = 1;
+  int nblk = 0;
+  int64_t row_lo = 0, row_hi = 0;
+  int shrink = 0;
+  bool ring = false;
+  int64_t gen_base = 0;
+  uint32_t* changed = nullptr;
+  int64_t flags_base = 0;
+  bool allow_drift = false;
+  bool full_width = false;
+};
+
 }  // namespace gol

@@ -155,5 +155,89 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   return 0;
 }
 
+bool life_flow_has_T(int T) { return T == 8 || T == 12 || T == 16; }
+
+int launch_life_flow(const FlowArgs& a, const LifeTuning& tune, FlowState& st, hipStream_t stream) {
+  const TileGeom& g = a.g;
+  if (g.layout != Layout::Bits || words_per_lane(g.layout, tune) != 1 || a.nblk < 1 || !life_flow_has_T(a.T) ||
+      !tune.chain_mem)
+    return -1;
+  const int64_t rows_min = (a.row_hi - a.row_lo) - 2 * int64_t(a.nblk - 1) * a.shrink;
+  GOL_REQUIRE(a.shrink >= 0 && a.row_lo - a.T >= 0 && a.row_hi + a.T <= g.R() && rows_min > 0 &&
+                  (a.shrink == 0 || a.shrink == a.T) && (!a.ring || (a.shrink == 0 && a.row_lo == g.Dv &&
+                                                                      a.row_hi == g.Dv + g.H)),
+              "life_flow: row ranges outside the tile");
+  GOL_REQUIRE(g.Wp() < (int64_t(1) << 30) && g.pitch < (int64_t(1) << 30) && g.pitch >= 4 * g.Wp() &&
+                  g.R() < (int64_t(1) << 30),
+              "life_flow: row geometry");
+  FlowParams f{};
+  LifeBlockParams& p = f.p;
+  p.pitch = g.pitch;
+  p.row_lo = a.row_lo;
+  p.row_hi = a.row_hi;
+  p.Wp = int(g.Wp());
+  p.own_w0 = int(g.cell0() / 32);
+  p.own_w1 = int(ceil_div(g.cell0() + g.W, 32));
+  const int64_t tail = (g.cell0() + g.W) % 32;
+  p.last_mask = tail ? (0xFFFFFFFFu >> (32 - tail)) : 0xFFFFFFFFu;
+  p.err = tune.err;
+  p.wrap_w = a.full_width && tune.wrap && g.W % 32 == 0 ? int(g.W / 32) : 0;
+  // A ring's blocks read rows across the torus seam: its halo rows must be the
+  // aliases, and every read of a block stays inside [row_lo - T, row_hi + T).
+  f.buf[0] = static_cast<uint8_t*>(a.buf[0]);
+  f.buf[1] = static_cast<uint8_t*>(a.buf[1]);
+  f.changed0 = a.changed ? a.changed + (a.gen_base + 1 - a.flags_base) : nullptr;
+  f.rows0 = a.row_hi - a.row_lo;
+  f.ring_rows = a.ring ? g.H : 0;
+  f.shrink = a.shrink;
+  f.nblk = a.nblk;
+  f.spin_log2 = tune.flow_spin_log2;
+  f.trace = st.trace;
+  // Window: the adder window (drifting frame) where the engine allows a
+  // drift and the one-sided light cone of the whole run fits the left halo.
+  int x = xlane_of(g.layout, 1, tune);
+  if (x == kXlaneAuto) x = kXlaneAdd;
+  if (x == kXlaneAdd &&
+      !(a.allow_drift && (p.wrap_w > 0 || 32 * int64_t(g.hw) >= 2 * int64_t(a.T) * a.nblk)))
+    x = kXlaneDpp;
+  if (x != kXlaneAdd && x != kXlaneDpp) return -1;
+  constexpr int kWaveOut = 63;  // both windows: 64 lanes, halo lane(s) excluded below
+  const int wave_out = x == kXlaneAdd ? kWaveOut : 62;
+  p.ncolw = int(ceil_div(p.wrap_w ? p.wrap_w : p.Wp, wave_out));
+  p.fold = 1;
+  p.fold_lanes = 64;
+  if (p.wrap_w && tune.fold && p.ncolw >= 2 && (f.rows0 + 2) * p.pitch < (int64_t(1) << 30)) {
+    const int lanes = p.wrap_w - (p.ncolw - 1) * wave_out + (x == kXlaneAdd ? 1 : 2);
+    const int fo = std::min(4, 64 / lanes);
+    if (fo >= 2) {
+      p.fold = fo;
+      p.fold_lanes = lanes;
+    }
+  }
+  // Tickets and completion words (monotonic; FlowParams).
+  f.counter = tune.chain_mem(9, 256);
+  const int max_items = int(ceil_div(int64_t(p.ncolw) * rows_min, int64_t(2 * a.T)));  // any plan's item bound
+  f.done = tune.chain_mem(8, size_t(std::max(1, max_items)) * 4);
+  if (st.counter != f.counter) {  // (re)allocated and zeroed
+    st.counter = f.counter;
+    st.ticket = 0;
+  }
+  f.base = st.ticket;
+  f.seq0 = st.seq + 1;
+  std::string desc;
+  int64_t tickets = 0;
+  int items = 0;
+  const bool ok = (x == kXlaneAdd ? launch_flow_bits_add : launch_flow_bits_dpp)(f, rows_min, a.T, tune, stream, &desc,
+                                                                                  &tickets, &items);
+  if (!ok) return -1;
+  st.ticket += uint32_t(tickets);  // every item, plus one ticket past the last per workgroup
+  st.items = items;
+  st.seq += uint32_t(a.nblk);
+  ++st.launches;
+  st.blocks += a.nblk;
+  st.last = (x == kXlaneAdd ? "adder " : "dpp ") + desc;
+  return x == kXlaneAdd ? a.T * a.nblk : 0;
+}
+
 }  // namespace hipk
 }  // namespace gol

@@ -88,6 +88,76 @@ struct LifeBlockParams {
 
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
 
+// ---- Persistent dataflow launch (life_flow_impl.hpp) -----------------------
+// Work items of one temporal block: (column strip, group of M wave segments),
+// the grouped schedule's workgroup.  Items are ordered by row position, every
+// strip of a position before the next position; with a folded last strip
+// (fold > 1) its item for groups [f*fold, f*fold + fold) comes right after
+// the other strips of its last group.  slot() is an item's index in that
+// order and names its completion word.
+struct FlowOrder {
+  int nseg;  // groups per strip
+  int nn;    // strips with one group per item (all but a folded last strip)
+  int fold;  // groups per item of the folded last strip (1: none)
+  __host__ __device__ int start(int pos) const { return fold > 1 ? nn * pos + pos / fold : nn * pos; }
+  __host__ __device__ int items() const { return fold > 1 ? nn * nseg + (nseg + fold - 1) / fold : nn * nseg; }
+  __host__ __device__ int fold_pos(int f) const { return (f * fold + fold < nseg ? f * fold + fold : nseg) - 1; }
+  // Item slot of (strip, group); strip == nn is the folded strip.
+  __host__ __device__ int slot(int strip, int g) const {
+    return (fold > 1 && strip == nn) ? start(fold_pos(g / fold)) + nn : start(g) + strip;
+  }
+  // Position (row group) of slot s; *r = s - start(pos) (r == nn: the fold item).
+  __host__ __device__ int pos_of(int s, int* r) const {
+    int p = fold > 1 ? int((int64_t(s) * fold) / (int64_t(nn) * fold + 1)) : s / (nn > 0 ? nn : 1);
+    if (p > nseg - 1) p = nseg - 1;
+    while (p + 1 < nseg && start(p + 1) <= s) ++p;
+    while (p > 0 && start(p) > s) --p;
+    *r = s - start(p);
+    return p;
+  }
+};
+
+// Kernel argument of a flow launch.  `p` carries the tile geometry and the
+// group plan shared by every block (ncolw, nseg, grp_q, fold, wrap_w, ...);
+// the kernel derives each block's in/out, row range and balanced group sizes
+// from it.  Tickets come from a monotonic counter (this launch's first
+// ticket is `base`); completion words are per item slot and monotonic too
+// (block j publishes seq0 + j), so neither is cleared between launches.
+struct FlowParams {
+  LifeBlockParams p;     // block 0's plan (row_lo, seg_rows/rem of block 0)
+  uint8_t* buf[2];       // block j: buf[j & 1] -> buf[(j & 1) ^ 1]
+  uint32_t* changed0;    // flags of block 0's first generation (null: none)
+  uint32_t* done;        // completion word per item slot
+  uint32_t* counter;     // ticket counter
+  int64_t rows0;         // block 0's output rows
+  int64_t ring_rows;     // > 0: rows wrap modulo this (row ring: owned rows)
+  uint32_t seq0;
+  uint32_t base;
+  int shrink;            // rows per side each block's range shrinks by
+  int nblk;
+  int items;             // per block (FlowOrder::items)
+  int nn;                // FlowOrder::nn
+  int rotate;            // ring: block j starts at row position j (dependencies sit a block back)
+  int spin_log2;         // dependency wait bound (log2 of polls)
+  // Diagnostics (GOL_FLOW_TRACE): per item i (local ticket), {workgroup |
+  // XCC_ID << 32 | HW_ID << 40 (CU, SIMD bits), t_dequeued, t_ready (after
+  // the dependency wait), t_done} in s_memrealtime ticks (100 MHz).
+  uint64_t* trace;
+};
+
+// Backend-owned state of flow launches (HipBackend).
+struct FlowState {
+  uint32_t* counter = nullptr;  // one word, zeroed at allocation
+  uint32_t ticket = 0;          // counter value at the next launch
+  uint32_t* done = nullptr;
+  size_t done_words = 0;
+  uint32_t seq = 0;             // last published block sequence number
+  int64_t launches = 0, blocks = 0;
+  std::string last;             // description of the last flow launch (T, M, groups, grid)
+  uint64_t* trace = nullptr;    // GOL_FLOW_TRACE: the traced launch's records (FlowParams::trace)
+  int items = 0;                // items per block of the last launch
+};
+
 // Cross-lane primitive that moves the edge words between lanes.
 //   kXlaneAdd: no cross-lane data op at all.  The horizontal window is
 //   one-sided (cells x-2, x-1, x): both shifts are add-with-carry
@@ -174,6 +244,11 @@ struct LifeTuning {
   uint32_t* err = nullptr;       // LifeBlockParams::err (4 words: code, then a give-up's diagnostics)
   int chain_spin_log2 = 16;      // LifeBlockParams::chain_spin_log2
   bool chain_acquire = true;     // LifeBlockParams::chain_acquire (GOL_CHAIN_ACQUIRE)
+  // Flow launches (life_flow_impl.hpp): waves per item (4 or 8; 0 = by the
+  // planner) and groups per strip (0 = by the planner).
+  int flow_m = 0;
+  int flow_nseg = 0;
+  int flow_spin_log2 = 20;
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).
   std::function<void*(size_t)> scratch;
 };
@@ -181,6 +256,20 @@ struct LifeTuning {
 // Returns the storage-frame drift of the launch in cells (T for the adder
 // window, 0 otherwise; BlockArgs::allow_drift).
 int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream);
+// A run of temporal blocks as one persistent dataflow launch
+// (life_flow_impl.hpp).  Returns the drift (nblk * T with the adder
+// window), or -1 when no flow plan fits (nothing launched: the caller runs
+// the blocks one by one).
+int launch_life_flow(const FlowArgs& a, const LifeTuning& tune, FlowState& st, hipStream_t stream);
+// Whether a flow kernel is compiled for T (bit layout, one word per lane).
+bool life_flow_has_T(int T);
+// Compiled flow windows (life_flow_*.hip): plan, launch, and the description
+// of the launch in *desc; false when no plan fits.
+#define GOL_FLOW_VARIANT(name)                                                                             \
+  bool name(const FlowParams& f, int64_t rows_min, int T, const LifeTuning& tune, hipStream_t s, std::string* desc, \
+            int64_t* tickets, int* items)
+GOL_FLOW_VARIANT(launch_flow_bits_add);
+GOL_FLOW_VARIANT(launch_flow_bits_dpp);
 // Description of the kernel variant the tuning selects for a layout.
 std::string life_block_variant(Layout layout, const LifeTuning& tune);
 // Largest T that keeps 2 waves/SIMD for the variant's words-per-lane.

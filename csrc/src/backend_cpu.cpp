@@ -98,7 +98,13 @@ class CpuBackend final : public Backend {
     const char* ring = std::getenv("GOL_CPU_RING");
     ring_ = ring && *ring && *ring != '0';
     ring_fail_ = ring && std::string(ring) == "fail";  // tests: the mapping fails after the size check
+    const char* flow = std::getenv("GOL_CPU_FLOW");
+    flow_ = flow && *flow && *flow != '0';
   }
+  // GOL_CPU_FLOW=1: the engine hands runs of equal blocks to run_flow (the
+  // HIP backend's persistent dataflow launch); the base class runs them
+  // block by block, so the engine's flow bookkeeping is testable on the CPU.
+  bool has_flow(Layout, int T) const override { return flow_ && T >= 2; }
   ~CpuBackend() override {
     for (auto& kv : rings_) ::munmap(kv.first, kv.second);
   }
@@ -231,6 +237,7 @@ class CpuBackend final : public Backend {
   bool resident_ = false;  // GOL_CPU_RESIDENT
   bool ring_ = false;      // GOL_CPU_RING
   bool ring_fail_ = false;  // GOL_CPU_RING=fail
+  bool flow_ = false;       // GOL_CPU_FLOW
   std::mutex ring_mu_;
   std::map<void*, size_t> rings_;  // row rings: base -> mapped bytes
 };

@@ -135,11 +135,28 @@ class HipBackend final : public Backend {
       tune_.link_force = env_int("GOL_LINK_FORCE", 0) != 0;
     }
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
+    // Persistent dataflow launches (life_flow_impl.hpp): GOL_FLOW=0 turns
+    // them off; GOL_FLOW_M / GOL_FLOW_NSEG pin the planner's waves per item
+    // and groups per strip (sweeps).
+    flow_on_ = env_int("GOL_FLOW", 0) != 0;
+    tune_.flow_m = env_int("GOL_FLOW_M", 0);
+    tune_.flow_nseg = env_int("GOL_FLOW_NSEG", 0);
+    tune_.flow_spin_log2 = std::min(26, std::max(8, env_int("GOL_FLOW_SPIN", 20)));
+    if (const char* t = std::getenv("GOL_FLOW_TRACE")) {
+      const std::string v(t);
+      const size_t c = v.find(':');
+      if (c != std::string::npos) {
+        flow_trace_at_ = std::atoi(v.substr(0, c).c_str());
+        flow_trace_path_ = v.substr(c + 1);
+      }
+    }
     if (!hipk::kExperimentalBuild) refuse_experimental();
     tune_log_ = env_int("GOL_TUNE_LOG", 0) != 0;
     tune_.chain_seq = &chain_seq_;
-    // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words
-    // (zeroed when allocated: flags and words are compared with sequence numbers).
+    // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words,
+    // 5..7 resident mirrors and flags, 8 flow completion words, 9 the flow
+    // ticket counter (zeroed when allocated: flags and words are compared with
+    // sequence numbers).
     tune_.chain_mem = [this](int which, size_t n) -> uint32_t* {
       void*& buf = chain_[which];
       size_t& cap = chain_bytes_[which];
@@ -198,11 +215,12 @@ class HipBackend final : public Backend {
                    "(launch call %.2f us)\n", (long long)prof_n_, prof_gap_ / double(std::max<int64_t>(1, prof_n_ - 1)),
                    prof_in_ / double(prof_n_), prof_launch_ / double(prof_n_));
     DeviceScope device_scope(dev_);
+    // Every stream drains before any ring is unmapped: linked launches on
+    // link_.stream[1] and transport work on comm_ may still use the rings.
     if (stream_) hipStreamSynchronize(stream_);
-    for (auto& kv : rings_) release_ring(kv.second);
     if (link_.stream[1]) hipStreamSynchronize(link_.stream[1]);
-    if (stream_) hipStreamSynchronize(stream_);
     if (comm_) hipStreamSynchronize(comm_);
+    for (auto& kv : rings_) release_ring(kv.second);
     if (stage_) hipFree(stage_);
     if (scratch_) hipFree(scratch_);
     for (void* c : chain_)
@@ -232,6 +250,59 @@ class HipBackend final : public Backend {
     }
   }
   int64_t linked_launches() const override { return link_.linked; }
+  bool has_flow(Layout l, int T) const override {
+    return flow_on_ && l == Layout::Bits && tune_.wpl_bits < 2 && hipk::life_flow_has_T(T);
+  }
+  std::string flow_desc() const override { return flow_.last; }
+  // One flow launch on the compute stream (never inside a capture: its
+  // tickets and sequence numbers are per launch); falls back to the blocks
+  // one by one when no flow plan fits the rows.
+  int run_flow(const FlowArgs& f) override {
+    GOL_ON_DEVICE();
+    join_streams();
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(stream_, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+    if (capturing) return Backend::run_flow(f);
+    if (check_dev_) {
+      check_ptr(f.buf[0], "run_flow buffer 0");
+      check_ptr(f.buf[1], "run_flow buffer 1");
+    }
+    // GOL_FLOW_TRACE=<flow launch>:<csv>: per-item timestamps of one launch
+    // (scripts/flow_trace.py: waits, item durations, concurrency).
+    const bool traced = flow_trace_at_ >= 0 && flow_.launches == flow_trace_at_;
+    size_t tbytes = 0;
+    if (traced) {
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      tbytes = size_t(f.nblk) * size_t(f.g.Wp() / 62 + 2) * size_t((f.row_hi - f.row_lo) / (2 * f.T) + 1) * 32;  // >= items x 32 B
+      HIP_CHECK(hipMalloc(&flow_.trace, tbytes));
+      HIP_CHECK(hipMemsetAsync(flow_.trace, 0, tbytes, stream_));
+    }
+    const int drift = hipk::launch_life_flow(f, tune_, flow_, stream_);
+    HIP_CHECK(hipGetLastError());
+    if (traced) {
+      std::vector<uint64_t> h(tbytes / 8);
+      HIP_CHECK(hipMemcpyAsync(h.data(), flow_.trace, tbytes, hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      HIP_CHECK(hipFree(flow_.trace));
+      flow_.trace = nullptr;
+      std::FILE* fp = std::fopen(flow_trace_path_.c_str(), "w");
+      GOL_REQUIRE(fp != nullptr, "GOL_FLOW_TRACE: cannot open " + flow_trace_path_);
+      std::fprintf(fp, "# %s\nitem,block,slot,wg,xcc,hw_id,t_deq,t_ready,t_done\n", flow_.last.c_str());
+      const int64_t n = drift >= 0 ? int64_t(f.nblk) * flow_.items : 0;
+      for (int64_t i = 0; i < n && 4 * i + 3 < int64_t(h.size()); ++i) {
+        const uint64_t* r = &h[size_t(4 * i)];
+        if (!r[3]) continue;
+        std::fprintf(fp, "%lld,%lld,%lld,%llu,%llu,%llu,%llu,%llu,%llu\n", (long long)i, (long long)(i / flow_.items),
+                     (long long)(i % flow_.items), (unsigned long long)(r[0] & 0xFFFFFFFFull),
+                     (unsigned long long)((r[0] >> 32) & 0xFF), (unsigned long long)(r[0] >> 40),
+                     (unsigned long long)r[1], (unsigned long long)r[2], (unsigned long long)r[3]);
+      }
+      std::fclose(fp);
+    }
+    if (drift < 0) return Backend::run_flow(f);
+    launches_ += 1;
+    return drift;
+  }
   std::string name() const override {
     hipk::LifeTuning t = tune_;
     t.chain = chain_mode_;
@@ -947,6 +1018,7 @@ class HipBackend final : public Backend {
                        : e == 5 ? "life_resident kernel: a wave gave up waiting for its neighbours' edge rows"
                        : e == 3 ? "life_group kernel (linked launches): a group gave up waiting for the previous "
                                   "launch's rows"
+                       : e == 6 ? "life_flow kernel: an item gave up waiting for the items of the block before it"
                                 : "life_short kernel: a wave gave up waiting for its neighbour's LDS rows") +
            " (device error word " + std::to_string(e) + "); the rows of that launch are invalid");
     }
@@ -1111,13 +1183,17 @@ class HipBackend final : public Backend {
   size_t scratch_bytes_ = 0;
   // chain_mem: chained groups' flags, slots; linked launches' 3 x completion
   // words; resident epochs' two mirrors and per-workgroup flags (5..7).
-  void* chain_[8] = {};
-  size_t chain_bytes_[8] = {};
+  void* chain_[10] = {};
+  size_t chain_bytes_[10] = {};
   int resident_mode_ = 0, resident_k_ = 8, resident_D_ = 0, resident_probe_ = 0;
   bool lds_add_ = false;  // GOL_LDS_ADD
   int64_t resident_launches_ = 0, res_trace_at_ = -1;
   std::string res_trace_path_;
   hipk::LinkState link_;  // linked launches (GOL_LINK)
+  hipk::FlowState flow_;  // flow launches: ticket counter, completion words (chain_mem 8, 9)
+  bool flow_on_ = true;   // GOL_FLOW
+  int64_t flow_trace_at_ = -1;  // GOL_FLOW_TRACE
+  std::string flow_trace_path_;
   bool link_on_ = false;  // every eligible launch (GOL_LINK=1)
   int link_mode_ = -1;
   uint32_t chain_seq_ = 0;

@@ -30,6 +30,27 @@ int64_t min_tile_rows(const Decomposition& d) { return d.H / d.Py; }
 int64_t min_tile_cols(const Decomposition& d) { return (d.W / d.col_unit / d.Px) * d.col_unit; }
 }  // namespace
 
+// Default flow: the blocks one by one (Backend::run_flow).
+int Backend::run_flow(const FlowArgs& f) {
+  int64_t drift = 0;
+  for (int j = 0; j < f.nblk; ++j) {
+    BlockArgs a;
+    a.in = f.buf[j & 1];
+    a.out = f.buf[(j & 1) ^ 1];
+    a.g = f.g;
+    a.row_lo = f.row_lo + int64_t(j) * f.shrink;
+    a.row_hi = f.row_hi - int64_t(j) * f.shrink;
+    a.T = f.T;
+    a.gen_base = f.gen_base + int64_t(j) * f.T;
+    a.changed = f.changed;
+    a.flags_base = f.flags_base;
+    a.allow_drift = f.allow_drift;
+    a.full_width = f.full_width;
+    drift += run_block(a);
+  }
+  return int(drift % std::max<int64_t>(1, f.g.W));
+}
+
 Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     : cfg_(cfg), be_(backend), tr_(transport) {
   GOL_REQUIRE(be_ && tr_, "engine needs a backend and a transport");
@@ -165,6 +186,18 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // (latency-bound), so poll half as often; a stop is still exact and at most
   // two windows late.
   poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : (tr_->size() > 1 || cfg_.self_exchange) ? 512 : 256;
+  // Flow launches (EngineConfig::flow): runs of equal blocks as one
+  // persistent launch, where the backend has the kernel for the layout and T.
+  // Not for the resident and LDS-tiled schedules (their own launches).  A
+  // ring's epoch then only paces the polls (one flow launch per poll window)
+  // and the column fills, if any: the column halos hold 32 hw cells of light
+  // cone (half with a drifting frame).
+  flow_ = cfg_.flow != 0 && be_->has_flow(cl, tmax_) && !resident_ && !rows_wrapped_;
+  if (flow_ && rows_ring_ && cfg_.epoch <= 0) {
+    int64_t cap = poll_gens_;
+    if (cols_filled_) cap = std::min<int64_t>(cap, 32 * int64_t(hw) / (drift_ok_ ? 2 : 1));
+    D_ = tmax_ * int(std::max<int64_t>(1, cap / tmax_));
+  }
 
   if (rows_ring_ && !via_bits_) {
     for (int i = 0; i < 2; ++i) buf_[i] = ring_bufs[i];
@@ -216,6 +249,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
   if (resident_) be_->reserve_resident(via_bits_ ? gb_ : g_);  // before any capture
   if (use_graphs_) early_ = comm_route_ = false;  // captured epochs stay on one stream
+  if (use_graphs_) flow_ = false;  // a flow launch takes tickets and sequence numbers: never replayed
   // Overlap auto: measure both schedules on the real ranks (see auto_choose).
   // The one-GPU RCCL rehearsal measured the early-boundary schedule slower
   // (profiles/r02/rehearsal_overlap.jsonl), but it has no xGMI latency in it;
@@ -508,6 +542,14 @@ void Engine::epoch_via_bits(int64_t d) {
   while (d > 0) {
     const int T = pick_T(d);
     if (rows_ring_) a = gb_.Dv - T;
+    if (const int n = flow_count(T, d, false)) {
+      add_drift(flow_blocks(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, n, a + T, gb_.R() - a - T, gen_));
+      bpar_ ^= n & 1;
+      gen_ += int64_t(n) * T;
+      a += int64_t(n) * T;
+      d -= int64_t(n) * T;
+      continue;
+    }
     add_drift(launch(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
     bpar_ ^= 1;
     gen_ += T;
@@ -561,6 +603,16 @@ void Engine::run_epoch(int64_t d) {
   while (d > 0) {
     const int T = pick_T(d);
     if (rows_ring_) a = g_.Dv - T;  // every block covers exactly the owned rows
+    // Runs of equal blocks as one flow launch; the early-boundary schedule
+    // keeps its split last block.
+    if (const int n = flow_count(T, d, early_ && send_next_ && full)) {
+      add_drift(flow_blocks(buf_[cur_], buf_[cur_ ^ 1], g_, T, n, a + T, g_.R() - a - T, gen_));
+      cur_ ^= n & 1;
+      gen_ += int64_t(n) * T;
+      a += int64_t(n) * T;
+      d -= int64_t(n) * T;
+      continue;
+    }
     if (d == T && early_ && send_next_ && full)
       last_block_early(T);
     else
@@ -679,6 +731,40 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   const int drift = be_->run_block(a);
   phase_end(kCompute, t, stream);
   ++launches_;
+  return drift;
+}
+
+int Engine::flow_count(int T, int64_t d, bool keep_last) const {
+  if (!flow_ || capturing_ || !be_->has_flow(via_bits_ ? Layout::Bits : cfg_.layout, T)) return 0;
+  int64_t n = d / T;
+  if (keep_last && n * T == d) --n;  // the last block runs on its own
+  return n >= 2 ? int(n) : 0;
+}
+
+int Engine::flow_blocks(void* in, void* out, const TileGeom& g, int T, int n, int64_t row_lo, int64_t row_hi,
+                        int64_t gen_base) {
+  FlowArgs f;
+  f.buf[0] = in;
+  f.buf[1] = out;
+  f.g = g;
+  f.T = T;
+  f.nblk = n;
+  f.row_lo = row_lo;
+  f.row_hi = row_hi;
+  f.shrink = rows_ring_ ? 0 : T;  // a ring's blocks all cover the owned rows; an epoch's shrink by T
+  f.ring = rows_ring_;
+  f.gen_base = gen_base;
+  const int64_t span = int64_t(n) * T;
+  f.changed = (flags_ && gen_base + span < flags_base_ + flags_len_ && gen_base >= flags_base_) ? flags_ : nullptr;
+  f.flags_base = flags_base_;
+  f.allow_drift = drift_ok_;
+  f.full_width = dec_.Px == 1 && cfg_.W % 32 == 0;
+  void* t = phase_begin(nullptr);
+  const int drift = be_->run_flow(f);
+  phase_end(kCompute, t, nullptr);
+  ++launches_;
+  ++flow_launches_;
+  flow_blocks_ += n;
   return drift;
 }
 
@@ -824,6 +910,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   const int64_t g0 = graph_runs_;
   const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_, es0 = early_sends_;
   const int64_t lk0 = be_->linked_launches();
+  const int64_t fl0 = flow_launches_, fb0 = flow_blocks_;
   trace::Range trace_run("gol.run");
   if (cfg_.timing_barriers) {
     settle_pending(false);  // one stream at a time on the communicator
@@ -921,6 +1008,8 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.graph_launches = graph_runs_ - g0;
   res.halo_bytes = halo_bytes_ - hb0;
   res.linked_launches = be_->linked_launches() - lk0;
+  res.flow_launches = flow_launches_ - fl0;
+  res.flow_blocks = flow_blocks_ - fb0;
   res.generations = limit;
   collect_phases(res);
   if (found >= 0) {

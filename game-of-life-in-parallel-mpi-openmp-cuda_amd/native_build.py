@@ -45,8 +45,10 @@ LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_add", "u8_w1_dpp", "u8_w1_add",
 EXPERIMENTAL_VARIANTS = ["bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "u8_w1_carry",
                          "u8_w1_carry_t24", "u8_w1_carry_t32"]
 RESIDENT_TUS = 9  # life_resident_rw0..8.hip: the resident kernel's rows-per-wave instantiations
+FLOW_VARIANTS = ["bits_add", "bits_dpp"]  # persistent dataflow launches (life_flow_impl.hpp)
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
-            *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
+            *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS],
+            *[f"kernels/life_flow_{v}.hip" for v in FLOW_VARIANTS], "kernels/life_step_lds.hip",
             "kernels/tile_ops.hip"]
 if EXPERIMENTAL:
     HIP_SRCS += [*[f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS], "kernels/life_resident.hip",
@@ -84,7 +86,7 @@ def _compile_cmd(src: Path, obj: Path) -> list[str]:
     inc = [f"-I{CSRC / 'include'}", f"-I{CSRC}", *(["-DGOL_EXPERIMENTAL=1"] if EXPERIMENTAL else [])]
     if src.suffix == ".hip":
         extra = []
-        if src.name.startswith("life_block_"):
+        if src.name.startswith(("life_block_", "life_flow_")):
             # Scheduler for the temporal-blocking kernels: max-ILP interleaves the
             # independent generation levels.  Measured on MI355X it is on par
             # with the default strategy (the kernel is VALU-throughput bound);
@@ -143,7 +145,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     # Longest compiles first (deep byte passes, then the kernel variants), so
     # the pool does not end on one long translation unit.
     todo.sort(key=lambda s: 0 if any(f"_t{t}" in s for t in (24, 32, 48, 64)) else
-              1 if ("life_block_" in s or "life_resident_rw" in s) else 2)
+              1 if ("life_block_" in s or "life_flow_" in s or "life_resident_rw" in s) else 2)
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]
