@@ -101,6 +101,10 @@ struct BlockArgs {
   // ordered by per-group completion words): Backend::KernelChoice::link, on
   // a single-rank ring tile whose epochs move no data between launches.
   bool link = false;
+  // The tile is a row ring (Backend::row_ring_halo) and the block covers its
+  // owned rows: rows outside them are the torus wrapped around, which a
+  // linked launch's dependency waits must follow (life_group_impl.hpp).
+  bool ring = false;
 };
 
 // A run of `nblk` temporal blocks of T generations as ONE persistent

@@ -99,6 +99,8 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   p.wrap_w = a.full_width && tune.wrap && g.W % 32 == 0 ? int(g.W / 32) : 0;
   p.fold = 1;
   p.fold_lanes = 64;
+  p.link_ring_rows = a.ring && a.row_lo == g.Dv && a.row_hi == g.Dv + g.H ? g.H : 0;
+  p.fault_delay = tune.fault_delay;
   const int64_t rows = a.row_hi - a.row_lo;
   int x = xlane_of(g.layout, w, tune);
   if (g.layout == Layout::U8 && tune.u8_lds && (a.T == 1 || a.T == 2 || a.T == 4 || a.T == 8 || a.T == 16 || a.T == 32)) {
@@ -155,9 +157,13 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   return 0;
 }
 
-bool life_flow_has_T(int T) { return T == 8 || T == 12 || T == 16; }
+bool life_flow_has_T(int T) { return kExperimentalBuild && (T == 8 || T == 12 || T == 16); }
 
 int launch_life_flow(const FlowArgs& a, const LifeTuning& tune, FlowState& st, hipStream_t stream) {
+#ifndef GOL_EXPERIMENTAL
+  (void)a, (void)tune, (void)st, (void)stream;
+  return -1;  // flow kernels are compiled into experimental builds only
+#else
   const TileGeom& g = a.g;
   if (g.layout != Layout::Bits || words_per_lane(g.layout, tune) != 1 || a.nblk < 1 || !life_flow_has_T(a.T) ||
       !tune.chain_mem)
@@ -181,6 +187,7 @@ int launch_life_flow(const FlowArgs& a, const LifeTuning& tune, FlowState& st, h
   const int64_t tail = (g.cell0() + g.W) % 32;
   p.last_mask = tail ? (0xFFFFFFFFu >> (32 - tail)) : 0xFFFFFFFFu;
   p.err = tune.err;
+  p.fault_delay = tune.fault_delay;
   p.wrap_w = a.full_width && tune.wrap && g.W % 32 == 0 ? int(g.W / 32) : 0;
   // A ring's blocks read rows across the torus seam: its halo rows must be the
   // aliases, and every read of a block stays inside [row_lo - T, row_hi + T).
@@ -237,6 +244,7 @@ int launch_life_flow(const FlowArgs& a, const LifeTuning& tune, FlowState& st, h
   st.blocks += a.nblk;
   st.last = (x == kXlaneAdd ? "adder " : "dpp ") + desc;
   return x == kXlaneAdd ? a.T * a.nblk : 0;
+#endif  // GOL_EXPERIMENTAL
 }
 
 }  // namespace hipk

@@ -59,7 +59,8 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
     return false;
   }
   const bool link = L.prev_valid && L.prev_out == q.in && L.prev.ncolw == q.ncolw && L.prev.wrap_w == q.wrap_w &&
-                    L.prev.pitch == q.pitch && L.prev_blocks + blocks <= cap;
+                    L.prev.pitch == q.pitch && L.prev.link_ring_rows == q.link_ring_rows &&
+                    L.prev_blocks + blocks <= cap;
   // Completion words of this launch: the third buffer back, so neither the
   // previous launch's words (read by this one) nor the ones before it (read by
   // the previous launch, which may still run) are overwritten.

@@ -285,6 +285,8 @@ void life_flow_kernel(const FlowParams f) {
     if (p.changed && lane < T && ((mask >> lane) & 1u)) p.changed[lane] = 1u;
     // Every wave's rows are written through, then one completion word.
     __builtin_amdgcn_s_waitcnt(0);
+    if (f.p.fault_delay && (pos == 0 || pos == ord.nseg - 1 || fold_item))  // tests: late producers at the seam
+      for (int d = 0; d < f.p.fault_delay; ++d) __builtin_amdgcn_s_sleep(127);
     __syncthreads();
     if (m == 0 && lane == 0) {
       __hip_atomic_store(f.done + s, f.seq0 + uint32_t(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

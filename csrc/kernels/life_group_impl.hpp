@@ -158,23 +158,38 @@ __device__ __forceinline__ void chain_fetch(const LifeBlockParams& p, int64_t sl
 // this one (the backend links two launches only when both fit on the GPU at
 // once), so the wait ends; bounded (~0.1 s) like chain_fetch, it raises the
 // error word 3 instead of hanging.
+//   On a row ring (link_ring_rows > 0) the rows beyond the owned ones are the
+// torus wrapped around: the top group reads the last rows and the bottom
+// group the first ones, so the groups are counted around the torus (an
+// unwrapped index, group + nseg per turn) and taken modulo nseg.
 __device__ __forceinline__ void link_wait(const LifeBlockParams& p, int kcol, int64_t r0, int64_t r1, int lane) {
   const int q1 = p.link_prev_seg_rows + 1;
   const int64_t big = int64_t(p.link_prev_seg_rem) * q1;
-  const auto grp_of = [&](int64_t r) {
-    const int64_t x = max<int64_t>(0, r - p.link_prev_row_lo);
+  const int nseg = p.link_prev_nseg;
+  const int64_t ring = p.link_ring_rows;
+  const auto grp_of = [&](int64_t r) -> int64_t {
+    int64_t x = r - p.link_prev_row_lo;
+    int64_t turns = 0;
+    if (ring > 0) {
+      turns = x >= 0 ? x / ring : -((-x + ring - 1) / ring);
+      x -= turns * ring;
+    } else {
+      x = max<int64_t>(0, x);
+    }
     const int64_t g = x < big ? x / q1 : p.link_prev_seg_rem + (x - big) / max(1, p.link_prev_seg_rows);
-    return int(min<int64_t>(g, p.link_prev_nseg - 1));
+    return turns * nseg + min<int64_t>(g, nseg - 1);
   };
-  const int g0 = grp_of(r0), g1 = grp_of(r1 - 1);
-  const int ng = g1 - g0 + 1;
+  const int64_t g0 = grp_of(r0);
+  const int ng = int(min<int64_t>(grp_of(r1 - 1) - g0 + 1, int64_t(nseg)));
   const int nflags = 3 * ng;
   for (int base = 0; base < nflags; base += 64) {
     const int f = base + lane;
     int k = kcol + f / ng - 1;
     if (p.wrap_w > 0) k = (k + p.ncolw) % p.ncolw;
     const bool mine = f < nflags && k >= 0 && k < p.ncolw;
-    const uint32_t* w = p.link_prev_flag + (int64_t(mine ? k : 0) * p.link_prev_nseg + g0 + (mine ? f % ng : 0));
+    int g = int((g0 + f % ng) % nseg);
+    if (g < 0) g += nseg;
+    const uint32_t* w = p.link_prev_flag + (int64_t(mine ? k : 0) * nseg + (mine ? g : 0));
     bool done = !mine;
     for (int spin = 0; spin < (1 << 16); ++spin) {
       if (!done) done = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.link_prev_seq;
@@ -467,6 +482,8 @@ void life_group_kernel(const LifeBlockParams p) {
   }
   if constexpr (IO::kLinked) {  // every wave's rows are written through, then one flag
     __builtin_amdgcn_s_waitcnt(0);
+    if (p.fault_delay && (grp == 0 || grp + nsub >= p.nseg))  // tests: the seam's producers publish late
+      for (int i = 0; i < p.fault_delay; ++i) __builtin_amdgcn_s_sleep(127);
     __syncthreads();
     // One word per group: a folded block publishes each of its groups.
     if (p.link_flag && m == 0 && lane < nsub && grp + lane < p.nseg)

@@ -84,6 +84,15 @@ struct LifeBlockParams {
   uint32_t link_prev_seq;
   int64_t link_prev_row_lo;
   int link_prev_nseg, link_prev_seg_rows, link_prev_seg_rem;
+  // > 0: both launches cover the owned rows of a row ring of this many rows;
+  // the rows a group reads beyond them wrap around the torus (link_wait).
+  int64_t link_ring_rows;
+  // Fault injection (GOL_FAULT_DELAY_SPINS, tests): producers at the torus
+  // seam - a linked launch's first and last groups, a flow block's first and
+  // last row positions and its folded items - sleep this many s_sleep 127
+  // rounds (~3.4 us each) before publishing, so a missing dependency wait
+  // reads stale rows deterministically instead of by chance.
+  int fault_delay;
 };
 
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
@@ -249,6 +258,7 @@ struct LifeTuning {
   int flow_m = 0;
   int flow_nseg = 0;
   int flow_spin_log2 = 20;
+  int fault_delay = 0;  // LifeBlockParams::fault_delay (GOL_FAULT_DELAY_SPINS)
   // Device scratch of at least n bytes, valid until the next call (stream-ordered).
   std::function<void*(size_t)> scratch;
 };
@@ -268,8 +278,10 @@ bool life_flow_has_T(int T);
 #define GOL_FLOW_VARIANT(name)                                                                             \
   bool name(const FlowParams& f, int64_t rows_min, int T, const LifeTuning& tune, hipStream_t s, std::string* desc, \
             int64_t* tickets, int* items)
+#ifdef GOL_EXPERIMENTAL  // measured slower than the grouped launches (docs/PERFORMANCE.md)
 GOL_FLOW_VARIANT(launch_flow_bits_add);
 GOL_FLOW_VARIANT(launch_flow_bits_dpp);
+#endif
 // Description of the kernel variant the tuning selects for a layout.
 std::string life_block_variant(Layout layout, const LifeTuning& tune);
 // Largest T that keeps 2 waves/SIMD for the variant's words-per-lane.

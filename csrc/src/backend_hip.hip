@@ -142,6 +142,7 @@ class HipBackend final : public Backend {
     tune_.flow_m = env_int("GOL_FLOW_M", 0);
     tune_.flow_nseg = env_int("GOL_FLOW_NSEG", 0);
     tune_.flow_spin_log2 = std::min(26, std::max(8, env_int("GOL_FLOW_SPIN", 20)));
+    tune_.fault_delay = std::max(0, std::min(4096, env_int("GOL_FAULT_DELAY_SPINS", 0)));
     if (const char* t = std::getenv("GOL_FLOW_TRACE")) {
       const std::string v(t);
       const size_t c = v.find(':');
@@ -1127,7 +1128,7 @@ class HipBackend final : public Backend {
     };
     static const Knob knobs[] = {{"GOL_WPL", 1},  {"GOL_SKEW", 0},     {"GOL_SPLIT", 0}, {"GOL_SHORT", 0},
                                  {"GOL_PIPE", 0}, {"GOL_RESIDENT", 0},
-                                 {"GOL_LDS_ADD", 0}};
+                                 {"GOL_LDS_ADD", 0}, {"GOL_FLOW", 0}};
     for (const Knob& k : knobs)
       if (env_int(k.name, k.dflt) != k.dflt)
         fail(std::string(k.name) + "=" + std::getenv(k.name) +

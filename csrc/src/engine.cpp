@@ -724,7 +724,11 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   a.wrap_rows = rows_wrapped_;
   a.stream = stream;
   a.resident = resident_;
-  a.link = link_;
+  // Linked launches assume the device to themselves: not while transport
+  // work may run beside them on the comm stream (early-boundary schedule,
+  // side polls).
+  a.link = link_ && !early_ && !comm_route_ && !poll_side_;
+  a.ring = rows_ring_;
   a.dual_offset = dual_offset;
   a.prio_boost = prio_boost;
   void* t = phase_begin(stream);

@@ -45,14 +45,18 @@ LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_add", "u8_w1_dpp", "u8_w1_add",
 EXPERIMENTAL_VARIANTS = ["bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "u8_w1_carry",
                          "u8_w1_carry_t24", "u8_w1_carry_t32"]
 RESIDENT_TUS = 9  # life_resident_rw0..8.hip: the resident kernel's rows-per-wave instantiations
-FLOW_VARIANTS = ["bits_add", "bits_dpp"]  # persistent dataflow launches (life_flow_impl.hpp)
+# Persistent dataflow launches (life_flow_impl.hpp): exact, measured slower
+# than the grouped launches on every tile (docs/PERFORMANCE.md "Persistent
+# dataflow launches"), so experimental builds only.
+FLOW_VARIANTS = ["bits_add", "bits_dpp"]
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
-            *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS],
-            *[f"kernels/life_flow_{v}.hip" for v in FLOW_VARIANTS], "kernels/life_step_lds.hip",
+            *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
             "kernels/tile_ops.hip"]
+EXPERIMENTAL_TUS = [*[f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS], "kernels/life_resident.hip",
+                    *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)],
+                    *[f"kernels/life_flow_{v}.hip" for v in FLOW_VARIANTS]]
 if EXPERIMENTAL:
-    HIP_SRCS += [*[f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS], "kernels/life_resident.hip",
-                 *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)]]
+    HIP_SRCS += EXPERIMENTAL_TUS
 MODE = "experimental" if EXPERIMENTAL else "default"
 BIND_SRCS = ["src/bindings.cpp"]
 CLI_MAIN = "tools/gol_main.cpp"
@@ -70,7 +74,7 @@ def _hipcc() -> str:
 
 # Headers only the experimental translation units include: editing them does
 # not make a default module stale.
-EXPERIMENTAL_HEADERS = {"kernels/life_resident_impl.hpp", "kernels/life_short_impl.hpp"}
+EXPERIMENTAL_HEADERS = {"kernels/life_resident_impl.hpp", "kernels/life_short_impl.hpp", "kernels/life_flow_impl.hpp"}
 
 
 def _headers_mtime() -> float:
@@ -193,9 +197,8 @@ def compile_experimental(verbose: bool = False, jobs: int | None = None) -> int:
     EXPERIMENTAL, BUILD = True, REPO / "build" / "obj_exp"
     try:
         BUILD.mkdir(parents=True, exist_ok=True)
-        srcs = [*[f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS], "kernels/life_resident.hip",
-                *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)], "kernels/life_block.hip",
-                "src/backend_hip.hip", "kernels/life_block_bits_w1_dpp.hip"]
+        srcs = [*EXPERIMENTAL_TUS, "kernels/life_block.hip", "src/backend_hip.hip",
+                "kernels/life_block_bits_w1_dpp.hip"]
         objs = {s: BUILD / (s.replace("/", "_") + ".o") for s in srcs}
         hdr = _headers_mtime()
         todo = [s for s in srcs if _needs(objs[s], CSRC / s, hdr)]
@@ -214,8 +217,7 @@ def build_experimental_module(out: Path, verbose: bool = False, jobs: int | None
     global EXPERIMENTAL, BUILD, HIP_SRCS
     saved = EXPERIMENTAL, BUILD, HIP_SRCS
     EXPERIMENTAL, BUILD = True, REPO / "build" / "obj_exp"
-    HIP_SRCS = HIP_SRCS + [f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS] + \
-        ["kernels/life_resident.hip", *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)]]
+    HIP_SRCS = HIP_SRCS + EXPERIMENTAL_TUS
     try:
         BUILD.mkdir(parents=True, exist_ok=True)
         srcs = HOST_SRCS + HIP_SRCS + BIND_SRCS

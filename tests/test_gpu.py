@@ -1103,3 +1103,21 @@ def test_small_ring_tiles_link_launches_by_default(gpu, monkeypatch):
         rep = sim.advance(200)
         assert rep.linked_launches > 0, layout
         assert (sim.tile() == want).all(), layout
+
+
+def test_linked_ring_late_seam_producers_vs_torch(gpu, monkeypatch):
+    """Linked launches on a row ring (the round-4 race): with
+    GOL_FAULT_DELAY_SPINS the first and last groups of every launch publish
+    ~1 ms late, so a group at the other end of the torus that read their rows
+    without waiting for them (link_wait before it wrapped the rows) would see
+    the previous generation."""
+    monkeypatch.setenv("GOL_LINK", "1")
+    monkeypatch.setenv("GOL_FAULT_DELAY_SPINS", "300")
+    W, H = 8192, 8192
+    sim = Simulation(LifeConfig(W, H, tmax=8, gen_limit=10_000), engine="hip")
+    assert sim.describe()["row_ring"]
+    g = random_grid(W, H, 8)
+    sim.load(g)
+    rep = sim.advance(8 * 12 + 3)
+    assert rep.linked_launches > 0
+    assert (sim.tile() == life_step_torch(g, 8 * 12 + 3, device="cuda")).all()
