@@ -28,6 +28,10 @@ namespace gol {
 // W x H text grid into `out` (0/1 bytes, row stride cols.size()).
 void read_text_tile(const std::string& path, int64_t W, int64_t H, Extent rows, Extent cols,
                     std::vector<uint8_t>& out);
+// The same into caller memory (row stride ld), which it fully overwrites:
+// no zero-fill of a multi-GB host buffer before the parallel read.
+void read_text_tile_into(const std::string& path, int64_t W, int64_t H, Extent rows, Extent cols, uint8_t* dst,
+                         int64_t ld);
 inline void read_text_grid(const std::string& path, int64_t W, int64_t H,
                            std::vector<uint8_t>& out) {
   read_text_tile(path, W, H, {0, H}, {0, W}, out);

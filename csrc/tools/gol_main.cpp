@@ -333,17 +333,26 @@ int run(const Options& o) {
     };
 
     auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> parse_ms(P, 0.0), load_ms(P, 0.0);
     par([&](int r) {
       Engine& e = *engines[r];
       if (o.random) {
         e.init_random(o.seed, o.density);
       } else {
-        std::vector<uint8_t> tile;
-        read_text_tile(o.input, o.W, o.H, e.rows(), e.cols(), tile);
-        e.load_cells(tile.data(), e.cols().size());
+        // Uninitialised host tile (a multi-GB zero fill would cost more than
+        // the parallel read that overwrites it).
+        const auto a = std::chrono::steady_clock::now();
+        std::unique_ptr<uint8_t[]> tile(new uint8_t[size_t(e.rows().size() * e.cols().size())]);
+        read_text_tile_into(o.input, o.W, o.H, e.rows(), e.cols(), tile.get(), e.cols().size());
+        parse_ms[r] = ms_since(a);
+        const auto b = std::chrono::steady_clock::now();
+        e.load_cells(tile.get(), e.cols().size());
+        load_ms[r] = ms_since(b);
       }
     });
     read_ms = ms_since(t0);
+    const double read_parse_ms = *std::max_element(parse_ms.begin(), parse_ms.end());
+    const double read_load_ms = *std::max_element(load_ms.begin(), load_ms.end());
     // Generation loop, in chunks of --checkpoint-every generations when
     // checkpointing (each chunk ends with every rank's tile on disk).
     std::vector<RunResult> results(P);
@@ -408,16 +417,21 @@ int run(const Options& o) {
     }
     res = total;
 
+    std::vector<double> store_ms(P, 0.0), format_ms(P, 0.0);
     if (want_grid) {
       auto t1 = std::chrono::steady_clock::now();
       if (o.output != "none") create_text_file(o.output, o.W, o.H);
       if (o.show) final_grid.assign(size_t(o.W * o.H), 0);
       par([&](int r) {
         Engine& e = *engines[r];
-        std::vector<uint8_t> tile(size_t(e.rows().size() * e.cols().size()));
-        e.store_cells(tile.data(), e.cols().size(), false);
+        const auto a = std::chrono::steady_clock::now();
+        std::unique_ptr<uint8_t[]> tile(new uint8_t[size_t(e.rows().size() * e.cols().size())]);
+        e.store_cells(tile.get(), e.cols().size(), false);
+        store_ms[r] = ms_since(a);
+        const auto b = std::chrono::steady_clock::now();
         if (o.output != "none")
-          write_text_tile(o.output, o.W, o.H, e.rows(), e.cols(), tile.data(), e.cols().size());
+          write_text_tile(o.output, o.W, o.H, e.rows(), e.cols(), tile.get(), e.cols().size());
+        format_ms[r] = ms_since(b);
         if (o.show)
           for (int64_t i = 0; i < e.rows().size(); ++i)
             std::memcpy(&final_grid[size_t((e.rows().begin + i) * o.W + e.cols().begin)],
@@ -434,7 +448,11 @@ int run(const Options& o) {
         << ", \"H\": " << o.H << ", \"generations\": " << res.generations
         << ", \"executed\": " << res.executed << ", \"stop_reason\": \"" << res.stop_reason
         << "\", \"loop_ms\": " << res.loop_ms << ", \"read_ms\": " << read_ms
-        << ", \"write_ms\": " << write_ms << ", \"cell_updates_per_s\": " << cups
+        << ", \"read_parse_ms\": " << read_parse_ms << ", \"read_load_ms\": " << read_load_ms
+        << ", \"write_ms\": " << write_ms
+        << ", \"write_store_ms\": " << *std::max_element(store_ms.begin(), store_ms.end())
+        << ", \"write_format_ms\": " << *std::max_element(format_ms.begin(), format_ms.end())
+        << ", \"file_bytes\": " << o.H * (o.W + 1) << ", \"cell_updates_per_s\": " << cups
         << ", \"epoch\": " << engines[0]->epoch_depth() << ", \"tmax\": " << engines[0]->tmax()
         << ", \"exchanges\": " << res.exchanges << ", \"polls\": " << res.polls
         << ", \"kernel_launches\": " << res.kernel_launches << ", \"comm\": \"" << (P > 1 ? comm : "self")
