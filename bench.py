@@ -111,20 +111,33 @@ def _launch_ranks(ngpus: int, argv: list[str], out_fd: int) -> int:
     return rc
 
 
-def metric_label(S: int, Hg: int, gps: int) -> tuple[str, bool, int | None]:
+def metric_label(S: int, Hg: int, gps: int, rehearsal: str | None = None) -> tuple[str, bool, int | None]:
     """(metric, headline, config_id) of a run.  Only the BASELINE.json grid and
     generation count carry the headline metric string; any other grid names
     itself.  config_id is the BASELINE.json config the grid belongs to (1-5:
     256^2 CPU plumbing, 8192^2 byte tile, 32768^2 node, 65536^2 bits,
-    1048576^2 bytes), None for an experiment's grid."""
+    1048576^2 bytes), None for an experiment's grid.  A rehearsal (ranks
+    sharing GPUs, or one rank exchanging with itself through RCCL) is never a
+    headline or a BASELINE config, whatever its grid: its metric names it,
+    e.g. "(rehearsal: 8 ranks on 1 GPU)"."""
+    grid = f"{S}^2" if S == Hg else f"{S}x{Hg}"
+    if rehearsal:
+        return f"cell-updates/sec, {grid} x {gps} gens (rehearsal: {rehearsal})", False, None
     headline = (S, Hg, gps) == HEADLINE
-    if headline:
-        metric = METRIC
-    else:
-        grid = f"{S}^2" if S == Hg else f"{S}x{Hg}"
-        metric = f"cell-updates/sec (whole node), {grid} x {gps} gens"
+    metric = METRIC if headline else f"cell-updates/sec (whole node), {grid} x {gps} gens"
     ids = {256: 1, 8192: 2, 32768: 3, 65536: 4, 1048576: 5}
     return metric, headline, (ids.get(S) if S == Hg else None)
+
+
+def rehearsal_label(world: int, shared: bool, self_rccl: bool, infos: list[dict]) -> str | None:
+    """What a rehearsal ran on, or None for a real run: ranks that share GPUs
+    (--share-gpus), or the one-rank RCCL self-exchange (--rehearse-rccl)."""
+    gpus = len({(i.get("host"), i.get("uuid") or i.get("pci_bus_id")) for i in infos}) or 1
+    if shared:
+        return f"{world} ranks on {gpus} GPU{'s' if gpus > 1 else ''}"
+    if self_rccl:
+        return "1 rank exchanging with itself through RCCL"
+    return None
 
 
 # The fp32 oracle runs on the whole grid up to 2^30 cells (the headline
@@ -167,11 +180,11 @@ def check_ranks(world: int, shared: bool, comm_count: int, infos: list[dict]) ->
     if len(infos) != world or sorted(i["rank"] for i in infos) != list(range(world)):
         return f"{len(infos)} of {world} ranks reported their device"
     if not shared:
-        # One logical device per rank: (host, PCI bus id, device ordinal).  The
-        # ordinal is part of the key so that partitions of one physical GPU
-        # (which may share a bus id) still count as distinct devices.
-        keys = [(i.get("host"), i["pci_bus_id"], i.get("device")) for i in infos if i.get("pci_bus_id")]
-        dup = sorted({k[1] for k in keys if keys.count(k) > 1})
+        # One physical device (or partition) per rank, named by (host, device
+        # UUID, PCI bus id) - never the process-local ordinal, which differs
+        # between ranks that see one GPU under different HIP_VISIBLE_DEVICES.
+        keys = [(i.get("host"), i.get("uuid"), i["pci_bus_id"]) for i in infos if i.get("pci_bus_id")]
+        dup = sorted({k[2] for k in keys if keys.count(k) > 1})
         if dup:
             return f"ranks share GPU(s) {dup} without --share-gpus: n_gpus would overstate the GPUs used"
     return None
@@ -288,6 +301,7 @@ def main() -> int:
     me = {"rank": rank, "local_rank": local, "host": socket.gethostname(),
           "device": (int(backend.device()) if on_gpu else "cpu"),
           "pci_bus_id": (native().hip_pci_bus_id(int(backend.device())) if on_gpu else None),
+          "uuid": (native().hip_uuid(int(backend.device())) if on_gpu else None),
           "comm_device": transport.comm_device()}
     if dist is not None:
         infos = [None] * world
@@ -411,7 +425,8 @@ def main() -> int:
             dist.barrier()
 
     desc = sim.describe()
-    metric, headline, config_id = metric_label(S, Hg, gps)
+    rehearsal = rehearsal_label(world, shared, bool(a.rehearse_rccl and world == 1 and on_gpu), infos)
+    metric, headline, config_id = metric_label(S, Hg, gps, rehearsal)
     if rank == 0:
         rec = {
             "metric": metric,
@@ -468,6 +483,7 @@ def main() -> int:
                 "phase_ms_one_step": phases,
                 "verify": verify,
                 "shared_gpus": shared,
+                "rehearsal": rehearsal,
                 "baseline": "8.9e8 cell-updates/s (best reference run in BASELINE.md: MPI, 4 ranks, 2048^2, CPU)",
             },
         }

@@ -140,5 +140,6 @@ std::vector<uint8_t> rccl_unique_id();
 bool rccl_available();
 // PCI bus id ("0000:05:00.0") of a HIP device: which physical GPU a rank ran on.
 std::string hip_pci_bus_id(int device);
+std::string hip_uuid(int device);
 
 }  // namespace gol

@@ -135,6 +135,7 @@ PYBIND11_MODULE(_gol, m) {
         py::arg("device") = 0);
   m.def("hip_available", &hip_available);
   m.def("hip_pci_bus_id", &hip_pci_bus_id);
+  m.def("hip_uuid", &hip_uuid);
   m.def("experimental_build", &experimental_build);
 
   py::class_<Transport, std::shared_ptr<Transport>>(m, "Transport")

@@ -19,6 +19,10 @@
 namespace gol {
 namespace {
 
+// Grids checkpoint_begin created that no commit has taken over yet, one name
+// per line (the orphan sweep's only source of names).
+constexpr const char* kInflightName = ".gol-inflight";
+
 void mkdirs(const std::string& dir) {
   std::string cur;
   for (size_t i = 0; i <= dir.size(); ++i) {
@@ -105,6 +109,14 @@ std::string checkpoint_begin(const std::string& dir, int64_t W, int64_t H, int64
   std::string name = "grid-" + std::to_string(generation) + ".txt";
   if (name == committed) name = "grid-" + std::to_string(generation) + "b.txt";
   const std::string path = dir + "/" + name;
+  // Record the grid as this run's before creating it: a commit only ever
+  // sweeps grids a checkpoint of ours created (an interrupted one's), never
+  // a user's file that happens to be named like one.
+  {
+    std::ofstream in(dir + "/" + kInflightName, std::ios::app);
+    if (!in || !(in << name << "\n") || !in.flush())
+      fail("checkpoint: cannot record the in-flight grid in '" + dir + "/" + kInflightName + "'");
+  }
   create_text_file(path, W, H);
   return path;
 }
@@ -133,17 +145,18 @@ void checkpoint_commit(const std::string& dir, const std::string& grid_path, Che
     fail("cannot publish checkpoint metadata '" + fin + "': " + std::strerror(errno));
   fsync_path(dir, true);
   // The committed checkpoint no longer needs the previous grid, nor any grid
-  // an interrupted checkpoint left behind (crash between begin and commit).
+  // an interrupted checkpoint of ours left behind (crash between begin and
+  // commit): exactly the names checkpoint_begin recorded in the in-flight
+  // list, which is then cleared.
   if (!previous.empty() && previous != m.grid) std::remove((dir + "/" + previous).c_str());
-  if (DIR* d = ::opendir(dir.c_str())) {
-    std::vector<std::string> orphans;
-    while (const dirent* e = ::readdir(d)) {
-      const std::string n = e->d_name;
-      if (n != m.grid && n.compare(0, 5, "grid-") == 0 && checkpoint_grid_name_ok(n)) orphans.push_back(n);
-    }
-    ::closedir(d);
-    for (const auto& n : orphans) std::remove((dir + "/" + n).c_str());
+  const std::string inflight = dir + "/" + kInflightName;
+  {
+    std::ifstream in(inflight);
+    std::string n;
+    while (std::getline(in, n))
+      if (n != m.grid && checkpoint_grid_name_ok(n)) std::remove((dir + "/" + n).c_str());
   }
+  std::remove(inflight.c_str());
 }
 
 CheckpointMeta checkpoint_load(const std::string& dir) {

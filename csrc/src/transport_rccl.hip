@@ -188,6 +188,21 @@ std::string hip_pci_bus_id(int device) {
   return id;
 }
 
+// Device UUID (hipDeviceGetUuid) as 32 hex digits: names one physical GPU or
+// partition across processes, whatever HIP_VISIBLE_DEVICES / the process-
+// local ordinal make of it.
+std::string hip_uuid(int device) {
+  hipUUID u{};
+  HIP_CHECK(hipDeviceGetUuid(&u, device));
+  static const char* hex = "0123456789abcdef";
+  std::string s;
+  for (unsigned char c : u.bytes) {
+    s.push_back(hex[c >> 4]);
+    s.push_back(hex[c & 15]);
+  }
+  return s;
+}
+
 std::unique_ptr<Transport> make_rccl_transport(const std::vector<uint8_t>& uid, int rank, int nranks,
                                                int device) {
   return std::make_unique<RcclTransport>(uid, rank, nranks, device);

@@ -30,6 +30,9 @@ from .termination import reported_generations, sim_phase_at
 
 
 _GRID_NAME = re.compile(r"grid-[0-9]+b?\.txt")
+# Grids a checkpoint created that no commit has taken over yet (one name per
+# line; the same file as csrc/src/checkpoint.cpp's kInflightName).
+INFLIGHT = ".gol-inflight"
 
 
 def grid_name_ok(name) -> bool:
@@ -91,6 +94,10 @@ def save_checkpoint(sim: Simulation, directory: str, is_root: bool = True, barri
     grid = d / name
     if is_root:
         from .io import create_text_file  # noqa: PLC0415
+        # Recorded before it exists: a commit sweeps only grids a checkpoint
+        # of ours created, never a user's file named like one.
+        with open(d / INFLIGHT, "a") as f:
+            f.write(name + "\n")
         create_text_file(str(grid), cfg.width, cfg.height)
     if barrier:
         barrier()
@@ -108,10 +115,14 @@ def save_checkpoint(sim: Simulation, directory: str, is_root: bool = True, barri
         _fsync(d, directory=True)
         if previous and previous != name and (d / previous).exists():
             (d / previous).unlink()
-        # Grids an interrupted checkpoint left behind (crash before commit).
-        for orphan in d.glob("grid-*.txt"):
-            if orphan.name != name and grid_name_ok(orphan.name):
-                orphan.unlink(missing_ok=True)
+        # Grids an interrupted checkpoint of ours left behind (crash before
+        # commit): the names in the in-flight list, which is then cleared.
+        inflight = d / INFLIGHT
+        if inflight.exists():
+            for orphan in inflight.read_text().split():
+                if orphan != name and grid_name_ok(orphan):
+                    (d / orphan).unlink(missing_ok=True)
+            inflight.unlink(missing_ok=True)
     if barrier:
         barrier()
     return d

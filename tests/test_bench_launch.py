@@ -88,19 +88,43 @@ def test_bench_metric_label_names_the_grid():
     assert b.metric_label(65536, 65536, 1000)[2] == 4 and b.metric_label(1048576, 1048576, 1000)[2] == 5
 
 
+def test_bench_rehearsal_is_never_a_headline():
+    """VERDICT r04 Weak 5: 8 rank processes on one GPU (--share-gpus) or the
+    one-rank RCCL self-exchange carry their own metric string, headline false
+    and no BASELINE config id, even on the headline grid."""
+    b = _bench_module()
+    infos = [{"rank": r, "host": "n0", "device": 0, "pci_bus_id": "0000:05:00.0", "uuid": "ab"} for r in range(8)]
+    reh = b.rehearsal_label(8, True, False, infos)
+    assert reh == "8 ranks on 1 GPU"
+    m, head, cid = b.metric_label(32768, 32768, 1000, reh)
+    assert head is False and cid is None and m != b.METRIC and "rehearsal: 8 ranks on 1 GPU" in m
+    assert b.rehearsal_label(1, False, True, infos[:1]) == "1 rank exchanging with itself through RCCL"
+    m, head, cid = b.metric_label(32768, 32768, 1000, b.rehearsal_label(1, False, True, infos[:1]))
+    assert head is False and cid is None and "rehearsal" in m
+    two = [dict(i, uuid=str(i["rank"] % 2), pci_bus_id=f"0000:0{i['rank'] % 2}:00.0") for i in infos]
+    assert b.rehearsal_label(8, True, False, two) == "8 ranks on 2 GPUs"
+    real = [dict(i, uuid=str(i["rank"]), pci_bus_id=f"0000:{i['rank'] + 5:02x}:00.0") for i in infos]
+    assert b.rehearsal_label(8, False, False, real) is None
+
+
 def test_bench_check_ranks_refuses_what_rccl_did_not_see():
     """A fake communicator view: the refusal cases of bench.py's rank check
     (rccl_nranks != WORLD_SIZE, a rank missing, two ranks on one physical GPU
     without --share-gpus)."""
     b = _bench_module()
-    infos = [{"rank": r, "host": "n0", "device": r, "pci_bus_id": f"0000:{r + 5:02x}:00.0"} for r in range(8)]
+    infos = [{"rank": r, "host": "n0", "device": r, "pci_bus_id": f"0000:{r + 5:02x}:00.0", "uuid": f"u{r}"}
+             for r in range(8)]
     assert b.check_ranks(8, False, 8, infos) is None
     assert "7 ranks" in b.check_ranks(8, False, 7, infos)
     assert "7 of 8" in b.check_ranks(8, False, 8, infos[:7])
-    same = [dict(i, pci_bus_id="0000:05:00.0", device=0) for i in infos]  # eight ranks on one device
+    same = [dict(i, pci_bus_id="0000:05:00.0", uuid="u0", device=0) for i in infos]  # eight ranks on one device
     assert "share GPU" in b.check_ranks(8, False, 8, same)
     assert b.check_ranks(8, True, 8, same) is None  # --share-gpus: a declared rehearsal
-    # Partitions of one physical GPU may share a bus id but are distinct devices.
+    # ADVICE r04: one GPU seen under different process-local ordinals (per-rank
+    # HIP_VISIBLE_DEVICES) is still one GPU.
+    renamed = [dict(i, pci_bus_id="0000:05:00.0", uuid="u0") for i in infos]
+    assert "share GPU" in b.check_ranks(8, False, 8, renamed)
+    # Partitions of one physical GPU may share a bus id but have UUIDs of their own.
     parts = [dict(i, pci_bus_id="0000:05:00.0") for i in infos]
     assert b.check_ranks(8, False, 8, parts) is None
 

@@ -251,22 +251,34 @@ def test_tampered_meta_grid_name_is_refused(gol_bin, native, tmp_path, bad):
 @pytest.mark.parametrize("writer", ["native", "python"])
 def test_commit_removes_orphans_of_interrupted_checkpoints(gol_bin, native, tmp_path, writer):
     """Grid files of checkpoints that crashed before their commit (about 1 GiB
-    each at 32768^2) are removed by the next successful commit; files that do
-    not look like checkpoint grids are left alone."""
+    each at 32768^2) are removed by the next successful commit - and only
+    those: a user's files in the directory survive, even when they are named
+    like checkpoint grids (the sweep takes its names from the
+    in-flight list checkpoint_begin writes, not from a name pattern)."""
     ck = tmp_path / "ck"
     ck.mkdir()
-    for stray in ("grid-7.txt", "grid-12b.txt"):
+    for stray in ("grid-7.txt", "grid-12b.txt"):  # a user's files, never created by a checkpoint
         (ck / stray).write_text("0\n")
     (ck / "notes.txt").write_text("keep me")
     W, H = 64, 32
+    args = [W, H, "--random", "3", "--engine", "cpu", "--gens", 60, "--no-similarity", "--checkpoint-every", 20,
+            "--checkpoint-dir", ck, "--output", "none"]
     if writer == "native":
-        _bin(gol_bin, [W, H, "--random", "3", "--engine", "cpu", "--gens", 60, "--no-similarity",
-                       "--checkpoint-every", 20, "--checkpoint-dir", ck, "--output", "none"], tmp_path)
-        want = "grid-40.txt"
+        # Crash after the 2nd checkpoint's grid is written, before its commit:
+        # grid-40.txt is an orphan on the in-flight list.
+        env = dict(os.environ, GOL_FAULT_CHECKPOINT_CRASH="2")
+        r = subprocess.run([str(gol_bin), *map(str, args)], cwd=tmp_path, env=env, capture_output=True, text=True)
+        assert r.returncode == 86
+        assert (ck / "grid-40.txt").exists() and (ck / ".gol-inflight").exists()
+        _bin(gol_bin, [*args[:-4], "--checkpoint-every", 30, "--checkpoint-dir", ck, "--output", "none"], tmp_path)
+        want = "grid-30.txt"
     else:
         sim = Simulation(LifeConfig(W, H, check_similarity=False), engine="cpu")
         sim.load(random_grid(W, H, 3))
         sim.advance(20)
+        (ck / ".gol-inflight").write_text("grid-17.txt\n")  # as an interrupted save leaves it
+        (ck / "grid-17.txt").write_text("0\n")
         save_checkpoint(sim, str(ck))
         want = "grid-20.txt"
-    assert sorted(p.name for p in ck.iterdir()) == sorted([want, "meta.json", "notes.txt"])
+    assert sorted(p.name for p in ck.iterdir()) == sorted([want, "meta.json", "notes.txt", "grid-7.txt",
+                                                           "grid-12b.txt"])
