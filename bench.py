@@ -144,8 +144,9 @@ def rehearsal_label(world: int, shared: bool, self_rccl: bool, infos: list[dict]
 # grid); larger grids are checked on row bands with their light cones.
 ORACLE_WHOLE_CELLS = 1 << 30
 ORACLE_BAND_ROWS = 128
-# Beyond this the verification step is skipped (host copies of the grid and
-# the byte-layout engine would not fit): 2^34 cells = 16 GiB per byte copy.
+# Several ranks gather the whole grid for the check up to this size (2^34
+# cells = 16 GiB per byte copy); one rank checks any size on bands read
+# straight from the device (Engine.store_rows), with no whole-grid host copy.
 VERIFY_MAX_CELLS = 1 << 34
 
 
@@ -153,6 +154,19 @@ def band_starts(H: int) -> list[int]:
     """First rows of the oracle bands: top, middle and bottom of the torus."""
     b = min(ORACLE_BAND_ROWS, H)
     return sorted({0, max(0, H // 2 - b // 2), max(0, H - b)})
+
+
+def wrapped_rows(eng, H: int, r0: int, n: int):
+    """Rows r0 .. r0 + n - 1 of the torus (indices mod H) from the device, in
+    contiguous pieces (Engine.store_rows)."""
+    import numpy as np  # noqa: PLC0415
+
+    parts, r, left = [], r0 % H, n
+    while left > 0:
+        k = min(left, H - r)
+        parts.append(eng.store_rows(r, k))
+        r, left = 0, left - k
+    return np.concatenate(parts, axis=0)
 
 
 def band_oracle(snap, r0: int, gens: int, device: str):
@@ -225,6 +239,8 @@ def parse_args(argv=None):
     ap.add_argument("--verify", type=int, default=240,
                     help="after the timed steps, run G more generations and check them against the fp32 "
                          "PyTorch oracle and the u8 layout (0: skip)")
+    ap.add_argument("--verify-bands", action="store_true",
+                    help="check on row bands read from the device even below 2^30 cells (one rank; tests)")
     ap.add_argument("--no-phase-step", action="store_true",
                     help="skip the extra per-phase-timed step after the timed ones")
     return ap.parse_args(argv)
@@ -377,11 +393,39 @@ def main() -> int:
     # continues from its current state; the oracle restarts from a snapshot.
     verify = None
     verified = None
-    if a.verify > 0 and S * Hg > VERIFY_MAX_CELLS:
-        # Host copies of the whole grid (snapshot, result) and a second byte-
-        # layout engine do not fit beside a grid this large.
-        log(f"bench.py: --verify skipped: {S}x{Hg} exceeds {VERIFY_MAX_CELLS} cells")
-        verify = {"skipped": f"grid beyond {VERIFY_MAX_CELLS} cells"}
+    if a.verify > 0 and (S * Hg > ORACLE_WHOLE_CELLS or a.verify_bands) and world == 1:
+        # One rank, a grid beyond the whole-grid oracle (up to 1048576^2 on one
+        # GPU): top, middle and bottom row bands with their light cones are read
+        # from the device before and after G generations - no whole-grid host
+        # copy, so no size limit - and checked against the fp32 oracle.
+        from gol_amd.ops.life_ops import life_step_torch_roll  # noqa: PLC0415
+
+        t_v = time.perf_counter()
+        g_snap = sim.generation
+        G, b = a.verify, min(ORACLE_BAND_ROWS, Hg)
+        starts = band_starts(Hg)
+        snaps = [wrapped_rows(eng, Hg, r0 - G, b + 2 * G) for r0 in starts]
+        rv = eng.run_until(g_snap + G)
+        done = sim.generation - g_snap
+        dev = "cuda" if on_gpu else "cpu"
+        ok_torch = True
+        for r0, snap in zip(starts, snaps):
+            # A run that stopped early ran `done` generations; its cone is the
+            # middle b + 2 done rows of the snapshot.
+            cone = snap[G - done:G + b + done]
+            want = life_step_torch_roll(cone, done, device=dev)[done:done + b]
+            ok_torch = ok_torch and bool(np.array_equal(eng.store_rows(r0, b), want))
+            del want, cone
+        del snaps
+        verified = ok_torch
+        verify = {"generations": int(done), "from_generation": int(g_snap), "stop_reason": rv.stop_reason,
+                  "oracle": f"{len(starts)} row bands of {b} read from the device (light cones of {done} rows)",
+                  "vs_torch_fp32_oracle": ok_torch, "vs_u8_layout": None,
+                  "seconds": round(time.perf_counter() - t_v, 2)}
+    elif a.verify > 0 and S * Hg > VERIFY_MAX_CELLS:
+        # Several ranks: gathering the grid for the check would not fit.
+        log(f"bench.py: --verify skipped: {S}x{Hg} on {world} ranks exceeds {VERIFY_MAX_CELLS} cells")
+        verify = {"skipped": f"grid beyond {VERIFY_MAX_CELLS} cells on several ranks"}
     elif a.verify > 0:
         from gol_amd.ops.life_ops import life_step_torch_roll  # noqa: PLC0415
         from gol_amd.parallel.dist import gather_grid  # noqa: PLC0415

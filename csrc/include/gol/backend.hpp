@@ -168,6 +168,10 @@ class Backend {
   // returns such a tile (zeroed) for a geometry with that Dv, or nullptr.
   // release() frees rings too.
   virtual int row_ring_halo(int64_t /*H*/, int64_t /*pitch*/, int /*min_halo*/) const { return 0; }
+  // Bytes the backend can still allocate (device memory free; host backends:
+  // unlimited).  The engine leaves the ring out when it would not fit beside
+  // the rest of the tile's buffers.
+  virtual size_t mem_free() const { return ~size_t(0); }
   virtual void* alloc_row_ring(const TileGeom& /*g*/) { return nullptr; }
   // Periodic self-fill of halo regions of a single tile (any tile size):
   // columns (left/right halo words of owned rows) and/or rows (full padded

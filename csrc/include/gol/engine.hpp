@@ -187,6 +187,9 @@ class Engine {
   // `grid` is the full global grid; this rank copies out its subarray.
   void load_global(const uint8_t* grid, int64_t ld);
   void store_cells(uint8_t* cells, int64_t ld, bool ascii);
+  // Owned rows [r0, r0 + n) of the tile only (0 <= r0, r0 + n <= rows()):
+  // checks a band of a grid whose whole-tile host copy would not fit.
+  void store_rows(uint8_t* cells, int64_t ld, int64_t r0, int64_t n, bool ascii);
   void init_random(uint64_t seed, double density);
   int64_t alive_count();  // local owned cells
 

@@ -376,6 +376,15 @@ class HipBackend final : public Backend {
     if ((H * pitch) % int64_t(gran) != 0 || H < 2 * dv) return 0;
     return int(dv);
   }
+  size_t mem_free() const override {
+    DeviceScope device_scope(dev_);
+    size_t fr = 0, total = 0;
+    if (hipMemGetInfo(&fr, &total) != hipSuccess) {
+      (void)hipGetLastError();
+      return ~size_t(0);
+    }
+    return fr;
+  }
   void* alloc_row_ring(const TileGeom& g) override {
     if (!ring_on_) return nullptr;
     join_streams();

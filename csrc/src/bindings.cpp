@@ -307,6 +307,17 @@ PYBIND11_MODULE(_gol, m) {
              return to_array(std::move(v), e.rows().size(), e.cols().size());
            },
            py::arg("ascii") = false)
+      // Owned rows [r0, r0 + n) only (a band of a grid too large for a host copy).
+      .def("store_rows",
+           [](Engine& e, int64_t r0, int64_t n, bool ascii) {
+             std::vector<uint8_t> v(size_t(std::max<int64_t>(0, n) * e.cols().size()));
+             {
+               py::gil_scoped_release rel;
+               e.store_rows(v.data(), e.cols().size(), r0, n, ascii);
+             }
+             return to_array(std::move(v), n, e.cols().size());
+           },
+           py::arg("r0"), py::arg("n"), py::arg("ascii") = false)
       .def("init_random", &Engine::init_random, py::arg("seed"), py::arg("density") = 0.5,
            py::call_guard<py::gil_scoped_release>())
       .def("alive_count", &Engine::alive_count, py::call_guard<py::gil_scoped_release>())

@@ -148,6 +148,15 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
       !std::getenv("GOL_PITCH_PAD")) {
     const TileGeom probe = TileGeom::make(cl, r.size(), c.size(), 0, hw);
     ring_dv = be_->row_ring_halo(probe.H, probe.pitch, tmax_);
+    // The byte layout on bit words keeps its byte tiles too: the rings must
+    // fit beside them (BASELINE config 5's share, 2 x 137 GB of bytes, has no
+    // room for 2 x 17 GB of bit rings on a 288 GB GPU; its bit words then
+    // live in the spare byte buffer with periodic fills).
+    if (ring_dv > 0 && via_bits_) {
+      const double bytes = 2.0 * double(TileGeom::make(cfg_.layout, r.size(), c.size(), 0, 0).bytes()) +
+                           2.0 * double(TileGeom::make(cl, r.size(), c.size(), ring_dv, hw).bytes());
+      if (bytes + double(size_t(1) << 31) > double(be_->mem_free())) ring_dv = 0;
+    }
     if (ring_dv > 0) {
       const TileGeom gr = TileGeom::make(cl, r.size(), c.size(), ring_dv, hw);
       try {
@@ -319,6 +328,18 @@ void Engine::store_cells(uint8_t* cells, int64_t ld, bool ascii) {
   normalize();
   be_->synchronize();
   be_->store_owned(buf_[cur_], g_, cells, ld, ascii);
+}
+
+void Engine::store_rows(uint8_t* cells, int64_t ld, int64_t r0, int64_t n, bool ascii) {
+  GOL_REQUIRE(r0 >= 0 && n >= 0 && r0 + n <= g_.H, "store_rows: rows outside the tile");
+  if (n == 0) return;
+  settle_pending(false);
+  normalize();
+  be_->synchronize();
+  // A view of the band: the same pitch and halos, its first owned row at r0.
+  TileGeom v = g_;
+  v.H = n;
+  be_->store_owned(static_cast<uint8_t*>(buf_[cur_]) + r0 * g_.pitch, v, cells, ld, ascii);
 }
 
 void Engine::init_random(uint64_t seed, double density) {

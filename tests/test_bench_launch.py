@@ -68,6 +68,37 @@ def test_bench_gpus_n_launches_n_ranks_itself(native, gpus):
     assert rec["metric"] == "cell-updates/sec (whole node), 256^2 x 100 gens"
 
 
+@pytest.mark.parametrize("height,drift", [(256, "0"), (192, "1")])
+def test_bench_band_verification_reads_rows_from_the_device(native, height, drift):
+    """The check of grids beyond 2^30 cells: row bands and
+    their light cones read straight from the engine (Engine.store_rows, no
+    whole-grid host copy), wrapped around the torus, against the fp32 oracle;
+    --verify-bands forces it on a small grid, with a drifting frame too."""
+    r = _bench([*SMALL[:4], "--height", height, *SMALL[4:], "--verify-bands"], env_extra={"GOL_CPU_DRIFT": drift})
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    v = rec["config"]["verify"]
+    assert rec["verified"] is True and v["vs_torch_fp32_oracle"] is True and v["vs_u8_layout"] is None
+    assert "read from the device" in v["oracle"] and v["generations"] == 40
+
+
+def test_store_rows_matches_the_tile(native):
+    from gol_amd import LifeConfig, Simulation, random_grid
+
+    for drift in ("0", "1"):
+        os.environ["GOL_CPU_DRIFT"] = drift
+        try:
+            sim = Simulation(LifeConfig(128, 96, tmax=4, gen_limit=100), engine="cpu")
+        finally:
+            os.environ.pop("GOL_CPU_DRIFT")
+        sim.load(random_grid(128, 96, 5))
+        sim.advance(13)
+        t = sim.tile()
+        eng = sim.native_engine
+        for r0, n in ((0, 96), (5, 17), (90, 6), (40, 0)):
+            assert (eng.store_rows(r0, n) == t[r0:r0 + n]).all(), (r0, n)
+
+
 def _bench_module():
     import importlib.util  # noqa: PLC0415
     spec = importlib.util.spec_from_file_location("gol_bench", REPO / "bench.py")
