@@ -277,11 +277,12 @@ def main() -> int:
             # own "node" (socket transport over loopback).
             shared = True
             os.environ["NCCL_HOSTID"] = f"gol-bench-rank{rank}"
-            # Resident epochs need every CU of the device for one launch, and
-            # linked launches that two of their launches fit on it at once
-            # (another rank's kernels would stretch a linked wait past its bound).
-            os.environ["GOL_RESIDENT"] = "0"
-            os.environ.setdefault("GOL_LINK", "0")
+            # Each rank of a shared GPU runs on a disjoint slice of its CUs
+            # (CU-masked streams, its RCCL kernels included), as on a node where
+            # every rank owns a GPU: the default schedule - linked launches
+            # wherever two fit on the rank's CUs - runs unchanged.
+            per = -(-world // ndev)
+            os.environ["GOL_CU_PARTITION"] = f"{local // ndev}/{per}"
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         local = local % max(1, ndev)
 
@@ -517,7 +518,10 @@ def main() -> int:
                 "flow_launches_per_step": rs[-1].flow_launches if rs else 0,
                 "flow_blocks_per_step": rs[-1].flow_blocks if rs else 0,
                 "flow_plan": desc["flow_plan"],
-                "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith("GOL_")},
+                # Knobs set by hand (bench.py's own rehearsal partition aside).
+                "env_knobs": {k: v for k, v in sorted(os.environ.items())
+                              if k.startswith("GOL_") and not (shared and k == "GOL_CU_PARTITION")},
+                "cu_partition": os.environ.get("GOL_CU_PARTITION") if shared else None,
                 "halo_bytes_per_step": rs[-1].halo_bytes if rs else 0,
                 "overlapped_halo_exchange": bool(rs and rs[-1].overlapped),
                 "overlap_mode": desc["overlap_mode"],

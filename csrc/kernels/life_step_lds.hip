@@ -23,10 +23,20 @@
 //     tile has no halo columns, the engine runs one-generation epochs with no
 //     periodic fill launches at all (each was ~5 us per epoch, a sixth of a
 //     generation at 8192^2), and every generation is exactly one launch.
-// It is HBM-bound (1 B read + 1 B write per cell-update); the temporal
-// blocking kernel (life_block_impl.hpp) is the fast path.  This one is kept
-// as the single-step u8 baseline ("8192^2 LDS-tiled u8 kernel")
-// and selected with GOL_U8_KERNEL=lds (forces T = 1).
+// The single-step kernel is HBM-bound (1 B read + 1 B write per
+// cell-update, 2.6e12 cell-updates/s at 8192^2).  The same file holds the
+// LDS-tiled family that GOL_U8_KERNEL=lds selects (with --u8-compute bytes):
+//   * life_lds_multi_kernel: T = 2, 4, 8 generations per launch on the byte
+//     tile in LDS (GOL_LDS_PACK=0);
+//   * life_lds_bits_kernel (the default of that family, T = 32; 8 and 16
+//     compiled): the byte tile is staged into LDS once, packed to bit words
+//     there, stepped T generations with the bit-sliced rule, and unpacked on
+//     the way out: 1.57e13 at 8192^2 (docs/PERFORMANCE.md).
+// BASELINE config 2 (8192^2 byte-per-cell) runs faster on the default path,
+// which is not LDS-tiled: the byte grid packed to bit words once per run and
+// stepped by the register-blocked kernels (life_block_impl.hpp,
+// Engine::epoch_via_bits), 4.0-4.2e13 - 2.6x this family.  These kernels stay
+// as the reference-shaped LDS path and the byte layout's cross-check.
 #include <type_traits>
 #include <hip/hip_runtime.h>
 

@@ -71,11 +71,17 @@ class HipBackend final : public Backend {
     check_dev_ = env_int("GOL_CHECK_DEVICE", 0) != 0;
     ring_on_ = env_int("GOL_ROW_RING", 1) != 0;
     GOL_ON_DEVICE();
-    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    stream_ = make_stream(dev_);
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
     cus_ = prop.multiProcessorCount;
+    // A CU partition (GOL_CU_PARTITION, ranks sharing a GPU): every stream of
+    // this backend runs on the slice, and launches are planned for it.
+    if (const int part = mask_cus(cu_partition_mask(cus_))) {
+      cu_part_ = " cu-partition=" + std::string(std::getenv("GOL_CU_PARTITION")) + ":" + std::to_string(part) + "CUs";
+      cus_ = part;
+    }
     tune_.cus = cus_;
     tune_.target_waves = env_int("GOL_TARGET_WAVES", 0);
     tune_.min_seg_rows = env_int("GOL_MIN_SEG_ROWS", 16);
@@ -129,10 +135,19 @@ class HipBackend final : public Backend {
     link_on_ = link_mode_ > 0;
     if (link_mode_ != 0) {
       link_.stream[0] = stream_;
-      HIP_CHECK(hipStreamCreateWithFlags(&link_.stream[1], hipStreamNonBlocking));
+      link_.stream[1] = make_stream(dev_);
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       link_.events = env_int("GOL_LINK_EVENTS", 1) != 0;
       tune_.link_force = env_int("GOL_LINK_FORCE", 0) != 0;
+    }
+    // A GPU shared by several processes (a CU partition) time-slices their
+    // queues, so a producer workgroup can be switched out for longer than a
+    // bounded cross-workgroup wait: no chained groups or linked launches there
+    // (a rank tile's launch does not fit its slice twice anyway).
+    if (!cu_part_.empty()) {
+      chain_mode_ = 0;
+      link_mode_ = 0;
+      link_on_ = false;
     }
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
     // Persistent dataflow launches (life_flow_impl.hpp): GOL_FLOW=0 turns
@@ -307,7 +322,7 @@ class HipBackend final : public Backend {
   std::string name() const override {
     hipk::LifeTuning t = tune_;
     t.chain = chain_mode_;
-    return "hip:" + std::to_string(dev_) + ":" + arch_ + " [" + hipk::life_block_variant(Layout::Bits, t) +
+    return "hip:" + std::to_string(dev_) + ":" + arch_ + cu_part_ + " [" + hipk::life_block_variant(Layout::Bits, t) +
            "; " + hipk::life_block_variant(Layout::U8, t) + "]" +
            (resident_mode_ ? " resident=" + std::string(resident_mode_ < 0 ? "auto" : "on") + " k=" +
                                  std::to_string(resident_k_)
@@ -591,7 +606,7 @@ class HipBackend final : public Backend {
   void* comm_stream() override {
     if (!comm_) {
       GOL_ON_DEVICE();
-      HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+      comm_ = make_stream(dev_);
       if (check_dev_) {
         int d = -1;
         HIP_CHECK(hipStreamGetDevice(comm_, &d));
@@ -1186,7 +1201,8 @@ class HipBackend final : public Backend {
   std::vector<hipEvent_t> timing_pool_;  // timing_mark() events
   hipStream_t stream_ = nullptr;
   std::string arch_;
-  int cus_ = 256;
+  int cus_ = 256;          // CUs this backend's launches may use (its partition, if any)
+  std::string cu_part_;    // GOL_CU_PARTITION, for name()
   hipk::LifeTuning tune_;
   hipStream_t comm_ = nullptr;
   void* scratch_ = nullptr;  // split-schedule boundary states

@@ -99,7 +99,7 @@ class RcclTransport final : public Transport {
       const char* side = std::getenv("GOL_SIDE_POLL");
       if (side && std::atoi(side) != 0) NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
     }
-    HIP_CHECK(hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking));
+    barrier_stream_ = make_stream(dev_);
     HIP_CHECK(hipMalloc(&barrier_buf_, 64));
     HIP_CHECK(hipMemsetAsync(barrier_buf_, 0, 64, barrier_stream_));  // HIP's hipMemset may return before it ran
     HIP_CHECK(hipStreamSynchronize(barrier_stream_));

@@ -1121,3 +1121,26 @@ def test_linked_ring_late_seam_producers_vs_torch(gpu, monkeypatch):
     rep = sim.advance(8 * 12 + 3)
     assert rep.linked_launches > 0
     assert (sim.tile() == life_step_torch(g, 8 * 12 + 3, device="cuda")).all()
+
+
+@pytest.mark.parametrize("overlap", ["off", "on"])
+def test_rank_tile_links_only_without_comm_stream_work(gpu, overlap):
+    """Linked launches assume the device to themselves (the "two launches
+    fit" cap counts only the pair): the engine links blocks of
+    the multi-rank schedule only while no transport work can run beside them
+    on the comm stream.  The 8-GPU rank tile's schedule, rehearsed with a
+    1-rank RCCL communicator: linked with the plain schedule, never with the
+    early-boundary one - and exact either way."""
+    native = gpu
+    W, H = 32768, 4096
+    tr = native.rccl_transport(native.rccl_unique_id(), 0, 1, 0)
+    sim = Simulation(LifeConfig(W, H, gen_limit=100_000, overlap=overlap, self_exchange=True, epoch=256),
+                     engine="hip", transport=tr)
+    g = random_grid(W, H, 77)
+    sim.load(g)
+    rep = sim.advance(600)
+    if overlap == "off":
+        assert rep.linked_launches > 0
+    else:
+        assert rep.linked_launches == 0 and rep.overlapped
+    assert (sim.tile() == life_step_torch(g, 600, device="cuda")).all()
