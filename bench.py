@@ -204,6 +204,18 @@ def check_ranks(world: int, shared: bool, comm_count: int, infos: list[dict]) ->
     return None
 
 
+def parse_tune(pairs: list[str]) -> dict:
+    """--tune key=value (repeatable) -> dict; keys and values are validated
+    by the native Tuning when the backend is made."""
+    out = {}
+    for kv in pairs:
+        k, eq, v = kv.partition("=")
+        if not eq or not k:
+            raise SystemExit(f"bench.py: --tune {kv!r}: expected key=value")
+        out[k] = v
+    return out
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,6 +253,8 @@ def parse_args(argv=None):
                          "PyTorch oracle and the u8 layout (0: skip)")
     ap.add_argument("--verify-bands", action="store_true",
                     help="check on row bands read from the device even below 2^30 cells (one rank; tests)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="runtime tuning (repeatable; python -m gol_amd.cli --tune help lists the keys)")
     ap.add_argument("--no-phase-step", action="store_true",
                     help="skip the extra per-phase-timed step after the timed ones")
     return ap.parse_args(argv)
@@ -263,6 +277,7 @@ def main() -> int:
     rank, world, local = env_rank()
     on_gpu = a.engine == "hip"
     shared = False
+    tune = parse_tune(a.tune)
     if on_gpu and world > 1:
         import torch  # noqa: PLC0415
 
@@ -278,11 +293,13 @@ def main() -> int:
             shared = True
             os.environ["NCCL_HOSTID"] = f"gol-bench-rank{rank}"
             # Each rank of a shared GPU runs on a disjoint slice of its CUs
-            # (CU-masked streams, its RCCL kernels included), as on a node where
-            # every rank owns a GPU: the default schedule - linked launches
-            # wherever two fit on the rank's CUs - runs unchanged.
+            # (tuning cu_partition: CU-masked streams, its RCCL kernels
+            # included), as on a node where every rank owns a GPU.  The GPU
+            # still time-slices the processes' queues, so the backend leaves
+            # out the schedules whose waves wait on other workgroups (chained
+            # groups, linked launches); everything else runs unchanged.
             per = -(-world // ndev)
-            os.environ["GOL_CU_PARTITION"] = f"{local // ndev}/{per}"
+            tune.setdefault("cu_partition", f"{local // ndev}/{per}")
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         local = local % max(1, ndev)
 
@@ -290,13 +307,14 @@ def main() -> int:
     import torch  # noqa: PLC0415
 
     from gol_amd import LifeConfig, Simulation, make_backend, native  # noqa: PLC0415
+    from gol_amd.models.life import make_tuning  # noqa: PLC0415
     from gol_amd.parallel.dist import allreduce_max_float  # noqa: PLC0415
 
     if on_gpu:
         if not torch.cuda.is_available():
             raise SystemExit("bench.py: no GPU visible (use --engine cpu for a CPU dry run)")
         torch.cuda.set_device(local)
-    backend = make_backend(a.engine, local)
+    backend = make_backend(a.engine, local, tune=tune)
     dist = None
     if world > 1:
         from gol_amd.parallel.dist import init_process_group, make_transport  # noqa: PLC0415
@@ -306,10 +324,10 @@ def main() -> int:
         # communicator (gather_grid, the MAX of the rank timings) runs the
         # same code path as on the node.
         dist = init_process_group("nccl" if on_gpu else "gloo", device=local if on_gpu else None)
-        transport = make_transport(a.comm, backend, local)
+        transport = make_transport(a.comm, backend, local, tune=tune)
     elif a.rehearse_rccl and on_gpu:
         C = native()
-        transport = C.rccl_transport(C.rccl_unique_id(), 0, 1, local)
+        transport = C.rccl_transport(C.rccl_unique_id(), 0, 1, local, tune=make_tuning(tune))
     else:
         transport = native().self_transport()
 
@@ -338,7 +356,8 @@ def main() -> int:
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
                      poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs, timing_barriers=False,
                      self_exchange=bool(a.rehearse_rccl and world == 1), u8_compute=a.u8_compute,
-                     watchdog_s=300.0)  # a stuck rank or kernel fails the run instead of hanging it
+                     watchdog_s=300.0,  # a stuck rank or kernel fails the run instead of hanging it
+                     tune=tune)
     sim = Simulation(cfg, transport=transport, backend=backend)
     eng = sim.native_engine
     sim.init_random(a.seed, 0.5)
@@ -518,10 +537,14 @@ def main() -> int:
                 "flow_launches_per_step": rs[-1].flow_launches if rs else 0,
                 "flow_blocks_per_step": rs[-1].flow_blocks if rs else 0,
                 "flow_plan": desc["flow_plan"],
-                # Knobs set by hand (bench.py's own rehearsal partition aside).
-                "env_knobs": {k: v for k, v in sorted(os.environ.items())
-                              if k.startswith("GOL_") and not (shared and k == "GOL_CU_PARTITION")},
-                "cu_partition": os.environ.get("GOL_CU_PARTITION") if shared else None,
+                # Knobs set by hand: GOL_* variables, and every tuning key off
+                # its default with its source (bench.py's own rehearsal
+                # partition aside); the effective values of the tune class.
+                "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith("GOL_")},
+                "tuning_changed": {k: v for k, v in desc["tuning_changed"].items()
+                                   if not (shared and k == "cu_partition")},
+                "tuning": desc["tuning"],
+                "cu_partition": desc["tuning"]["cu_partition"] if shared else None,
                 "halo_bytes_per_step": rs[-1].halo_bytes if rs else 0,
                 "overlapped_halo_exchange": bool(rs and rs[-1].overlapped),
                 "overlap_mode": desc["overlap_mode"],

@@ -12,6 +12,7 @@
 #include <string>
 
 #include "gol/tile.hpp"
+#include "gol/tuning.hpp"
 
 namespace gol {
 
@@ -194,14 +195,23 @@ class Backend {
   // grid is identical for every decomposition and layout.
   virtual void init_random(void* buf, const TileGeom& g, uint64_t seed, double density,
                            int64_t grow0, int64_t gcol0) = 0;
+
+  // The tuning the backend was constructed with (gol/tuning.hpp): its knobs
+  // are read from it once, at construction.
+  const Tuning& tuning() const { return tuning_; }
+
+ protected:
+  explicit Backend(const Tuning& t) : tuning_(t) {}
+  Tuning tuning_;
 };
 
 // drift: emulate the drifting frame of the HIP adder window (each block's
 // output shifted right by T cells), so the engine's drift bookkeeping is
-// testable on the CPU; GOL_CPU_DRIFT=1 turns it on for default backends.
-std::unique_ptr<Backend> make_cpu_backend(int threads, int drift = -1);
-// Defined in backend_hip.hip; throws if no device or the kernels are missing.
-std::unique_ptr<Backend> make_hip_backend(int device);
+// testable on the CPU; -1: the tuning's cpu_drift.
+std::unique_ptr<Backend> make_cpu_backend(int threads, int drift = -1, const Tuning& tune = Tuning::from_env());
+// Defined in backend_hip.hip; throws if no device or the kernels are missing,
+// or if `tune` selects a kernel this build does not carry.
+std::unique_ptr<Backend> make_hip_backend(int device, const Tuning& tune = Tuning::from_env());
 bool hip_available();
 // Whether the HIP kernels were built with GOL_EXPERIMENTAL (the measured-
 // slower variants and schedules; docs/PERFORMANCE.md).

@@ -95,6 +95,11 @@ struct EngineConfig {
   // items of the block before them instead of a launch boundary.  -1 auto
   // (wherever the backend has the kernel), 0 off, 1 on (same as auto).
   int flow = -1;
+  // Runtime tuning (gol/tuning.hpp): the engine's own knobs (u8_via_bits,
+  // side_poll, watchdog_s, pitch_pad, overlap_auto) come from here; the
+  // backend's from the Tuning it was constructed with.  Default: the table's
+  // defaults under the GOL_* environment overrides.
+  Tuning tune = Tuning::from_env();
 };
 
 struct RunResult {

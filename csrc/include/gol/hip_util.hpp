@@ -9,7 +9,6 @@
 
 #include <cstdint>
 #include <cstdio>
-#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -49,18 +48,17 @@ class DeviceScope {
   int dev_, prev_ = -1;
 };
 
-// CU partition of this process on its device (GOL_CU_PARTITION=k/n: the k-th
-// of n equal, disjoint slices of the CUs).  Ranks that share one GPU in a
-// rehearsal (bench.py --share-gpus) each take a slice, so each rank's
+// CU partition of this process on its device (tuning cu_partition = "k/n":
+// the k-th of n equal, disjoint slices of the CUs).  Ranks that share one GPU
+// in a rehearsal (bench.py --share-gpus) each take a slice, so each rank's
 // kernels - its own and the RCCL kernels it enqueues on its streams - run on
 // CUs of their own, as on a node where every rank owns a GPU, and the
 // backend plans its launches for the slice.  Empty mask: the whole device.
-inline std::vector<uint32_t> cu_partition_mask(int cus) {
-  const char* e = std::getenv("GOL_CU_PARTITION");
-  if (!e || !*e) return {};
+inline std::vector<uint32_t> cu_partition_mask(const std::string& spec, int cus) {
+  if (spec.empty()) return {};
   int k = -1, n = 0;
-  if (std::sscanf(e, "%d/%d", &k, &n) != 2 || n < 1 || k < 0 || k >= n || n > cus)
-    fail(std::string("GOL_CU_PARTITION=") + e + ": expected k/n with 0 <= k < n <= " + std::to_string(cus));
+  if (std::sscanf(spec.c_str(), "%d/%d", &k, &n) != 2 || n < 1 || k < 0 || k >= n || n > cus)
+    fail("tuning cu_partition=" + spec + ": expected k/n with 0 <= k < n <= " + std::to_string(cus));
   std::vector<uint32_t> m(size_t((cus + 31) / 32), 0u);
   for (int c = int(int64_t(k) * cus / n); c < int(int64_t(k + 1) * cus / n); ++c) m[size_t(c / 32)] |= 1u << (c % 32);
   return m;
@@ -70,12 +68,12 @@ inline int mask_cus(const std::vector<uint32_t>& m) {
   for (uint32_t w : m) c += __builtin_popcount(w);
   return c;
 }
-// A stream for `dev`'s work: non-blocking, or restricted to the process's CU
-// partition when it has one (HIP's CU-masked streams).
-inline hipStream_t make_stream(int dev) {
+// A stream for `dev`'s work: non-blocking, or restricted to the CU partition
+// `cu_partition` when it names one (HIP's CU-masked streams).
+inline hipStream_t make_stream(int dev, const std::string& cu_partition) {
   hipDeviceProp_t prop;
   HIP_CHECK(hipGetDeviceProperties(&prop, dev));
-  const std::vector<uint32_t> m = cu_partition_mask(prop.multiProcessorCount);
+  const std::vector<uint32_t> m = cu_partition_mask(cu_partition, prop.multiProcessorCount);
   hipStream_t s = nullptr;
   if (m.empty())
     HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));

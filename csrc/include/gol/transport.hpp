@@ -28,6 +28,8 @@
 #include <string>
 #include <vector>
 
+#include "gol/tuning.hpp"
+
 namespace gol {
 
 class Backend;
@@ -108,7 +110,8 @@ class ThreadHub {
 
 class ThreadTransport final : public Transport {
  public:
-  ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, Backend* backend);
+  ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, Backend* backend,
+                  const Tuning& tune = Tuning::from_env());
   int rank() const override { return rank_; }
   int size() const override { return hub_->size(); }
   const char* name() const override { return "thread"; }
@@ -120,11 +123,11 @@ class ThreadTransport final : public Transport {
   std::shared_ptr<ThreadHub> hub_;
   int rank_;
   Backend* backend_;
-  // Fault injection for tests: GOL_FAULT_DELAY_US = random
-  // delay (0..N us) before publishing and before consuming each message, to
-  // shake out ordering bugs; GOL_FAULT_GARBLE = corrupt the N-th message this
-  // rank receives (1-based; low bit of every 8th byte), which the golden comparison must
-  // catch.
+  // Fault injection for tests: tuning fault_delay_us =
+  // random delay (0..N us) before publishing and before consuming each
+  // message, to shake out ordering bugs; fault_garble = corrupt the N-th
+  // message this rank receives (1-based; low bit of every 8th byte), which
+  // the golden comparison must catch.
   int delay_us_ = 0;
   int64_t garble_at_ = 0, received_ = 0;
   uint64_t rng_ = 0;
@@ -133,9 +136,11 @@ class ThreadTransport final : public Transport {
 };
 
 // RCCL transport (one process per GPU).  `unique_id` is the 128-byte
-// ncclUniqueId created on rank 0 and broadcast by the caller.
+// ncclUniqueId created on rank 0 and broadcast by the caller.  From `tune`:
+// side_poll (a second communicator for the flag reductions) and
+// cu_partition (its barrier stream's CUs).
 std::unique_ptr<Transport> make_rccl_transport(const std::vector<uint8_t>& unique_id, int rank,
-                                               int nranks, int device);
+                                               int nranks, int device, const Tuning& tune = Tuning::from_env());
 std::vector<uint8_t> rccl_unique_id();
 bool rccl_available();
 // PCI bus id ("0000:05:00.0") of a HIP device: which physical GPU a rank ran on.

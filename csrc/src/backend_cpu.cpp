@@ -92,16 +92,17 @@ inline uint32_t owned_mask(const TileGeom& g, int64_t c) {
 
 class CpuBackend final : public Backend {
  public:
-  CpuBackend(int threads, bool drift) : pool_(threads > 0 ? threads : default_host_threads()), drift_(drift) {
-    const char* r = std::getenv("GOL_CPU_RESIDENT");
-    resident_ = r && *r && *r != '0';
-    const char* ring = std::getenv("GOL_CPU_RING");
-    ring_ = ring && *ring && *ring != '0';
-    ring_fail_ = ring && std::string(ring) == "fail";  // tests: the mapping fails after the size check
-    const char* flow = std::getenv("GOL_CPU_FLOW");
-    flow_ = flow && *flow && *flow != '0';
+  CpuBackend(int threads, bool drift, const Tuning& t)
+      : Backend(t),
+        pool_(threads > 0 ? threads : t.i("host_threads") > 0 ? t.i("host_threads") : default_host_threads()),
+        drift_(drift) {
+    resident_ = t.on("cpu_resident");
+    const std::string& ring = t.s("cpu_ring");
+    ring_ = !ring.empty() && ring != "0";
+    ring_fail_ = ring == "fail";  // tests: the mapping fails after the size check
+    flow_ = t.on("cpu_flow");
   }
-  // GOL_CPU_FLOW=1: the engine hands runs of equal blocks to run_flow (the
+  // Tuning cpu_flow=1: the engine hands runs of equal blocks to run_flow (the
   // HIP backend's persistent dataflow launch); the base class runs them
   // block by block, so the engine's flow bookkeeping is testable on the CPU.
   bool has_flow(Layout, int T) const override { return flow_ && T >= 2; }
@@ -530,12 +531,9 @@ void CpuBackend::init_random(void* buf, const TileGeom& g, uint64_t seed, double
 
 }  // namespace
 
-std::unique_ptr<Backend> make_cpu_backend(int threads, int drift) {
-  if (drift < 0) {
-    const char* e = std::getenv("GOL_CPU_DRIFT");
-    drift = e && *e && *e != '0' ? 1 : 0;
-  }
-  return std::make_unique<CpuBackend>(threads, drift != 0);
+std::unique_ptr<Backend> make_cpu_backend(int threads, int drift, const Tuning& tune) {
+  if (drift < 0) drift = tune.on("cpu_drift");
+  return std::make_unique<CpuBackend>(threads, drift != 0, tune);
 }
 
 }  // namespace gol

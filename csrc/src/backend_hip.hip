@@ -28,18 +28,7 @@
 namespace gol {
 namespace {
 
-// Integer from the environment (any value, including 0 and negatives);
-// unset, empty or unparsable -> dflt.
-int env_int(const char* name, int dflt) {
-  if (const char* s = std::getenv(name)) {
-    char* end = nullptr;
-    const long v = std::strtol(s, &end, 10);
-    if (end != s && *end == '\0') return int(v);
-  }
-  return dflt;
-}
-
-// GOL_CHECK_DEVICE=1: every entry point asserts that its device is current,
+// Tuning check_device=1 (GOL_CHECK_DEVICE): every entry point asserts that its device is current,
 // and every buffer the backend allocates or a launch touches is checked to
 // live on that device (hipPointerGetAttributes).
 #define GOL_ON_DEVICE()              \
@@ -59,7 +48,8 @@ std::map<int, int>& live_backends() {
 
 class HipBackend final : public Backend {
  public:
-  explicit HipBackend(int device) : dev_(device) {
+  HipBackend(int device, const Tuning& t) : Backend(t), dev_(device) {
+    t.require_build(hipk::kExperimentalBuild);
     {
       std::lock_guard<std::mutex> lk(live_mu());
       ++live_backends()[device];
@@ -68,77 +58,71 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGetDeviceCount(&n));
     GOL_REQUIRE(n > 0, "no HIP device available");
     GOL_REQUIRE(device >= 0 && device < n, "HIP device index out of range");
-    check_dev_ = env_int("GOL_CHECK_DEVICE", 0) != 0;
-    ring_on_ = env_int("GOL_ROW_RING", 1) != 0;
+    check_dev_ = t.on("check_device");
+    ring_on_ = t.on("row_ring");
     GOL_ON_DEVICE();
-    stream_ = make_stream(dev_);
+    stream_ = make_stream(dev_, tuning_.s("cu_partition"));
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
     cus_ = prop.multiProcessorCount;
-    // A CU partition (GOL_CU_PARTITION, ranks sharing a GPU): every stream of
-    // this backend runs on the slice, and launches are planned for it.
-    if (const int part = mask_cus(cu_partition_mask(cus_))) {
-      cu_part_ = " cu-partition=" + std::string(std::getenv("GOL_CU_PARTITION")) + ":" + std::to_string(part) + "CUs";
+    // A CU partition (tuning cu_partition, ranks sharing a GPU): every stream
+    // of this backend runs on the slice, and launches are planned for it.
+    if (const int part = mask_cus(cu_partition_mask(t.s("cu_partition"), cus_))) {
+      cu_part_ = " cu-partition=" + t.s("cu_partition") + ":" + std::to_string(part) + "CUs";
       cus_ = part;
     }
     tune_.cus = cus_;
-    tune_.target_waves = env_int("GOL_TARGET_WAVES", 0);
-    tune_.min_seg_rows = env_int("GOL_MIN_SEG_ROWS", 16);
-    tune_.skew = env_int("GOL_SKEW", 0) != 0;
-    tune_.wpl_bits = env_int("GOL_WPL", 1);
-    tune_.xlane = env_int("GOL_XLANE", hipk::kXlaneAuto);
-    if (const char* k = std::getenv("GOL_U8_KERNEL")) tune_.u8_lds = std::string(k) == "lds";
-    tune_.lds_rows = env_int("GOL_LDS_ROWS", 32);
-    tune_.lds_pack = env_int("GOL_LDS_PACK", 1) != 0;
-    tune_.lds_xcd = env_int("GOL_LDS_XCD", 0) != 0;
-    tune_.lds_waves = env_int("GOL_LDS_WAVES", 0);
-    GOL_REQUIRE(tune_.lds_waves == 0 || tune_.lds_waves == 8 || tune_.lds_waves == 16, "GOL_LDS_WAVES: 0, 8 or 16");
-    lds_add_ = env_int("GOL_LDS_ADD", 0) != 0;  // packed LDS tile: adder window (drifting frame)
+    tune_.target_waves = t.i("target_waves");
+    tune_.min_seg_rows = t.i("min_seg_rows");
+    tune_.skew = t.on("skew");
+    tune_.wpl_bits = t.i("wpl");
+    tune_.xlane = t.i("xlane");
+    tune_.u8_lds = t.s("u8_kernel") == "lds";
+    GOL_REQUIRE(tune_.u8_lds || t.s("u8_kernel") == "auto", "tuning u8_kernel: auto or lds");
+    tune_.lds_rows = t.i("lds_rows");
+    tune_.lds_pack = t.on("lds_pack");
+    tune_.lds_xcd = t.on("lds_xcd");
+    tune_.lds_waves = t.i("lds_waves");
+    GOL_REQUIRE(tune_.lds_waves == 0 || tune_.lds_waves == 8 || tune_.lds_waves == 16, "tuning lds_waves: 0, 8 or 16");
+    lds_add_ = t.on("lds_add");  // packed LDS tile: adder window (drifting frame)
     // 8192^2 per generation: bytes T = 1 26.6, 2 24.9, 4 20.4, 8 17.9 us; packed T = 8 6.5, 16 4.9, 32 4.7
-    tune_.lds_T = env_int("GOL_LDS_T", tune_.lds_pack ? 32 : 8);
+    tune_.lds_T = t.i("lds_t") > 0 ? t.i("lds_t") : tune_.lds_pack ? 32 : 8;
     GOL_REQUIRE(tune_.lds_T == 1 || tune_.lds_T == 2 || tune_.lds_T == 4 || tune_.lds_T == 8 ||
                     (tune_.lds_pack && (tune_.lds_T == 16 || tune_.lds_T == 32)),
-                "GOL_LDS_T must be 1, 2, 4 or 8 (16 or 32 with the packed tile, GOL_LDS_PACK=1)");
-    tune_.split = env_int("GOL_SPLIT", 0);  // measured slower so far (profiles/)
-    tune_.group = env_int("GOL_GROUP", 8);  // grouped schedule (life_group_impl.hpp)
-    tune_.group_small = std::getenv("GOL_GROUP") ? tune_.group : env_int("GOL_GROUP_SMALL", 4);
+                "tuning lds_t must be 1, 2, 4 or 8 (16 or 32 with the packed tile, lds_pack=1)");
+    tune_.split = t.i("split");  // measured slower so far (profiles/)
+    tune_.group = t.i("group");  // grouped schedule (life_group_impl.hpp)
+    tune_.group_small = !t.is_default("group") && t.is_default("group_small") ? tune_.group : t.i("group_small");
     // Short-segment groups (life_short_impl.hpp): exact, but 10-20 % slower
     // than the grouped kernel on the per-rank tile (profiles/sweep_short_segments.jsonl).
-    tune_.short_seg = env_int("GOL_SHORT", 0);
-    tune_.pipe = env_int("GOL_PIPE", 0);
-    tune_.wrap = env_int("GOL_WRAP", 1) != 0;
-    tune_.fold = env_int("GOL_FOLD", 1) != 0;
-    chain_mode_ = env_int("GOL_CHAIN", -1);
-    // Resident epochs (life_resident_impl.hpp): GOL_RESIDENT -1 auto, 0 off,
-    // 1 on where the tile fits; GOL_RES_K refresh period / halo rows (<= 16);
-    // GOL_RES_D epoch depth; GOL_RES_PROBE=1 timing probe without refreshes.
-    resident_mode_ = env_int("GOL_RESIDENT", 0);
-    resident_k_ = std::min(16, std::max(0, env_int("GOL_RES_K", 0)));  // 0: as deep as the band's slack allows
-    resident_D_ = env_int("GOL_RES_D", 0);
-    resident_probe_ = env_int("GOL_RES_PROBE", 0);
-    if (const char* t = std::getenv("GOL_RES_TRACE")) {
-      const std::string v(t);
-      const size_t c = v.find(':');
-      if (c != std::string::npos) {
-        res_trace_at_ = std::atoi(v.substr(0, c).c_str());
-        res_trace_path_ = v.substr(c + 1);
-      }
-    }
-    u8_pipe_ = env_int("GOL_U8_PIPE", 1) != 0;
+    tune_.short_seg = t.i("short");
+    tune_.pipe = t.i("pipe");
+    tune_.wrap = t.on("wrap");
+    tune_.fold = t.on("fold");
+    chain_mode_ = t.i("chain");
+    // Resident epochs (life_resident_impl.hpp): resident -1 auto, 0 off, 1 on
+    // where the tile fits; res_k refresh period / halo rows (<= 16); res_d
+    // epoch depth; res_probe=1 timing probe without refreshes.
+    resident_mode_ = t.i("resident");
+    resident_k_ = std::min(16, std::max(0, t.i("res_k")));  // 0: as deep as the band's slack allows
+    resident_D_ = t.i("res_d");
+    resident_probe_ = t.i("res_probe");
+    split_trace(t.s("res_trace"), &res_trace_at_, &res_trace_path_);
+    u8_pipe_ = t.on("u8_pipe");
     // Linked launches: consecutive grouped launches of an epoch overlap on
     // two streams, ordered by per-group completion words (LifeBlockParams::
     // link_*): small tiles whose launches alone hold only 2 waves per SIMD.
-    // GOL_LINK: 1 every eligible launch, 0 never, -1 (default) where the
+    // Tuning link: 1 every eligible launch, 0 never, -1 (default) where the
     // engine passes KernelChoice::link (small single-rank ring tiles).
-    link_mode_ = env_int("GOL_LINK", -1);
+    link_mode_ = t.i("link");
     link_on_ = link_mode_ > 0;
     if (link_mode_ != 0) {
       link_.stream[0] = stream_;
-      link_.stream[1] = make_stream(dev_);
+      link_.stream[1] = make_stream(dev_, tuning_.s("cu_partition"));
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      link_.events = env_int("GOL_LINK_EVENTS", 1) != 0;
-      tune_.link_force = env_int("GOL_LINK_FORCE", 0) != 0;
+      link_.events = t.on("link_events");
+      tune_.link_force = t.on("link_force");
     }
     // A GPU shared by several processes (a CU partition) time-slices their
     // queues, so a producer workgroup can be switched out for longer than a
@@ -150,24 +134,16 @@ class HipBackend final : public Backend {
       link_on_ = false;
     }
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
-    // Persistent dataflow launches (life_flow_impl.hpp): GOL_FLOW=0 turns
-    // them off; GOL_FLOW_M / GOL_FLOW_NSEG pin the planner's waves per item
-    // and groups per strip (sweeps).
-    flow_on_ = env_int("GOL_FLOW", 0) != 0;
-    tune_.flow_m = env_int("GOL_FLOW_M", 0);
-    tune_.flow_nseg = env_int("GOL_FLOW_NSEG", 0);
-    tune_.flow_spin_log2 = std::min(26, std::max(8, env_int("GOL_FLOW_SPIN", 20)));
-    tune_.fault_delay = std::max(0, std::min(4096, env_int("GOL_FAULT_DELAY_SPINS", 0)));
-    if (const char* t = std::getenv("GOL_FLOW_TRACE")) {
-      const std::string v(t);
-      const size_t c = v.find(':');
-      if (c != std::string::npos) {
-        flow_trace_at_ = std::atoi(v.substr(0, c).c_str());
-        flow_trace_path_ = v.substr(c + 1);
-      }
-    }
-    if (!hipk::kExperimentalBuild) refuse_experimental();
-    tune_log_ = env_int("GOL_TUNE_LOG", 0) != 0;
+    // Persistent dataflow launches (life_flow_impl.hpp, experimental builds):
+    // flow_m / flow_nseg pin the planner's waves per item and groups per
+    // strip (sweeps).
+    flow_on_ = t.on("flow");
+    tune_.flow_m = t.i("flow_m");
+    tune_.flow_nseg = t.i("flow_nseg");
+    tune_.flow_spin_log2 = std::min(26, std::max(8, t.i("flow_spin")));
+    tune_.fault_delay = std::max(0, std::min(4096, t.i("fault_delay_spins")));
+    split_trace(t.s("flow_trace"), &flow_trace_at_, &flow_trace_path_);
+    tune_log_ = t.on("tune_log");
     tune_.chain_seq = &chain_seq_;
     // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words,
     // 5..7 resident mirrors and flags, 8 flow completion words, 9 the flow
@@ -188,26 +164,20 @@ class HipBackend final : public Backend {
       if (check_dev_) check_ptr(buf, which == 0 ? "chain flags" : which == 1 ? "chain slots" : "link words");
       return static_cast<uint32_t*>(buf);
     };
-    if (const char* t = std::getenv("GOL_WG_TRACE")) {
-      const std::string v(t);
-      const size_t c = v.find(':');
-      if (c != std::string::npos) {
-        trace_at_ = std::atoi(v.substr(0, c).c_str());
-        trace_path_ = v.substr(c + 1);
-        // "N:path:pair": launches N and N + 1, left linked (overlap evidence).
-        const size_t c2 = trace_path_.rfind(":pair");
-        if (c2 != std::string::npos && c2 + 5 == trace_path_.size()) {
-          trace_pair_ = true;
-          trace_path_ = trace_path_.substr(0, c2);
-        }
+    if (split_trace(t.s("wg_trace"), &trace_at_, &trace_path_)) {
+      // "N:path:pair": launches N and N + 1, left linked (overlap evidence).
+      const size_t c2 = trace_path_.rfind(":pair");
+      if (c2 != std::string::npos && c2 + 5 == trace_path_.size()) {
+        trace_pair_ = true;
+        trace_path_ = trace_path_.substr(0, c2);
       }
     }
     // Kernel error word: fine-grained pinned host memory the kernels write
     // through its device alias and the host reads without a copy.
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 4 * sizeof(uint32_t), hipHostMallocMapped));
     for (int i = 0; i < 4; ++i) err_host_[i] = 0;
-    tune_.chain_spin_log2 = std::min(24, std::max(4, env_int("GOL_CHAIN_SPIN", 16)));
-    tune_.chain_acquire = env_int("GOL_CHAIN_ACQUIRE", 1) != 0;
+    tune_.chain_spin_log2 = std::min(24, std::max(4, t.i("chain_spin")));
+    tune_.chain_acquire = t.on("chain_acquire");
     HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&tune_.err), err_host_, 0));
     tune_.scratch = [this](size_t n) -> void* {
       if (n > scratch_bytes_) {
@@ -606,7 +576,7 @@ class HipBackend final : public Backend {
   void* comm_stream() override {
     if (!comm_) {
       GOL_ON_DEVICE();
-      comm_ = make_stream(dev_);
+      comm_ = make_stream(dev_, tuning_.s("cu_partition"));
       if (check_dev_) {
         int d = -1;
         HIP_CHECK(hipStreamGetDevice(comm_, &d));
@@ -1142,26 +1112,13 @@ class HipBackend final : public Backend {
       h = {};
     }
   }
-  // Default builds carry neither the measured-slower variants nor their
-  // schedules (hipk::kExperimentalBuild): an environment asking for one fails
-  // here, loudly, instead of silently running the default kernel.
-  static void refuse_experimental() {
-    struct Knob {
-      const char* name;
-      int dflt;
-    };
-    static const Knob knobs[] = {{"GOL_WPL", 1},  {"GOL_SKEW", 0},     {"GOL_SPLIT", 0}, {"GOL_SHORT", 0},
-                                 {"GOL_PIPE", 0}, {"GOL_RESIDENT", 0},
-                                 {"GOL_LDS_ADD", 0}, {"GOL_FLOW", 0}};
-    for (const Knob& k : knobs)
-      if (env_int(k.name, k.dflt) != k.dflt)
-        fail(std::string(k.name) + "=" + std::getenv(k.name) +
-             " selects a measured-slower variant that this build does not carry; rebuild with "
-             "GOL_EXPERIMENTAL=1 python -m gol_amd.native_build");
-    const int x = env_int("GOL_XLANE", hipk::kXlaneAuto);
-    if (x == hipk::kXlaneBpermute || x == hipk::kXlaneCarry)
-      fail("GOL_XLANE=" + std::to_string(x) + " (ds_bpermute / carry-chain window) needs an experimental build "
-           "(GOL_EXPERIMENTAL=1 python -m gol_amd.native_build)");
+  // Trace settings "N:path": launch N's trace goes to path.
+  static bool split_trace(const std::string& v, int64_t* at, std::string* path) {
+    const size_t c = v.find(':');
+    if (c == std::string::npos) return false;
+    *at = std::atoll(v.substr(0, c).c_str());
+    *path = v.substr(c + 1);
+    return true;
   }
   int64_t rows_per_chunk(const TileGeom& g) const {
     const int64_t budget = int64_t(256) << 20;
@@ -1230,7 +1187,7 @@ class HipBackend final : public Backend {
   std::deque<Pending> pending_;  // timed trial launches not collected yet
   std::vector<hipEvent_t> free_events_;
   int64_t launches_ = 0;
-  bool prof_on_ = env_int("GOL_HOST_PROFILE", 0) != 0;
+  bool prof_on_ = tuning_.on("host_profile");
   int64_t prof_n_ = 0;
   double prof_gap_ = 0, prof_in_ = 0, prof_launch_ = 0;
   std::chrono::steady_clock::time_point prof_exit_{};
@@ -1256,11 +1213,11 @@ bool hip_available() {
   return n > 0;
 }
 
-std::unique_ptr<Backend> make_hip_backend(int device) {
+std::unique_ptr<Backend> make_hip_backend(int device, const Tuning& tune) {
   GOL_REQUIRE(hip_available(), "no HIP device available (HIP backend requested)");
   // Engine trace ranges -> roctx (visible with rocprofv3 --marker-trace).
   trace::set_hooks([](const char* m) { roctxRangePushA(m); }, [] { roctxRangePop(); });
-  return std::make_unique<HipBackend>(device);
+  return std::make_unique<HipBackend>(device, tune);
 }
 
 }  // namespace gol

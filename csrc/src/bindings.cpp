@@ -10,6 +10,7 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <optional>
 #include <thread>
 #include <tuple>
 
@@ -120,8 +121,39 @@ PYBIND11_MODULE(_gol, m) {
       .def("Wp", &TileGeom::Wp)
       .def("bytes", &TileGeom::bytes);
 
+  // Runtime tuning (gol/tuning.hpp).  Python passes a dict: LifeConfig.tune,
+  // make_backend(tune=...), bench.py / gol_amd.cli --tune key=value.
+  py::class_<Tuning>(m, "Tuning")
+      .def(py::init<>())
+      .def_static("from_env", &Tuning::from_env)
+      .def("set", py::overload_cast<const std::string&, const std::string&>(&Tuning::set),
+           py::return_value_policy::reference_internal)
+      .def("get", &Tuning::s)
+      .def("is_default", &Tuning::is_default)
+      .def("source", &Tuning::source)
+      .def("values", &Tuning::values)
+      .def("changed", &Tuning::changed)
+      .def("summary", &Tuning::summary)
+      .def("require_build", &Tuning::require_build)
+      .def("copy", [](const Tuning& t) { return Tuning(t); });
+  m.def("tuning_keys", []() {
+    py::list out;
+    for (const TuningKey& k : tuning_keys()) {
+      py::dict d;
+      d["key"] = k.key;
+      d["env"] = k.env;
+      d["default"] = k.dflt;
+      d["type"] = std::string(1, k.type);
+      d["class"] = k.cls;
+      d["doc"] = k.doc;
+      out.append(d);
+    }
+    return out;
+  });
+
   py::class_<Backend, std::shared_ptr<Backend>>(m, "Backend")
       .def("name", &Backend::name)
+      .def("tuning", &Backend::tuning, py::return_value_policy::copy)
       .def("flow_desc", &Backend::flow_desc)
       .def("is_device", &Backend::is_device)
       .def("device", &Backend::device)
@@ -129,10 +161,15 @@ PYBIND11_MODULE(_gol, m) {
       .def("synchronize", &Backend::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("bind_thread", &Backend::bind_thread);
   m.def("cpu_backend",
-        [](int threads, int drift) { return std::shared_ptr<Backend>(make_cpu_backend(threads, drift)); },
-        py::arg("threads") = 0, py::arg("drift") = -1);
-  m.def("hip_backend", [](int device) { return std::shared_ptr<Backend>(make_hip_backend(device)); },
-        py::arg("device") = 0);
+        [](int threads, int drift, std::optional<Tuning> tune) {
+          return std::shared_ptr<Backend>(make_cpu_backend(threads, drift, tune ? *tune : Tuning::from_env()));
+        },
+        py::arg("threads") = 0, py::arg("drift") = -1, py::arg("tune") = py::none());
+  m.def("hip_backend",
+        [](int device, std::optional<Tuning> tune) {
+          return std::shared_ptr<Backend>(make_hip_backend(device, tune ? *tune : Tuning::from_env()));
+        },
+        py::arg("device") = 0, py::arg("tune") = py::none());
   m.def("hip_available", &hip_available);
   m.def("hip_pci_bus_id", &hip_pci_bus_id);
   m.def("hip_uuid", &hip_uuid);
@@ -164,10 +201,11 @@ PYBIND11_MODULE(_gol, m) {
   m.def("self_transport", []() { return std::shared_ptr<Transport>(new SelfTransport()); });
   py::class_<ThreadHub, std::shared_ptr<ThreadHub>>(m, "ThreadHub").def(py::init<int>());
   m.def("thread_transport",
-        [](std::shared_ptr<ThreadHub> hub, int rank, std::shared_ptr<Backend> be) {
-          return std::shared_ptr<Transport>(new ThreadTransport(std::move(hub), rank, be.get()));
+        [](std::shared_ptr<ThreadHub> hub, int rank, std::shared_ptr<Backend> be, std::optional<Tuning> tune) {
+          return std::shared_ptr<Transport>(
+              new ThreadTransport(std::move(hub), rank, be.get(), tune ? *tune : Tuning::from_env()));
         },
-        py::keep_alive<0, 3>());
+        py::arg("hub"), py::arg("rank"), py::arg("backend"), py::arg("tune") = py::none(), py::keep_alive<0, 3>());
   m.def("callback_transport",
         [](int rank, int size, CallbackTransport::ExchangeFn ex, CallbackTransport::ReduceFn red,
            CallbackTransport::BarrierFn bar) {
@@ -177,16 +215,19 @@ PYBIND11_MODULE(_gol, m) {
     auto v = rccl_unique_id();
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
   });
-  m.def("rccl_transport", [](py::bytes uid, int rank, int nranks, int device) {
-    std::string s = uid;
-    std::vector<uint8_t> v(s.begin(), s.end());
-    std::shared_ptr<Transport> t;
-    {
-      py::gil_scoped_release rel;
-      t = make_rccl_transport(v, rank, nranks, device);
-    }
-    return t;
-  });
+  m.def("rccl_transport",
+        [](py::bytes uid, int rank, int nranks, int device, std::optional<Tuning> tune) {
+          std::string s = uid;
+          std::vector<uint8_t> v(s.begin(), s.end());
+          const Tuning t = tune ? *tune : Tuning::from_env();
+          std::shared_ptr<Transport> tr;
+          {
+            py::gil_scoped_release rel;
+            tr = make_rccl_transport(v, rank, nranks, device, t);
+          }
+          return tr;
+        },
+        py::arg("uid"), py::arg("rank"), py::arg("nranks"), py::arg("device"), py::arg("tune") = py::none());
 
   py::class_<EngineConfig>(m, "EngineConfig")
       .def(py::init<>())
@@ -209,7 +250,8 @@ PYBIND11_MODULE(_gol, m) {
       .def_readwrite("u8_compute", &EngineConfig::u8_compute)
       .def_readwrite("flow", &EngineConfig::flow)
       .def_readwrite("graphs", &EngineConfig::graphs)
-      .def_readwrite("watchdog_s", &EngineConfig::watchdog_s);
+      .def_readwrite("watchdog_s", &EngineConfig::watchdog_s)
+      .def_readwrite("tune", &EngineConfig::tune);
 
   py::class_<RunResult>(m, "RunResult")
       .def_readonly("generations", &RunResult::generations)
@@ -262,6 +304,7 @@ PYBIND11_MODULE(_gol, m) {
              return new Engine(c, be.get(), tr.get());
            }),
            py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def_property_readonly("config", &Engine::config, py::return_value_policy::copy)
       .def_property_readonly("rank", &Engine::rank)
       .def_property_readonly("rows", &Engine::rows)
       .def_property_readonly("cols", &Engine::cols)

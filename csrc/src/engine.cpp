@@ -67,10 +67,9 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // decision on every rank (configuration, backend kind and environment).
   if (cfg_.layout == Layout::U8 && cfg_.W % 32 == 0) {
     int mode = cfg_.u8_compute;
-    if (mode < 0) {
-      const char* e = std::getenv("GOL_U8_VIA_BITS");
-      mode = e ? (std::atoi(e) != 0) : (be_->is_device() && cfg_.overlap != 1 && cfg_.overlap != 2);
-    }
+    if (mode < 0) mode = cfg_.tune.i("u8_via_bits");
+    if (mode < 0) mode = be_->is_device() && cfg_.overlap != 1 && cfg_.overlap != 2;
+    else mode = mode != 0;
     via_bits_ = mode == 1;
   }
   // Layout the temporal blocks run on.
@@ -145,7 +144,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   int ring_dv = 0;
   void* ring_bufs[2] = {nullptr, nullptr};
   if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !rows_wrapped_ && !resident_ &&
-      !std::getenv("GOL_PITCH_PAD")) {
+      cfg_.tune.i("pitch_pad") == 0) {
     const TileGeom probe = TileGeom::make(cl, r.size(), c.size(), 0, hw);
     ring_dv = be_->row_ring_halo(probe.H, probe.pitch, tmax_);
     // The byte layout on bit words keeps its byte tiles too: the rings must
@@ -190,7 +189,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // joins the streams first.  Not with column fills between blocks.
   link_ = kc.link && !cols_filled_;
   // Experiment knob: extra bytes per padded row (multiple of 256).
-  if (const char* pad = std::getenv("GOL_PITCH_PAD")) g_.pitch += 256 * (std::max(0, std::atoi(pad)) / 256);
+  g_.pitch += 256 * (std::max(0, cfg_.tune.i("pitch_pad")) / 256);
   // Several ranks: every poll is a flag all-reduce on the compute stream
   // (latency-bound), so poll half as often; a stop is still exact and at most
   // two windows late.
@@ -250,9 +249,9 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     for (auto& e : edge_)
       for (auto& b : e) b = be_->alloc(size_t(gs_.bytes()));
   }
-  watchdog_s_ = cfg_.watchdog_s > 0 ? cfg_.watchdog_s : 900.0;
-  if (cfg_.watchdog_s <= 0)
-    if (const char* w = std::getenv("GOL_WATCHDOG_S")) watchdog_s_ = std::max(1.0, std::atof(w));
+  watchdog_s_ = cfg_.watchdog_s > 0 ? cfg_.watchdog_s
+                : cfg_.tune.i("watchdog_s") > 0 ? std::max(1.0, double(cfg_.tune.i("watchdog_s")))
+                                                : 900.0;
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
@@ -269,12 +268,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // stream after a mark on the compute stream, which never waits for them:
   // the reduction's latency leaves the critical path.  The halo exchanges
   // stay on the compute stream.
-  // Opt-in (GOL_SIDE_POLL=1): in the one-GPU RCCL rehearsal the cross-stream
+  // Opt-in (tuning side_poll=1): in the one-GPU RCCL rehearsal the cross-stream
   // hop cost ~10 us per poll, more than the 1-rank reduction it hides
   // (profiles/r02/side_poll_ab.jsonl); with 8 ranks the reduction is longer.
-  const char* side = std::getenv("GOL_SIDE_POLL");
   poll_side_ = tr_->side_reduce() && be_->is_device() && !early_ && !comm_route_ && !use_graphs_ &&
-               !auto_overlap_ && side && std::atoi(side) != 0;
+               !auto_overlap_ && cfg_.tune.on("side_poll");
   gen_ = cfg_.start_gen;
 }
 
@@ -1113,10 +1111,9 @@ void Engine::auto_decide() {
   auto_ms_[0] = v[0] * 1e-4;
   auto_ms_[1] = v[1] * 1e-4;
   bool early = double(v[1]) < 0.98 * double(v[0]);
-  if (const char* f = std::getenv("GOL_OVERLAP_AUTO")) {
-    if (std::strcmp(f, "early") == 0) early = true;
-    if (std::strcmp(f, "plain") == 0) early = false;
-  }
+  const std::string& forced = cfg_.tune.s("overlap_auto");  // fault injection (tests)
+  if (forced == "early") early = true;
+  if (forced == "plain") early = false;
   early_ = comm_route_ = early;
   auto_overlap_ = false;
   auto_decided_ = true;

@@ -1,4 +1,5 @@
 #include "gol/parallel.hpp"
+#include "gol/tuning.hpp"
 
 #include <atomic>
 
@@ -74,10 +75,7 @@ void ThreadPool::worker_loop(int) {
 }
 
 int default_host_threads() {
-  if (const char* s = std::getenv("GOL_HOST_THREADS")) {
-    int v = std::atoi(s);
-    if (v > 0) return v;
-  }
+  if (const int v = Tuning::from_env().i("host_threads"); v > 0) return v;
   unsigned hc = std::thread::hardware_concurrency();
   return int(std::min<unsigned>(hc ? hc : 4, 16));
 }

@@ -17,10 +17,10 @@ void SelfTransport::exchange(const std::vector<P2POp>& ops, void*) {
 
 ThreadHub::ThreadHub(int nranks) : red(), n_(nranks) { GOL_REQUIRE(nranks > 0, "hub size"); }
 
-ThreadTransport::ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, Backend* backend)
+ThreadTransport::ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, Backend* backend, const Tuning& tune)
     : hub_(std::move(hub)), rank_(rank), backend_(backend) {
-  if (const char* d = std::getenv("GOL_FAULT_DELAY_US")) delay_us_ = std::max(0, std::atoi(d));
-  if (const char* g = std::getenv("GOL_FAULT_GARBLE")) garble_at_ = std::atoll(g);
+  delay_us_ = std::max(0, tune.i("fault_delay_us"));
+  garble_at_ = tune.i("fault_garble");
   rng_ = 0x9E3779B97F4A7C15ull * uint64_t(rank + 1);
 }
 

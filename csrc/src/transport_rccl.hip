@@ -83,7 +83,7 @@ class StdoutToStderr {
 
 class RcclTransport final : public Transport {
  public:
-  RcclTransport(const std::vector<uint8_t>& uid, int rank, int nranks, int device)
+  RcclTransport(const std::vector<uint8_t>& uid, int rank, int nranks, int device, const Tuning& tune)
       : rank_(rank), size_(nranks), dev_(device) {
     GOL_REQUIRE(uid.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size");
     ncclUniqueId id;
@@ -92,14 +92,13 @@ class RcclTransport final : public Transport {
     {
       StdoutToStderr quiet;
       NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
-      // Side-stream polls (GOL_SIDE_POLL=1, the same on every rank): the
+      // Side-stream polls (tuning side_poll=1, the same on every rank): the
       // termination-flag reductions get their own communicator.  RCCL orders
       // the operations of one communicator by issue, and two streams on one
       // communicator could interleave differently on different ranks.
-      const char* side = std::getenv("GOL_SIDE_POLL");
-      if (side && std::atoi(side) != 0) NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
+      if (tune.on("side_poll")) NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
     }
-    barrier_stream_ = make_stream(dev_);
+    barrier_stream_ = make_stream(dev_, tune.s("cu_partition"));
     HIP_CHECK(hipMalloc(&barrier_buf_, 64));
     HIP_CHECK(hipMemsetAsync(barrier_buf_, 0, 64, barrier_stream_));  // HIP's hipMemset may return before it ran
     HIP_CHECK(hipStreamSynchronize(barrier_stream_));
@@ -204,8 +203,8 @@ std::string hip_uuid(int device) {
 }
 
 std::unique_ptr<Transport> make_rccl_transport(const std::vector<uint8_t>& uid, int rank, int nranks,
-                                               int device) {
-  return std::make_unique<RcclTransport>(uid, rank, nranks, device);
+                                               int device, const Tuning& tune) {
+  return std::make_unique<RcclTransport>(uid, rank, nranks, device, tune);
 }
 
 }  // namespace gol

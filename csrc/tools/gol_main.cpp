@@ -59,6 +59,7 @@ struct Options {
   std::string checkpoint_dir;       // where they go
   std::string resume;               // checkpoint directory to resume from
   bool gens_set = false, sim_set = false;
+  Tuning tune = Tuning::from_env();  // --tune key=value over the GOL_* environment
 };
 
 [[noreturn]] void usage(int code) {
@@ -86,6 +87,8 @@ struct Options {
                "                              ranks and keep the faster (row strips only)\n"
                "  --graphs auto|on|off        replay full epochs as captured HIP graphs\n"
                "  --threads N                 host threads for the cpu engine\n"
+               "  --tune KEY=VALUE            runtime tuning (repeatable; --tune help lists the keys,\n"
+               "                              their GOL_* overrides and defaults)\n"
                "  --style serial|mpi|async|collective|openmp|cuda\n"
                "                              stdout format and output name of that reference build\n"
                "  --metrics-json PATH         write run metrics as JSON\n"
@@ -130,6 +133,15 @@ Options parse(int argc, char** argv) {
     else if (a == "--gpus") o.gpus = std::atoi(next().c_str());
     else if (a == "--ranks") o.ranks = std::atoi(next().c_str());
     else if (a == "--threads") o.threads = std::atoi(next().c_str());
+    else if (a == "--tune") {
+      const std::string kv = next();
+      if (kv == "help") {
+        for (const TuningKey& k : tuning_keys())
+          std::printf("%-22s %-13s %-27s default %-6s %s\n", k.key, k.cls, k.env, *k.dflt ? k.dflt : "''", k.doc);
+        std::exit(0);
+      }
+      o.tune.set(kv);
+    }
     else if (a == "--tmax") o.tmax = std::atoi(next().c_str());
     else if (a == "--epoch" || a == "--halo-depth") o.epoch = std::atoi(next().c_str());
     else if (a == "--poll" || a == "--poll-every") o.poll = std::atoi(next().c_str());
@@ -268,6 +280,7 @@ int run(const Options& o) {
     cfg.u8_compute = o.u8_compute;
     cfg.start_gen = o.start_gen;
     cfg.sim_phase = o.sim_phase;
+    cfg.tune = o.tune;
     int ndev = 1;
     if (engine == "hip") {
       GOL_REQUIRE(hip_available(), "--engine hip: no HIP device available");
@@ -289,7 +302,8 @@ int run(const Options& o) {
     std::vector<uint8_t> uid;
     if (comm == "rccl" && P > 1) uid = rccl_unique_id();
     for (int r = 0; r < P; ++r)
-      backends[r] = engine == "hip" ? make_hip_backend(r % ndev) : make_cpu_backend(o.threads > 0 ? o.threads : 0);
+      backends[r] = engine == "hip" ? make_hip_backend(r % ndev, o.tune)
+                                    : make_cpu_backend(o.threads > 0 ? o.threads : 0, -1, o.tune);
     if (P == 1) {
       transports[0] = std::make_unique<SelfTransport>();
     } else if (comm == "rccl") {
@@ -299,7 +313,7 @@ int run(const Options& o) {
         th.emplace_back([&, r] {
           try {
             backends[r]->bind_thread();
-            transports[r] = make_rccl_transport(uid, r, P, r % ndev);
+            transports[r] = make_rccl_transport(uid, r, P, r % ndev, o.tune);
           } catch (const std::exception& e) {
             errs[r] = e.what();
           }
@@ -308,7 +322,7 @@ int run(const Options& o) {
       for (auto& e : errs)
         if (!e.empty()) throw Error(e);
     } else {
-      for (int r = 0; r < P; ++r) transports[r] = std::make_unique<ThreadTransport>(hub, r, backends[r].get());
+      for (int r = 0; r < P; ++r) transports[r] = std::make_unique<ThreadTransport>(hub, r, backends[r].get(), o.tune);
     }
     for (int r = 0; r < P; ++r) {
       engines[r] = std::make_unique<Engine>(cfg, backends[r].get(), transports[r].get());
@@ -410,8 +424,8 @@ int run(const Options& o) {
         m.layout = layout_name(layout);
         // Fault injection (tests): die after the N-th checkpoint's tiles are
         // written, before it is committed.
-        if (const char* c = std::getenv("GOL_FAULT_CHECKPOINT_CRASH"))
-          if (++checkpoints_written == std::atoll(c)) std::_Exit(86);
+        if (const int c = o.tune.i("fault_checkpoint_crash"))
+          if (++checkpoints_written == c) std::_Exit(86);
         checkpoint_commit(o.checkpoint_dir, grid_path, m);
       }
     }
@@ -444,7 +458,8 @@ int run(const Options& o) {
       double cups = res.loop_ms > 0 ? double(o.W) * double(o.H) * double(res.executed) / (res.loop_ms * 1e-3) : 0;
       f << "{\"engine\": \"" << engine << "\", \"backend\": \"" << backends[0]->name()
         << "\", \"layout\": \"" << layout_name(layout) << "\", \"ranks\": " << P
-        << ", \"decomp\": \"" << engines[0]->decomp().describe() << "\", \"W\": " << o.W
+        << ", \"decomp\": \"" << engines[0]->decomp().describe() << "\", \"tuning\": \"" << o.tune.summary()
+        << "\", \"W\": " << o.W
         << ", \"H\": " << o.H << ", \"generations\": " << res.generations
         << ", \"executed\": " << res.executed << ", \"stop_reason\": \"" << res.stop_reason
         << "\", \"loop_ms\": " << res.loop_ms << ", \"read_ms\": " << read_ms

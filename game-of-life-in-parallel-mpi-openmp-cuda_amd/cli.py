@@ -15,7 +15,7 @@ import os
 import sys
 import time
 
-from .models.life import LifeConfig, Simulation, make_backend, reference_run
+from .models.life import LifeConfig, Simulation, make_backend, parse_tune_args, reference_run
 from .utils.metrics import stdout_lines, write_json
 
 
@@ -48,6 +48,8 @@ def parse_args(argv=None):
     p.add_argument("--graphs", default="off", choices=["auto", "on", "off"],
                    help="replay full epochs as captured HIP graphs")
     p.add_argument("--threads", type=int, default=0)
+    p.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                   help="runtime tuning (repeatable; --tune help lists the keys, their GOL_* overrides and defaults)")
     p.add_argument("--style", default="serial", choices=["serial", "mpi", "async", "collective", "openmp", "cuda"])
     p.add_argument("--metrics-json", default=None,
                    help="write run metrics as JSON (per-phase device times with --phase-timing)")
@@ -71,8 +73,18 @@ def parse_args(argv=None):
     return a
 
 
+def print_tuning_keys() -> None:
+    from ._native import native  # noqa: PLC0415
+
+    for k in native().tuning_keys():
+        print(f"{k['key']:<22} {k['class']:<13} {k['env']:<27} default {k['default'] or repr(''):<6} {k['doc']}")
+
+
 def main(argv=None) -> int:
     a = parse_args(argv)
+    if "help" in a.tune:
+        print_tuning_keys()
+        return 0
     if a.input_file is None and a.random is None and a.resume is None:
         print("Finished")
         return 0
@@ -105,13 +117,14 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    backend = make_backend(a.engine, local, a.threads)
+    tune = parse_tune_args(a.tune)
+    backend = make_backend(a.engine, local, a.threads, tune)
     if world > 1:
         from .parallel.dist import init_process_group, make_transport  # noqa: PLC0415
 
         init_process_group("nccl" if backend.is_device() else "gloo",
                            device=int(backend.device()) if backend.is_device() else None)
-        transport = make_transport(a.comm, backend, local)
+        transport = make_transport(a.comm, backend, local, tune=tune)
     else:
         from ._native import native  # noqa: PLC0415
 
@@ -120,7 +133,7 @@ def main(argv=None) -> int:
     cfg = LifeConfig(a.width, a.height, gen_limit=a.gens, check_similarity=not a.no_similarity,
                      sim_freq=a.sim_freq, layout=a.layout, decomp=a.decomp, tmax=a.tmax,
                      epoch=a.epoch, poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs,
-                     u8_compute=a.u8_compute)
+                     u8_compute=a.u8_compute, tune=tune)
     src = a.input_file
     if a.resume:
         from .utils.checkpoint import load_checkpoint  # noqa: PLC0415

@@ -53,6 +53,10 @@ class LifeConfig:
     u8_compute: str = "auto"      # auto | bits | bytes: byte-layout epochs on bit words (packed once per epoch)
                                   # or on the bytes themselves; auto = bits on the GPU with the plain schedule
     flow: str = "auto"            # auto | on | off: runs of equal temporal blocks as one persistent dataflow launch
+    # Runtime tuning, key -> value (``native().tuning_keys()``; csrc/include/gol/tuning.hpp): kernel and
+    # schedule knobs over the GOL_* environment overrides.  Used by the engine and by the backend this
+    # Simulation creates (an explicitly passed backend keeps the tuning it was created with).
+    tune: dict = dataclasses.field(default_factory=dict)
 
     def resolved_layout(self) -> str:
         if self.layout == "auto":
@@ -84,19 +88,53 @@ class LifeConfig:
         c.watchdog_s = float(self.watchdog_s)
         c.u8_compute = {"auto": -1, "bytes": 0, "bits": 1}[self.u8_compute]
         c.flow = {"auto": -1, "off": 0, "on": 1}[self.flow]
+        c.tune = make_tuning(self.tune)
         return c
 
 
-def make_backend(engine: str = "auto", device: int = 0, threads: int = 0):
-    """``hip`` -> MI355X backend on ``device``; ``cpu`` -> threaded host backend."""
+def make_tuning(tune=None):
+    """A native ``Tuning``: the table's defaults, the GOL_* environment, then
+    ``tune`` (a dict key -> value, a list of ``"key=value"`` strings, or a
+    ``Tuning``, returned as a copy).  Unknown keys and non-integer values of
+    integer keys raise."""
+    C = native()
+    if isinstance(tune, C.Tuning):
+        return tune.copy()
+    t = C.Tuning.from_env()
+    items = tune.items() if isinstance(tune, dict) else (kv.split("=", 1) for kv in (tune or []))
+    for k, v in items:
+        t.set(str(k), str(int(v)) if isinstance(v, bool) else str(v))
+    return t
+
+
+def parse_tune_args(pairs) -> dict:
+    """``["key=value", ...]`` (CLI --tune, repeatable) -> dict, validated."""
+    out = {}
+    for kv in pairs or []:
+        if "=" not in kv:
+            raise ValueError(f"--tune {kv!r}: expected key=value")
+        k, v = kv.split("=", 1)
+        out[k] = v
+    make_tuning(out)  # unknown keys / bad values fail here, before any device work
+    return out
+
+
+def make_backend(engine: str = "auto", device: int = 0, threads: int = 0, tune=None):
+    """``hip`` -> MI355X backend on ``device``; ``cpu`` -> threaded host backend.
+    ``tune``: runtime tuning (see make_tuning), read once, here."""
     C = native()
     if engine == "auto":
         engine = "hip" if C.hip_available() else "cpu"
     if engine == "hip":
-        return C.hip_backend(int(device))
+        return C.hip_backend(int(device), tune=make_tuning(tune))
     if engine == "cpu":
-        return C.cpu_backend(int(threads))
+        return C.cpu_backend(int(threads), tune=make_tuning(tune))
     raise ValueError(f"unknown engine {engine!r} (want hip, cpu or auto)")
+
+
+# Tuning keys the engine reads from EngineConfig::tune (engine.cpp); the rest
+# are read by the backend (or the transports) at construction.
+_ENGINE_KEYS = frozenset({"u8_via_bits", "side_poll", "watchdog_s", "pitch_pad", "overlap_auto"})
 
 
 @dataclasses.dataclass
@@ -150,7 +188,7 @@ class Simulation:
         C = native()
         self.config = config
         self.engine_name = engine
-        self.backend = backend if backend is not None else make_backend(engine, device, threads)
+        self.backend = backend if backend is not None else make_backend(engine, device, threads, config.tune)
         self.transport = transport if transport is not None else C.self_transport()
         self._eng = C.Engine(config.to_native(), self.backend, self.transport)
         self.last_report: Optional[RunReport] = None
@@ -205,7 +243,25 @@ class Simulation:
                 "u8_compute": ("bits" if self._eng.via_bits else "bytes") if self.config.resolved_layout() == "u8" else None,
                 "row_ring": bool(self._eng.row_ring), "flow": bool(self._eng.flow),
                 "flow_plan": self.backend.flow_desc(),
-                "kernel": self._kernel_name()}
+                "kernel": self._kernel_name(),
+                "tuning": self.tuning(), "tuning_changed": self.tuning_changed()}
+
+    def tuning(self) -> dict[str, str]:
+        """Effective value of every tuning key of class ``tune`` (the default
+        build's knobs): the backend's for its keys, the engine's for the keys
+        it reads."""
+        be, eng = self.backend.tuning().values(), self._eng.config.tune.values()
+        keys = [k for k in native().tuning_keys() if k["class"] == "tune"]
+        return {k["key"]: (eng if k["key"] in _ENGINE_KEYS else be)[k["key"]] for k in keys}
+
+    def tuning_changed(self) -> dict[str, str]:
+        """Every key off its default, any class: ``value (source)``, source
+        ``env`` (a GOL_* variable) or ``set`` (LifeConfig.tune / --tune)."""
+        out = {}
+        for t in (self.backend.tuning(), self._eng.config.tune):
+            for k, v in t.changed().items():
+                out.setdefault(k, f"{v} ({t.source(k)})")
+        return out
 
     def _kernel_name(self) -> str:
         """What the temporal blocks run, for reports (bench.py config.kernel)."""

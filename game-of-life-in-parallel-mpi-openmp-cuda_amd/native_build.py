@@ -38,7 +38,7 @@ BUILD = REPO / "build" / ("obj_exp" if EXPERIMENTAL else "obj")
 MODE_STAMP = PKG_DIR / "_gol.mode"  # which mode _gol.so / bin/* were linked in (travels with the .so)
 
 HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/transport.cpp",
-             "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp"]
+             "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp", "src/tuning.cpp"]
 LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_add", "u8_w1_dpp", "u8_w1_add",
                  *[f"u8_w1_dpp_t{t}" for t in (24, 32)],  # deep byte passes
                  "u8_w1_dpp_t48"]  # pipelined wave pairs (life_pipe_impl.hpp)

@@ -145,18 +145,21 @@ def torch_transport(backend_obj, group=None):
     return native().callback_transport(rank, world, exchange, allreduce, barrier)
 
 
-def rccl_transport(device: int, group=None):
-    """Native RCCL communicator, uid broadcast over the torch process group."""
+def rccl_transport(device: int, group=None, tune=None):
+    """Native RCCL communicator, uid broadcast over the torch process group
+    (``tune``: side_poll / cu_partition, see models.life.make_tuning)."""
+    from ..models.life import make_tuning  # noqa: PLC0415
+
     import torch.distributed as dist  # noqa: PLC0415
 
     C = native()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     obj = [C.rccl_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0, group=group)
-    return C.rccl_transport(obj[0], rank, world, int(device))
+    return C.rccl_transport(obj[0], rank, world, int(device), tune=make_tuning(tune))
 
 
-def make_transport(kind: str, backend_obj, device: int = 0):
+def make_transport(kind: str, backend_obj, device: int = 0, tune=None):
     """``self`` (1 rank) | ``rccl`` | ``torch``; ``auto`` -> rccl on GPU, torch on CPU."""
     import torch.distributed as dist  # noqa: PLC0415
 
@@ -165,7 +168,7 @@ def make_transport(kind: str, backend_obj, device: int = 0):
     if kind == "auto":
         kind = "rccl" if backend_obj.is_device() else "torch"
     if kind == "rccl":
-        return rccl_transport(device)
+        return rccl_transport(device, tune=tune)
     if kind == "torch":
         return torch_transport(backend_obj)
     raise ValueError(f"unknown transport {kind!r}")

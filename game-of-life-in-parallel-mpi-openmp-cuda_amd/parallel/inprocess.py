@@ -18,7 +18,7 @@ from typing import Callable, Optional, Sequence
 import numpy as np
 
 from .._native import native
-from ..models.life import LifeConfig, RunReport, Simulation, make_backend
+from ..models.life import LifeConfig, RunReport, Simulation, make_backend, make_tuning
 
 
 class InProcessGroup:
@@ -34,9 +34,10 @@ class InProcessGroup:
         # Every backend before any engine: an engine's schedule may depend on
         # how many ranks share its device (resident epochs need a whole GPU),
         # and all ranks must take the same decision.
-        self.backends = [make_backend(engine, devs[r % len(devs)], threads_per_rank) for r in range(self.nranks)]
+        self.backends = [make_backend(engine, devs[r % len(devs)], threads_per_rank, config.tune)
+                         for r in range(self.nranks)]
         for r, be in enumerate(self.backends):
-            tr = C.thread_transport(self.hub, r, be)
+            tr = C.thread_transport(self.hub, r, be, tune=make_tuning(config.tune))
             self.sims.append(Simulation(config, transport=tr, backend=be))
 
     def parallel(self, fn: Callable[[Simulation], object]) -> list:

@@ -49,6 +49,14 @@ def gpu(native):
     return native
 
 
+@pytest.fixture
+def tune() -> dict:
+    """Runtime tuning a test passes through LifeConfig.tune and the backends
+    it makes (csrc/include/gol/tuning.hpp); test modules override it with
+    their own defaults."""
+    return {}
+
+
 @pytest.fixture(scope="session")
 def repo() -> Path:
     return REPO

@@ -11,22 +11,23 @@ import numpy as np
 import pytest
 
 from gol_amd import LifeConfig, Simulation, random_grid, reference_run
+from gol_amd.models.life import make_tuning
 from gol_amd.parallel import InProcessGroup
 
 from golden import CONVERGING
 
 
 def sim_with(native, cfg, drift):
-    return Simulation(cfg, backend=native.cpu_backend(2, drift))
+    return Simulation(cfg, backend=native.cpu_backend(2, drift, tune=make_tuning(cfg.tune)))
 
 
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("tmax,epoch", [(16, 0), (8, 24), (4, 12), (3, 7)])
-def test_drift_frame_matches_reference(native, layout, tmax, epoch):
+def test_drift_frame_matches_reference(native, tune, layout, tmax, epoch):
     W, H = 256, 90
     g = random_grid(W, H, 17 + tmax)
     ref, rgens, _ = reference_run(g, 300)
-    sim = sim_with(native, LifeConfig(W, H, gen_limit=300, layout=layout, tmax=tmax, epoch=epoch), 1)
+    sim = sim_with(native, LifeConfig(W, H, gen_limit=300, layout=layout, tmax=tmax, epoch=epoch, tune=tune), 1)
     sim.load(g)
     rep = sim.run()
     assert sim.native_engine.drift == rep.executed % W  # every block drifted
@@ -35,10 +36,10 @@ def test_drift_frame_matches_reference(native, layout, tmax, epoch):
     assert sim.native_engine.drift == 0  # the read-out rotated it out
 
 
-def test_drift_accumulates_and_wraps(native):
+def test_drift_accumulates_and_wraps(native, tune):
     W, H = 64, 40
     g = random_grid(W, H, 3)
-    sim = sim_with(native, LifeConfig(W, H, gen_limit=10_000, tmax=16, epoch=32), 1)
+    sim = sim_with(native, LifeConfig(W, H, gen_limit=10_000, tmax=16, epoch=32, tune=tune), 1)
     sim.load(g)
     eng = sim.native_engine
     for n in (5, 16, 59, 64, 100):
@@ -51,14 +52,14 @@ def test_drift_accumulates_and_wraps(native):
     assert (sim.tile() == want).all()
 
 
-def test_drift_needs_whole_width_tiles(native, monkeypatch):
+def test_drift_needs_whole_width_tiles(native, tune):
     """Column decompositions (Px > 1) keep the symmetric kernel: a drift would
     move cells across rank boundaries."""
-    monkeypatch.setenv("GOL_CPU_DRIFT", "1")
+    tune["cpu_drift"] = "1"
     W, H = 128, 64
     g = random_grid(W, H, 8)
     ref, rgens, _ = reference_run(g, 150)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=150, decomp="2x2", tmax=8), 4, engine="cpu")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=150, decomp="2x2", tmax=8, tune=tune), 4, engine="cpu")
     assert all("drift" in s.backend.name() for s in grp.sims)
     grp.load(g)
     reps = grp.run()
@@ -68,15 +69,15 @@ def test_drift_needs_whole_width_tiles(native, monkeypatch):
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x3", 3), ("1x4", 4)])
 @pytest.mark.parametrize("overlap", ["off", "on", "edges"])
-def test_drift_row_strips_and_overlap(native, monkeypatch, spec, P, overlap):
+def test_drift_row_strips_and_overlap(native, tune, spec, P, overlap):
     """Row strips (the multi-GPU default) drift in lockstep on every rank;
     the early-boundary launches and the edge scratch tiles drift with the
     interior."""
-    monkeypatch.setenv("GOL_CPU_DRIFT", "1")
+    tune["cpu_drift"] = "1"
     W, H = 192, 120
     g = random_grid(W, H, P + 40)
     ref, rgens, _ = reference_run(g, 200)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=200, decomp=spec, tmax=4, epoch=12, overlap=overlap), P,
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=200, decomp=spec, tmax=4, epoch=12, overlap=overlap, tune=tune), P,
                          engine="cpu")
     grp.load(g)
     reps = grp.run()
@@ -86,22 +87,22 @@ def test_drift_row_strips_and_overlap(native, monkeypatch, spec, P, overlap):
 
 
 @pytest.mark.parametrize("W,H,seed,density", [c for c in CONVERGING if c[0] % 32 == 0][:4])
-def test_drift_termination_exact(native, W, H, seed, density):
+def test_drift_termination_exact(native, tune, W, H, seed, density):
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
-    sim = sim_with(native, LifeConfig(W, H, tmax=8, epoch=16, poll_gens=16), 1)
+    sim = sim_with(native, LifeConfig(W, H, tmax=8, epoch=16, poll_gens=16, tune=tune), 1)
     sim.load(g)
     rep = sim.run()
     assert rep.generations == rgens
     assert (sim.tile() == ref).all()
 
 
-def test_rotate_cols_matches_numpy(native):
+def test_rotate_cols_matches_numpy(native, tune):
     """The rotated-out drifted buffer equals the non-drifting backend's tile."""
     W, H = 96, 20
     g = random_grid(W, H, 21)
-    a = sim_with(native, LifeConfig(W, H, gen_limit=50, tmax=4, epoch=8), 1)
-    b = sim_with(native, LifeConfig(W, H, gen_limit=50, tmax=4, epoch=8), 0)
+    a = sim_with(native, LifeConfig(W, H, gen_limit=50, tmax=4, epoch=8, tune=tune), 1)
+    b = sim_with(native, LifeConfig(W, H, gen_limit=50, tmax=4, epoch=8, tune=tune), 0)
     for s in (a, b):
         s.load(g)
         s.advance(37)

@@ -13,19 +13,20 @@ from gol_amd.parallel import InProcessGroup
 from golden import CONVERGING
 
 
-@pytest.fixture(autouse=True)
-def _flow(monkeypatch):
-    monkeypatch.setenv("GOL_CPU_FLOW", "1")
+@pytest.fixture
+def tune():
+    """Tuning passed through LifeConfig.tune (gol/tuning.hpp): the CPU backend accepts flow runs."""
+    return {"cpu_flow": "1"}
 
 
 @pytest.mark.parametrize("ring", ["0", "1"])
 @pytest.mark.parametrize("drift", ["0", "1"])
 @pytest.mark.parametrize("layout,u8c", [("bits", "auto"), ("u8", "bits")])
-def test_flow_single_rank_matches_oracle(native, monkeypatch, ring, drift, layout, u8c):
-    monkeypatch.setenv("GOL_CPU_RING", ring)
-    monkeypatch.setenv("GOL_CPU_DRIFT", drift)
+def test_flow_single_rank_matches_oracle(native, tune, ring, drift, layout, u8c):
+    tune["cpu_ring"] = ring
+    tune["cpu_drift"] = drift
     W, H = 256, 128
-    sim = Simulation(LifeConfig(W, H, layout=layout, u8_compute=u8c, tmax=8, gen_limit=2000, poll_gens=64),
+    sim = Simulation(LifeConfig(W, H, layout=layout, u8_compute=u8c, tmax=8, gen_limit=2000, poll_gens=64, tune=tune),
                      engine="cpu")
     d = sim.describe()
     assert d["flow"] is True
@@ -42,9 +43,9 @@ def test_flow_single_rank_matches_oracle(native, monkeypatch, ring, drift, layou
     assert sim.last_report.flow_launches == 0  # 3 generations: no run of two blocks
 
 
-def test_flow_counts_blocks(native, monkeypatch):
-    monkeypatch.setenv("GOL_CPU_RING", "1")
-    sim = Simulation(LifeConfig(128, 64, tmax=8, gen_limit=1000, poll_gens=64), engine="cpu")
+def test_flow_counts_blocks(native, tune):
+    tune["cpu_ring"] = "1"
+    sim = Simulation(LifeConfig(128, 64, tmax=8, gen_limit=1000, poll_gens=64, tune=tune), engine="cpu")
     sim.load(random_grid(128, 64, 3))
     rep = sim.advance(200)  # 3 windows of 64 (8 blocks each) + 8: three flow runs and one block
     assert rep.flow_launches == 3
@@ -52,9 +53,9 @@ def test_flow_counts_blocks(native, monkeypatch):
     assert rep.kernel_launches == 4
 
 
-def test_flow_off(native, monkeypatch):
-    monkeypatch.setenv("GOL_CPU_RING", "1")
-    sim = Simulation(LifeConfig(128, 64, tmax=8, gen_limit=100, flow="off"), engine="cpu")
+def test_flow_off(native, tune):
+    tune["cpu_ring"] = "1"
+    sim = Simulation(LifeConfig(128, 64, tmax=8, gen_limit=100, flow="off", tune=tune), engine="cpu")
     assert sim.describe()["flow"] is False
     sim.load(random_grid(128, 64, 3))
     assert sim.advance(64).flow_launches == 0
@@ -62,11 +63,11 @@ def test_flow_off(native, monkeypatch):
 
 @pytest.mark.parametrize("W,H,seed,density", [c for c in CONVERGING if c[1] % 16 == 0][:4])
 @pytest.mark.parametrize("ring", ["0", "1"])
-def test_flow_termination_is_exact(native, monkeypatch, W, H, seed, density, ring):
-    monkeypatch.setenv("GOL_CPU_RING", ring)
+def test_flow_termination_is_exact(native, tune, W, H, seed, density, ring):
+    tune["cpu_ring"] = ring
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
-    sim = Simulation(LifeConfig(W, H, tmax=4, poll_gens=32), engine="cpu")
+    sim = Simulation(LifeConfig(W, H, tmax=4, poll_gens=32, tune=tune), engine="cpu")
     sim.load(g)
     rep = sim.run()
     assert rep.generations == rgens
@@ -76,7 +77,7 @@ def test_flow_termination_is_exact(native, monkeypatch, W, H, seed, density, rin
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("2x2", 4), ("2x3", 6)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("overlap", ["off", "on"])
-def test_flow_multirank_trapezoid_epochs(native, spec, P, layout, overlap):
+def test_flow_multirank_trapezoid_epochs(native, tune, spec, P, layout, overlap):
     """Deep-halo epochs of several ranks: one flow run per epoch whose blocks
     shrink by T rows per side (the early-boundary schedule keeps its split
     last block out of the run)."""
@@ -84,7 +85,7 @@ def test_flow_multirank_trapezoid_epochs(native, spec, P, layout, overlap):
     g = random_grid(W, H, 77)
     ref, rgens, _ = reference_run(g, 150)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=150, decomp=spec, layout=layout, tmax=4, epoch=16,
-                                    overlap=overlap), P, engine="cpu")
+                                    overlap=overlap, tune=tune), P, engine="cpu")
     assert all(s.describe()["flow"] for s in grp.sims)
     grp.load(g)
     reps = grp.run()
@@ -93,10 +94,11 @@ def test_flow_multirank_trapezoid_epochs(native, spec, P, layout, overlap):
     assert all(r.flow_launches > 0 for r in reps)
 
 
-def test_flow_self_exchange_rehearsal(native):
+def test_flow_self_exchange_rehearsal(native, tune):
     W, H = 128, 96
     g = random_grid(W, H, 4)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=100, tmax=4, epoch=16, self_exchange=True), 1, engine="cpu")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=100, tmax=4, epoch=16, self_exchange=True, tune=tune), 1,
+                         engine="cpu")
     grp.load(g)
     rep = grp.sims[0].advance(70)
     assert rep.flow_launches >= 4

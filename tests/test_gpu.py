@@ -6,6 +6,7 @@ import pytest
 
 from gol_amd import LifeConfig, Simulation, life_step, life_step_numpy, life_step_torch, random_grid, \
     reference_run, simulate
+from gol_amd.models.life import make_tuning
 from gol_amd.parallel import InProcessGroup
 
 from golden import CASES, CONVERGING, GLIDER
@@ -17,16 +18,18 @@ experimental = pytest.mark.experimental
 X = experimental
 
 
-@pytest.fixture(autouse=True)
-def _byte_kernels(monkeypatch):
-    """The byte-layout tests here exercise the byte kernels themselves; the
-    GPU's default byte-layout path (bit words, EngineConfig::u8_compute auto)
-    has its own tests at the end of this file (test_u8_via_bits_*)."""
-    monkeypatch.setenv("GOL_U8_VIA_BITS", "0")
+@pytest.fixture
+def tune():
+    """Runtime tuning each test passes through LifeConfig.tune and the
+    backends it makes (gol/tuning.hpp).  The byte-layout tests here exercise
+    the byte kernels themselves; the GPU's default byte-layout path (bit
+    words, EngineConfig::u8_compute auto) has its own tests at the end of this
+    file (test_u8_via_bits_*), which drop the key."""
+    return {"u8_via_bits": "0"}
 
 
-def test_hip_backend_is_native_gfx950(gpu):
-    be = gpu.hip_backend(0)
+def test_hip_backend_is_native_gfx950(gpu, tune):
+    be = gpu.hip_backend(0, tune=make_tuning(tune))
     assert be.is_device()
     assert "gfx950" in be.name()
 
@@ -63,13 +66,13 @@ def test_every_temporal_block_size(gpu, tmax, layout):
     pytest.param(*v, marks=X) for v in [(1, 1, 0), (1, 2, 0), (2, 0, 0), (2, 2, 0), (1, 0, 1), (1, 2, 1), (2, 0, 1),
                                         (1, 3, 1)]])
 @pytest.mark.parametrize("tmax", [1, 4, 8, 12, 16])
-def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
+def test_kernel_variants_vs_torch(gpu, tune, wpl, xlane, skew, tmax):
     """Every compiled life_block variant (words/lane x DPP|bpermute|carry x
     schedule) against the fp32 conv oracle, including the changed-flag
     termination."""
-    monkeypatch.setenv("GOL_WPL", str(wpl))
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
-    monkeypatch.setenv("GOL_SKEW", str(skew))
+    tune["wpl"] = str(wpl)
+    tune["xlane"] = str(xlane)
+    tune["skew"] = str(skew)
     # 4000 cells wide: 125 words -> tail handling in the last column wave.
     W, H = 4000 - 4000 % 32, 333
     g = random_grid(W, H, 11 * wpl + tmax)
@@ -86,8 +89,8 @@ def test_kernel_variants_vs_torch(gpu, monkeypatch, wpl, xlane, skew, tmax):
 
 @pytest.mark.parametrize("xlane", [0, pytest.param(2, marks=X), 3])
 @pytest.mark.parametrize("tmax", [1, 8, 16])
-def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
+def test_u8_kernel_variants_vs_torch(gpu, tune, xlane, tmax):
+    tune["xlane"] = str(xlane)
     W, H = 1999, 301
     g = random_grid(W, H, 5 + tmax)
     gens = 2 * tmax + 5
@@ -97,18 +100,18 @@ def test_u8_kernel_variants_vs_torch(gpu, monkeypatch, xlane, tmax):
 
 @pytest.mark.parametrize("tmax", [24, 32])
 @pytest.mark.parametrize("xlane", [0, pytest.param(2, marks=X), 3])
-def test_deep_byte_passes_vs_torch(gpu, monkeypatch, tmax, xlane):
+def test_deep_byte_passes_vs_torch(gpu, tune, tmax, xlane):
     """T = 24 / 32 byte-layout passes (life_block_u8_w1_*_t24/_t32.hip, the
     HBM-bound layout's deep passes) in every byte variant and schedule,
     against the fp32 conv oracle, and the exact Generations count."""
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    tune["xlane"] = str(xlane)
     for group in ("8", "4", "0"):
-        monkeypatch.setenv("GOL_GROUP", group)
+        tune["group"] = group
         for W, H in [(32 * 200, 900), (1999, 777)]:
             g = random_grid(W, H, W + H + tmax)
             gens = 2 * tmax + 7
             want = life_step_torch(g, gens, device="cuda")
-            sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=tmax), engine="hip")
+            sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=tmax, tune=tune), engine="hip")
             assert sim.describe()["tmax"] == tmax
             sim.load(g)
             sim.advance(gens)
@@ -125,13 +128,13 @@ def test_deep_byte_passes_vs_torch(gpu, monkeypatch, tmax, xlane):
 @pytest.mark.parametrize("group", ["0", "4", "8", "-1"])
 @pytest.mark.parametrize("tmax", [4, 8, 12, 16])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_grouped_schedule_vs_torch(gpu, monkeypatch, group, tmax, layout):
+def test_grouped_schedule_vs_torch(gpu, tune, group, tmax, layout):
     """Grouped schedule (csrc/kernels/life_group_impl.hpp: the M waves of a
     workgroup share their segment boundaries through LDS, so only group
     boundaries keep the redundant triangle) against the fp32 conv oracle:
     several groups per strip, uneven group sizes, last-wave remainders, tail
     words.  GOL_GROUP=0 is the classic schedule, -1 the model's choice."""
-    monkeypatch.setenv("GOL_GROUP", group)
+    tune["group"] = group
     for W, H in [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333)]:
         g = random_grid(W, H, W + H + tmax)
         gens = 2 * tmax + 3
@@ -142,18 +145,18 @@ def test_grouped_schedule_vs_torch(gpu, monkeypatch, group, tmax, layout):
 @pytest.mark.parametrize("group", ["0", "4", "8", "-1"])
 @pytest.mark.parametrize("tmax", [2, 4, 8, 12, 16])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_adder_window_vs_torch(gpu, monkeypatch, group, tmax, layout):
+def test_adder_window_vs_torch(gpu, tune, group, tmax, layout):
     """The DPP-free adder window (GOL_XLANE=3, kXlaneAdd: one-sided horizontal
     window from add-with-carry lane masks, storage frame drifting T cells per
     block) in every schedule, against the fp32 conv oracle; the drift is
     rotated out by the read-out."""
-    monkeypatch.setenv("GOL_XLANE", "3")
-    monkeypatch.setenv("GOL_GROUP", group)
+    tune["xlane"] = "3"
+    tune["group"] = group
     for W, H in [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (64, 40), (32, 3)]:
         g = random_grid(W, H, W + H + tmax)
         gens = 2 * tmax + 3
         want = life_step_torch(g, gens, device="cuda")
-        sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout=layout, tmax=tmax), engine="hip")
+        sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout=layout, tmax=tmax, tune=tune), engine="hip")
         sim.load(g)
         sim.advance(gens)
         assert sim.native_engine.drift == gens % W, (W, H)
@@ -162,18 +165,18 @@ def test_adder_window_vs_torch(gpu, monkeypatch, group, tmax, layout):
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("1x8", 8)])
 @pytest.mark.parametrize("overlap", ["off", "on"])
-def test_adder_window_row_strips_and_termination(gpu, monkeypatch, spec, P, overlap):
+def test_adder_window_row_strips_and_termination(gpu, tune, spec, P, overlap):
     """Row-strip subdomains on one GPU (the multi-GPU default decomposition)
     with the drifting adder window: lockstep drift, overlapped edges, exact
     Generations."""
-    monkeypatch.setenv("GOL_XLANE", "3")
+    tune["xlane"] = "3"
     for W, H, seed, density in [c for c in CONVERGING if c[0] % 32 == 0][:3] + [(256, 512, 77, 0.5)]:
         if H < 8 * P:
             continue
         g = random_grid(W, H, seed, density)
         ref, rgens, _ = reference_run(g)
-        grp = InProcessGroup(LifeConfig(W, H, decomp=spec, tmax=8, epoch=16, poll_gens=32, overlap=overlap), P,
-                             engine="hip")
+        grp = InProcessGroup(LifeConfig(W, H, decomp=spec, tmax=8, epoch=16, poll_gens=32, overlap=overlap,
+                                        tune=tune), P, engine="hip")
         grp.load(g)
         reps = grp.run()
         assert {r.generations for r in reps} == {rgens}, (W, H, seed)
@@ -181,11 +184,11 @@ def test_adder_window_row_strips_and_termination(gpu, monkeypatch, spec, P, over
 
 
 @pytest.mark.parametrize("group", ["4", "8"])
-def test_grouped_schedule_many_groups_and_termination(gpu, monkeypatch, group):
+def test_grouped_schedule_many_groups_and_termination(gpu, tune, group):
     """As many groups as the rows allow (GOL_TARGET_WAVES), and the exact
     Generations count when the grid settles inside a grouped launch."""
-    monkeypatch.setenv("GOL_GROUP", group)
-    monkeypatch.setenv("GOL_TARGET_WAVES", "1000000")
+    tune["group"] = group
+    tune["target_waves"] = "1000000"
     g = random_grid(2048, 1500, 9)
     for tmax in (8, 16):
         want = life_step_torch(g, 3 * tmax + 1, device="cuda")
@@ -204,26 +207,26 @@ def test_grouped_schedule_many_groups_and_termination(gpu, monkeypatch, group):
 @pytest.mark.parametrize("layout", ["bits", "u8"])  # u8: falls back to the grouped kernel
 @pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
-def test_short_segment_schedule_vs_torch(gpu, monkeypatch, layout, W, H, xlane, tmax):
+def test_short_segment_schedule_vs_torch(gpu, tune, layout, W, H, xlane, tmax):
     """Short-segment groups (csrc/kernels/life_short_impl.hpp: segments of
     Q < 2T rows, the whole sweep unrolled, level rows of the lower wave handed
     over through LDS with per-level flags) forced on, against the fp32 conv
     oracle; several segment lengths Q via the wave-count target."""
-    monkeypatch.setenv("GOL_SHORT", "2")
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    tune["short"] = "2"
+    tune["xlane"] = str(xlane)
     g = random_grid(W, H, W * 3 + H)
     want = life_step_torch(g, 35, device="cuda")
     for target in ("0", "100000", "3000"):
-        monkeypatch.setenv("GOL_TARGET_WAVES", target)
+        tune["target_waves"] = target
         assert (life_step(g, 35, engine="hip", layout=layout, tmax=tmax) == want).all(), target
 
 
 @experimental
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
-def test_short_segment_schedule_termination(gpu, monkeypatch, xlane, tmax):
-    monkeypatch.setenv("GOL_SHORT", "2")
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
-    monkeypatch.setenv("GOL_TARGET_WAVES", "100000")
+def test_short_segment_schedule_termination(gpu, tune, xlane, tmax):
+    tune["short"] = "2"
+    tune["xlane"] = str(xlane)
+    tune["target_waves"] = "100000"
     grid = np.zeros((1024, 512), dtype=np.uint8)
     W, H, seed, density = CONVERGING[5]
     grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
@@ -237,18 +240,18 @@ def test_short_segment_schedule_termination(gpu, monkeypatch, xlane, tmax):
 @experimental
 @pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (3, 16), (0, 12)])
-def test_pipe_schedule_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
+def test_pipe_schedule_vs_torch(gpu, tune, W, H, xlane, tmax):
     """Level-pipelined wave pairs (csrc/kernels/life_pipe_impl.hpp: stage A
     runs levels 0..T/2-1 and hands its rows to stage B through an LDS ring)
     forced on, against the fp32 conv oracle; several group shapes via the
     wave-count target."""
-    monkeypatch.setenv("GOL_PIPE", "2")
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    tune["pipe"] = "2"
+    tune["xlane"] = str(xlane)
     g = random_grid(W, H, W * 5 + H)
     want = life_step_torch(g, 2 * tmax + 11, device="cuda")
     for target in ("0", "100000", "3000"):
-        monkeypatch.setenv("GOL_TARGET_WAVES", target)
-        sim = Simulation(LifeConfig(W, H, gen_limit=2 * tmax + 11, tmax=tmax), engine="hip")
+        tune["target_waves"] = target
+        sim = Simulation(LifeConfig(W, H, gen_limit=2 * tmax + 11, tmax=tmax, tune=tune), engine="hip")
         assert "pipe=forced" in sim.describe()["backend"]
         sim.load(g)
         sim.advance(2 * tmax + 11)
@@ -257,12 +260,12 @@ def test_pipe_schedule_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
 
 @experimental
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
-def test_pipe_schedule_termination(gpu, monkeypatch, xlane, tmax):
+def test_pipe_schedule_termination(gpu, tune, xlane, tmax):
     """Exact Generations with the pipelined pairs: both stages raise their
     levels' change flags."""
-    monkeypatch.setenv("GOL_PIPE", "2")
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
-    monkeypatch.setenv("GOL_TARGET_WAVES", "100000")
+    tune["pipe"] = "2"
+    tune["xlane"] = str(xlane)
+    tune["target_waves"] = "100000"
     grid = np.zeros((1024, 512), dtype=np.uint8)
     W, H, seed, density = CONVERGING[5]
     grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
@@ -276,36 +279,36 @@ def test_pipe_schedule_termination(gpu, monkeypatch, xlane, tmax):
                                  (32768, 600)])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (0, 8), (3, 4), (0, 12)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_chained_groups_vs_torch(gpu, monkeypatch, W, H, xlane, tmax, layout):
+def test_chained_groups_vs_torch(gpu, tune, W, H, xlane, tmax, layout):
     """Chained groups (GOL_CHAIN=1, life_group_impl.hpp chain_fetch: the last
     wave of every group but a strip's last ends with the inverted triangle fed
     by the next group's wave 0 through global memory and a per-launch flag)
     against the fp32 conv oracle; few, many (several dispatch rounds) and a
     middle number of groups via the wave-count target."""
-    monkeypatch.setenv("GOL_CHAIN", "1")
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    tune["chain"] = "1"
+    tune["xlane"] = str(xlane)
     g = random_grid(W, H, W * 7 + H)
     gens = 2 * tmax + 11
     want = life_step_torch(g, gens, device="cuda")
     for target in ("0", "100000", "3000"):
-        monkeypatch.setenv("GOL_TARGET_WAVES", target)
-        sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout=layout, tmax=tmax), engine="hip")
+        tune["target_waves"] = target
+        sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout=layout, tmax=tmax, tune=tune), engine="hip")
         assert " chain" in sim.describe()["backend"]
         sim.load(g)
         sim.advance(gens)
         assert (sim.tile() == want).all(), target
 
 
-def test_chain_autotuning_is_exact(gpu, monkeypatch, capfd):
+def test_chain_autotuning_is_exact(gpu, tune, capfd):
     """Default launch-shape autotuning (GOL_CHAIN=-1): trial launches of both
     options (timed with events) and the settled choice give the same rows as
     the fp32 conv oracle, and every launch shape reaches a decision."""
-    monkeypatch.setenv("GOL_CHAIN", "-1")
-    monkeypatch.setenv("GOL_TUNE_LOG", "1")
+    tune["chain"] = "-1"
+    tune["tune_log"] = "1"
     W, H, gens = 8192, 1024, 16 * 12
     g = random_grid(W, H, 4242)
     want = life_step_torch(g, gens, device="cuda")
-    sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=16, epoch=32), engine="hip")
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=16, epoch=32, tune=tune), engine="hip")
     assert "chain=tuned" in sim.describe()["backend"]
     sim.load(g)
     sim.advance(gens // 2)  # the trials (6 launches per shape); returns with the device idle
@@ -316,11 +319,11 @@ def test_chain_autotuning_is_exact(gpu, monkeypatch, capfd):
 
 
 @pytest.mark.parametrize("graphs", ["off", "on"])
-def test_chained_groups_termination_and_row_strips(gpu, monkeypatch, graphs):
+def test_chained_groups_termination_and_row_strips(gpu, tune, graphs):
     """Exact Generations with chained groups, in graph capture (where the
     chain is off) and on 1x4 row-strip subdomains of one GPU."""
-    monkeypatch.setenv("GOL_CHAIN", "1")
-    monkeypatch.setenv("GOL_TARGET_WAVES", "100000")
+    tune["chain"] = "1"
+    tune["target_waves"] = "100000"
     grid = np.zeros((1024, 512), dtype=np.uint8)
     W, H, seed, density = CONVERGING[5]
     grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
@@ -329,8 +332,8 @@ def test_chained_groups_termination_and_row_strips(gpu, monkeypatch, graphs):
         out, rep = simulate(grid, 1000, engine="hip", layout=layout, tmax=16, graphs=graphs)
         assert rep.generations == rgens, layout
         assert (out == ref).all(), layout
-    grp = InProcessGroup(LifeConfig(512, 1024, decomp="1x4", tmax=16, epoch=64, poll_gens=64, graphs=graphs), 4,
-                         engine="hip")
+    grp = InProcessGroup(LifeConfig(512, 1024, decomp="1x4", tmax=16, epoch=64, poll_gens=64, graphs=graphs,
+                                    tune=tune), 4, engine="hip")
     grp.load(grid)
     reps = grp.run()
     assert {r.generations for r in reps} == {rgens}
@@ -340,7 +343,7 @@ def test_chained_groups_termination_and_row_strips(gpu, monkeypatch, graphs):
 @pytest.mark.parametrize("words", [79, 93, 136, 1024])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (0, 8), (3, 4)])
 @pytest.mark.parametrize("wrap,fold", [("1", "1"), ("1", "0"), ("0", "0")])
-def test_wrap_and_folded_strip_vs_torch(gpu, monkeypatch, words, xlane, tmax, wrap, fold):
+def test_wrap_and_folded_strip_vs_torch(gpu, tune, words, xlane, tmax, wrap, fold):
     """Wrap mode (whole-width tiles read owned words mod the width, no halo
     columns; csrc/kernels/life_block_impl.hpp lane_cols) and the folded last
     strip (life_group_kernel: the narrow last strip's lanes packed 2-4 times
@@ -348,16 +351,16 @@ def test_wrap_and_folded_strip_vs_torch(gpu, monkeypatch, words, xlane, tmax, wr
     fp32 conv oracle.  Widths: 79 / 93 / 136 words leave a last strip of
     16 / 30 / 10 words (fold 3 / 2 / 4); several group counts, including ones
     that leave a partial fold and unequal group sizes."""
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
-    monkeypatch.setenv("GOL_WRAP", wrap)
-    monkeypatch.setenv("GOL_FOLD", fold)
+    tune["xlane"] = str(xlane)
+    tune["wrap"] = wrap
+    tune["fold"] = fold
     W, H = 32 * words, 613 if words < 1024 else 300
     g = random_grid(W, H, words * 7 + tmax)
     gens = 2 * tmax + 5
     want = life_step_torch(g, gens, device="cuda")
     for target in ("0", "2000", "100000"):
-        monkeypatch.setenv("GOL_TARGET_WAVES", target)
-        sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax), engine="hip")
+        tune["target_waves"] = target
+        sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax, tune=tune), engine="hip")
         sim.load(g)
         sim.advance(gens)
         assert (sim.tile() == want).all(), target
@@ -365,28 +368,28 @@ def test_wrap_and_folded_strip_vs_torch(gpu, monkeypatch, words, xlane, tmax, wr
 
 @pytest.mark.parametrize("words", [1, 2, 3, 31, 32, 33, 62, 63, 64, 65, 94, 125, 126, 127, 129, 190])
 @pytest.mark.parametrize("xlane", [0, 3])
-def test_wrap_mode_widths_vs_torch(gpu, monkeypatch, words, xlane):
+def test_wrap_mode_widths_vs_torch(gpu, tune, words, xlane):
     """Wrap mode across torus widths: narrower than one strip (lanes wrap
     several times around the row), one word either side of a strip boundary,
     and every fold factor of the last strip (1-4)."""
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    tune["xlane"] = str(xlane)
     W, H = 32 * words, 97 + words
     g = random_grid(W, H, words * 13 + xlane)
     for tmax in (16, 12, 4):
         gens = tmax + 7
         want = life_step_torch(g, gens, device="cuda")
-        sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax), engine="hip")
+        sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax, tune=tune), engine="hip")
         sim.load(g)
         sim.advance(gens)
         assert (sim.tile() == want).all(), tmax
 
 
 @pytest.mark.parametrize("xlane", [0, 3])
-def test_folded_strip_termination_and_row_strips(gpu, monkeypatch, xlane):
+def test_folded_strip_termination_and_row_strips(gpu, tune, xlane):
     """Exact Generations with a folded last strip (the change flags of every
     sub-strip), and row-strip subdomains (Px = 1, so wrap mode on every rank)."""
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
-    monkeypatch.setenv("GOL_TARGET_WAVES", "3000")
+    tune["xlane"] = str(xlane)
+    tune["target_waves"] = "3000"
     grid = np.zeros((700, 32 * 79), dtype=np.uint8)
     W, H, seed, density = CONVERGING[5]
     grid[300:300 + H, 2500 - W:2500] = random_grid(W, H, seed, density)  # straddles the folded strip
@@ -394,32 +397,33 @@ def test_folded_strip_termination_and_row_strips(gpu, monkeypatch, xlane):
     out, rep = simulate(grid, 1000, engine="hip", tmax=12 if xlane == 3 else 16)
     assert rep.generations == rgens
     assert (out == ref).all()
-    grp = InProcessGroup(LifeConfig(32 * 79, 700, decomp="1x3", tmax=8, epoch=16, poll_gens=32), 3, engine="hip")
+    grp = InProcessGroup(LifeConfig(32 * 79, 700, decomp="1x3", tmax=8, epoch=16, poll_gens=32, tune=tune), 3,
+                         engine="hip")
     grp.load(grid)
     reps = grp.run()
     assert {r.generations for r in reps} == {rgens}
     assert (grp.gather() == ref).all()
 
 
-def test_grouped_schedule_is_the_default(gpu):
-    sim = Simulation(LifeConfig(4096, 2048), engine="hip")
+def test_grouped_schedule_is_the_default(gpu, tune):
+    sim = Simulation(LifeConfig(4096, 2048, tune=tune), engine="hip")
     assert "group=8" in sim.describe()["backend"]
 
 
 @pytest.mark.parametrize("W,H", [(1, 1), (5, 3), (100, 70), (1023, 65), (1025, 200), (3000, 129), (32, 40),
                                  (2048, 333), (3072, 97), (8192, 130)])
 @pytest.mark.parametrize("lds_rows", [32, 64])
-def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H, lds_rows):
+def test_u8_lds_single_step_kernel_vs_torch(gpu, tune, W, H, lds_rows):
     """The LDS-tiled single-step byte kernel (GOL_U8_KERNEL=lds, T = 1); widths
     that are multiples of 32 run the torus-wrap loads (no halo columns, no
     fills: one launch per generation)."""
-    monkeypatch.setenv("GOL_U8_KERNEL", "lds")
-    monkeypatch.setenv("GOL_LDS_ROWS", str(lds_rows))
-    monkeypatch.setenv("GOL_LDS_T", "1")
+    tune["u8_kernel"] = "lds"
+    tune["lds_rows"] = str(lds_rows)
+    tune["lds_t"] = "1"
     g = random_grid(W, H, W ^ H)
     want = life_step_torch(g, 9, device="cuda")
     assert (life_step(g, 9, engine="hip", layout="u8") == want).all()
-    sim = Simulation(LifeConfig(W, H, layout="u8"), engine="hip")
+    sim = Simulation(LifeConfig(W, H, layout="u8", tune=tune), engine="hip")
     assert "lds" in sim.describe()["backend"] and sim.describe()["tmax"] == 1
 
 
@@ -427,7 +431,7 @@ def test_u8_lds_single_step_kernel_vs_torch(gpu, monkeypatch, W, H, lds_rows):
                                  (2048, 333), (3072, 97), (8192, 130), (992, 56), (1984, 113)])
 @pytest.mark.parametrize("lds_T,pack", [(2, 0), (4, 0), (8, 0), (8, 1), (16, 1), (32, 1), (32, 2),
                                          (8, 3), (32, 3)])
-def test_u8_lds_multi_generation_kernel_vs_torch(gpu, monkeypatch, W, H, lds_T, pack):
+def test_u8_lds_multi_generation_kernel_vs_torch(gpu, tune, W, H, lds_T, pack):
     """The LDS-tiled byte kernel with T generations per launch: on the bytes
     (992-cell tiles with a 16-byte halo chunk per side) or packed to bit words
     in LDS (1984-cell tiles with a halo word per side); torus-wrap tiles
@@ -435,35 +439,36 @@ def test_u8_lds_multi_generation_kernel_vs_torch(gpu, monkeypatch, W, H, lds_T, 
     at the end).  Packed tiles run 16-wave workgroups on these small grids;
     pack == 2: with the XCD-aware tile order (GOL_LDS_XCD=1), pack == 3:
     8-wave workgroups (the large-grid choice)."""
-    monkeypatch.setenv("GOL_U8_KERNEL", "lds")
-    monkeypatch.setenv("GOL_LDS_T", str(lds_T))
-    monkeypatch.setenv("GOL_LDS_PACK", str(min(pack, 1)))
-    monkeypatch.setenv("GOL_LDS_XCD", str(int(pack == 2)))
-    monkeypatch.setenv("GOL_LDS_WAVES", "8" if pack == 3 else "0")
+    tune["u8_kernel"] = "lds"
+    tune["lds_t"] = str(lds_T)
+    tune["lds_pack"] = str(min(pack, 1))
+    tune["lds_xcd"] = str(int(pack == 2))
+    tune["lds_waves"] = "8" if pack == 3 else "0"
     g = random_grid(W, H, W * 3 + H + lds_T)
     want = life_step_torch(g, 45, device="cuda")
     assert (life_step(g, 45, engine="hip", layout="u8") == want).all()
-    sim = Simulation(LifeConfig(W, H, layout="u8"), engine="hip")
+    sim = Simulation(LifeConfig(W, H, layout="u8", tune=tune), engine="hip")
     assert f"lds-tiled T={lds_T}" in sim.describe()["backend"] and sim.describe()["tmax"] == lds_T
 
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("2x1", 2), ("2x2", 4)])
-def test_u8_lds_kernel_multi_subdomain(gpu, monkeypatch, spec, P):
+def test_u8_lds_kernel_multi_subdomain(gpu, tune, spec, P):
     """LDS kernel with row exchanges (column wrap on 1xN strips) and column
     exchanges (halo columns), several subdomains on one GPU."""
-    monkeypatch.setenv("GOL_U8_KERNEL", "lds")
+    tune["u8_kernel"] = "lds"
     W, H = 32 * 40, 210
     g = random_grid(W, H, 8)
     want = life_step_torch(g, 40, device="cuda")
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=40, layout="u8", decomp=spec), P, engine="hip", devices=[0])
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=40, layout="u8", decomp=spec, tune=tune), P, engine="hip",
+                         devices=[0])
     grp.load(g)
     grp.advance(40)
     assert (grp.gather() == want).all()
 
 
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
-def test_u8_lds_termination(gpu, monkeypatch, W, H, seed, density):
-    monkeypatch.setenv("GOL_U8_KERNEL", "lds")
+def test_u8_lds_termination(gpu, tune, W, H, seed, density):
+    tune["u8_kernel"] = "lds"
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
     out, rep = simulate(g, 1000, engine="hip", layout="u8")
@@ -475,11 +480,11 @@ def test_u8_lds_termination(gpu, monkeypatch, W, H, seed, density):
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("tmax", [4, 8, 16])
 @pytest.mark.parametrize("W,H", [(4000 - 4000 % 32, 1500), (2048, 333), (96, 100)])
-def test_split_schedule_vs_torch(gpu, monkeypatch, layout, tmax, W, H):
+def test_split_schedule_vs_torch(gpu, tune, layout, tmax, W, H):
     """Split schedule (trapezoid per segment + inverted triangle per boundary,
     boundary states through memory) forced on, many short segments."""
-    monkeypatch.setenv("GOL_SPLIT", "1")
-    monkeypatch.setenv("GOL_MIN_SEG_ROWS", "1")
+    tune["split"] = "1"
+    tune["min_seg_rows"] = "1"
     g = random_grid(W, H, 3 * tmax + W)
     gens = 3 * tmax + 2
     want = life_step_torch(g, gens, device="cuda")
@@ -489,9 +494,9 @@ def test_split_schedule_vs_torch(gpu, monkeypatch, layout, tmax, W, H):
 
 @experimental
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
-def test_split_schedule_termination(gpu, monkeypatch, W, H, seed, density):
-    monkeypatch.setenv("GOL_SPLIT", "1")
-    monkeypatch.setenv("GOL_MIN_SEG_ROWS", "1")
+def test_split_schedule_termination(gpu, tune, W, H, seed, density):
+    tune["split"] = "1"
+    tune["min_seg_rows"] = "1"
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
     for tmax in (4, 8):
@@ -501,10 +506,10 @@ def test_split_schedule_termination(gpu, monkeypatch, W, H, seed, density):
 
 
 @experimental
-def test_split_schedule_tall_grid_flags(gpu, monkeypatch):
+def test_split_schedule_tall_grid_flags(gpu, tune):
     """Many boundaries per launch; the changed flags of both phases must OR
     to the exact per-generation result (compare a run that stops early)."""
-    monkeypatch.setenv("GOL_SPLIT", "1")
+    tune["split"] = "1"
     g = np.zeros((4096, 512), dtype=np.uint8)
     g[2000:2002, 100:102] = 1  # a block (still life)
     W, H, seed, density = CONVERGING[5]
@@ -516,7 +521,7 @@ def test_split_schedule_tall_grid_flags(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_graph_replay_matches_plain_launches(gpu, layout):
+def test_graph_replay_matches_plain_launches(gpu, tune, layout):
     """Full epochs replayed from captured HIP graphs (device-side generation
     offset for the flags) == plain launches, incl. exact termination."""
     for W, H, seed, density in CONVERGING:
@@ -525,7 +530,7 @@ def test_graph_replay_matches_plain_launches(gpu, layout):
         outs = {}
         for mode in ("on", "off"):
             lay = layout if (layout == "u8" or W % 32 == 0) else "u8"
-            sim = Simulation(LifeConfig(W, H, layout=lay, tmax=4, epoch=8, poll_gens=16, graphs=mode),
+            sim = Simulation(LifeConfig(W, H, layout=lay, tmax=4, epoch=8, poll_gens=16, graphs=mode, tune=tune),
                              engine="hip")
             sim.load(g)
             rep = sim.run()
@@ -534,7 +539,7 @@ def test_graph_replay_matches_plain_launches(gpu, layout):
             outs[mode] = sim.tile()
         assert (outs["on"] == ref).all() and (outs["off"] == ref).all()
     g = random_grid(1000 - 1000 % 32, 300, 5)
-    a = Simulation(LifeConfig(992, 300, gen_limit=500, epoch=64, graphs="on"), engine="hip")
+    a = Simulation(LifeConfig(992, 300, gen_limit=500, epoch=64, graphs="on", tune=tune), engine="hip")
     a.load(g)
     r = a.run()
     assert r.graph_launches >= 7 and a.describe()["graphs"]
@@ -575,12 +580,12 @@ def test_termination_gpu(gpu, W, H, seed, density):
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("2x2", 4), ("2x4", 8), ("3x3", 9)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("overlap", ["off", "on", "edges"])
-def test_multi_subdomain_one_gpu(gpu, spec, P, layout, overlap):
+def test_multi_subdomain_one_gpu(gpu, tune, spec, P, layout, overlap):
     W, H = 32 * 12, 300
     g = random_grid(W, H, 42)
     want = life_step_numpy(g, 150)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=150, decomp=spec, layout=layout, tmax=16, epoch=16,
-                                    overlap=overlap), P, engine="hip", devices=[0])
+                                    overlap=overlap, tune=tune), P, engine="hip", devices=[0])
     grp.load(g)
     reps = grp.run()
     assert all(r.generations == 150 for r in reps)
@@ -588,19 +593,19 @@ def test_multi_subdomain_one_gpu(gpu, spec, P, layout, overlap):
     assert (grp.gather() == want).all()
 
 
-def test_random_init_on_device_matches_host(gpu):
-    s = Simulation(LifeConfig(4096, 100), engine="hip")
+def test_random_init_on_device_matches_host(gpu, tune):
+    s = Simulation(LifeConfig(4096, 100, tune=tune), engine="hip")
     s.init_random(11, 0.5)
     assert (s.tile() == random_grid(4096, 100, 11, 0.5)).all()
     assert s.alive_count() == int(random_grid(4096, 100, 11, 0.5).sum())
 
 
-def test_text_io_on_device(gpu, tmp_path):
+def test_text_io_on_device(gpu, tune, tmp_path):
     from gol_amd.utils import io
 
     p = tmp_path / "in.txt"
     io.generate(str(p), 300, 200, seed=3)
-    s = Simulation(LifeConfig(300, 200, gen_limit=50), engine="hip")
+    s = Simulation(LifeConfig(300, 200, gen_limit=50, tune=tune), engine="hip")
     s.load_text(str(p))
     s.run()
     out = tmp_path / "out.txt"
@@ -609,13 +614,13 @@ def test_text_io_on_device(gpu, tmp_path):
     assert out.read_text() == io.format_text(ref)
 
 
-def test_rccl_single_rank_self_exchange(gpu):
+def test_rccl_single_rank_self_exchange(gpu, tune):
     """RCCL transport plumbing on one GPU: a 1-rank communicator with
     send/recv to itself and a MAX all-reduce."""
     import torch
 
     C = gpu
-    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0)
+    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0, tune=make_tuning(tune))
     assert tr.size() == 1 and tr.name() == "rccl"
     tr.barrier()
     # The engine's row-phase op order (send N, recv S, send S, recv N) with
@@ -637,23 +642,24 @@ def test_rccl_single_rank_self_exchange(gpu):
 
 @pytest.mark.parametrize("overlap,side", [("off", "1"), ("off", "0"), ("on", "1"), ("edges", "1")])
 @pytest.mark.parametrize("xlane", [0, -1])
-def test_rccl_self_exchange_rehearsal(gpu, monkeypatch, overlap, side, xlane):
+def test_rccl_self_exchange_rehearsal(gpu, tune, overlap, side, xlane):
     """The multi-rank row-strip schedule on one GPU (bench.py --rehearse-rccl):
     row halos through a 1-rank RCCL communicator sending to itself on the
     comm stream, early-boundary dual launch concurrent with the interior,
     termination polls reduced on the side stream through the transport's
     flags communicator (GOL_SIDE_POLL, overlap off), against the fp32 conv
     oracle and the exact Generations."""
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
-    monkeypatch.setenv("GOL_SIDE_POLL", side)
+    tune["xlane"] = str(xlane)
+    tune["side_poll"] = side
     C = gpu
     W, H = 32 * 96, 1200
     g = random_grid(W, H, 31)
     gens = 300
     want = life_step_torch(g, gens, device="cuda")
-    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0)
+    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0, tune=make_tuning(tune))
     sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=12 if xlane else 16, epoch=96, overlap=overlap,
-                                self_exchange=True), transport=tr, backend=C.hip_backend(0))
+                                self_exchange=True, tune=tune),
+                     transport=tr, backend=C.hip_backend(0, tune=make_tuning(tune)))
     sim.load(g)
     rep = sim.advance(gens)
     assert rep.exchanges >= gens // 96 and rep.overlapped == (overlap != "off")
@@ -661,8 +667,9 @@ def test_rccl_self_exchange_rehearsal(gpu, monkeypatch, overlap, side, xlane):
     for cw, ch, seed, density in [c for c in CONVERGING if c[0] % 32 == 0]:
         grid = random_grid(cw, ch, seed, density)
         ref, rgens, _ = reference_run(grid)
-        s2 = Simulation(LifeConfig(cw, ch, tmax=4, epoch=8, poll_gens=16, overlap=overlap, self_exchange=True),
-                        transport=tr, backend=C.hip_backend(0))
+        s2 = Simulation(LifeConfig(cw, ch, tmax=4, epoch=8, poll_gens=16, overlap=overlap, self_exchange=True,
+                                   tune=tune),
+                        transport=tr, backend=C.hip_backend(0, tune=make_tuning(tune)))
         s2.load(grid)
         assert s2.run().generations == rgens
         assert (s2.tile() == ref).all()
@@ -682,22 +689,22 @@ def test_torch_tensor_views_of_engine_buffers(gpu):
 
 
 @pytest.mark.parametrize("W,H,epoch", [(64, 5, 32), (96, 70, 64), (2048, 40, 128), (32, 1, 16)])
-def test_fused_periodic_fill_matches_cpu_buffer(gpu, monkeypatch, W, H, epoch):
+def test_fused_periodic_fill_matches_cpu_buffer(gpu, tune, W, H, epoch):
     """Single-rank halo_exchange is one fused launch (fill_all_bits): the whole
     padded buffer (column halos, halo rows and corners, multi-wrap when Dv > H)
     must equal the CPU backend's two-pass fill.  Halo mode (GOL_WRAP=0): in
     wrap mode the engine fills no column halos."""
     import torch
 
-    monkeypatch.setenv("GOL_WRAP", "0")
-    monkeypatch.setenv("GOL_ROW_RING", "0")  # a row ring has no row halos to fill
+    tune["wrap"] = "0"
+    tune["row_ring"] = "0"  # a row ring has no row halos to fill
 
     from gol_amd.parallel.dist import tensor_view
 
     g = random_grid(W, H, W * 3 + H)
     bufs = []
     for engine in ("hip", "cpu"):
-        sim = Simulation(LifeConfig(W, H, gen_limit=64, layout="bits", epoch=epoch), engine=engine)
+        sim = Simulation(LifeConfig(W, H, gen_limit=64, layout="bits", epoch=epoch, tune=tune), engine=engine)
         sim.load(g)
         eng = sim.native_engine
         eng.halo_exchange()
@@ -712,7 +719,7 @@ def test_fused_periodic_fill_matches_cpu_buffer(gpu, monkeypatch, W, H, epoch):
     assert np.array_equal(a, b)
 
 
-def test_inprocess_ranks_keep_device_affinity(gpu, monkeypatch, tmp_path):
+def test_inprocess_ranks_keep_device_affinity(gpu, tune, tmp_path):
     """Single-process multi-rank run from fresh Python threads with
     GOL_CHECK_DEVICE=1: every backend entry point asserts its device is
     current and that its staging / chain / scratch buffers and the launch
@@ -720,13 +727,13 @@ def test_inprocess_ranks_keep_device_affinity(gpu, monkeypatch, tmp_path):
     launches, halo exchanges and store_cells (gather)."""
     from gol_amd.utils import io
 
-    monkeypatch.setenv("GOL_CHECK_DEVICE", "1")
-    monkeypatch.setenv("GOL_CHAIN", "-1")
+    tune["check_device"] = "1"
+    tune["chain"] = "-1"
     W, H, gens = 32 * 64, 4 * 640, 300
     p = tmp_path / "in.txt"
     io.generate(str(p), W, H, seed=9)
     g = io.read_grid(str(p), W, H)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x4", epoch=96), 4, engine="hip",
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x4", epoch=96, tune=tune), 4, engine="hip",
                          devices=[0, 0, 0, 0])
     grp.parallel(lambda s: s.load_text(str(p)))
     reps = grp.advance(gens)
@@ -735,20 +742,20 @@ def test_inprocess_ranks_keep_device_affinity(gpu, monkeypatch, tmp_path):
 
 
 @pytest.mark.parametrize("W,H", [(32 * 200, 1500), (1999, 1300), (32 * 300, 5000)])
-def test_pipelined_byte_pass_t48_vs_torch(gpu, W, H):
+def test_pipelined_byte_pass_t48_vs_torch(gpu, tune, W, H):
     """T = 48 byte-layout passes as level-pipelined wave pairs (24 + 24
     levels, life_block_u8_w1_dpp_t48.hip) against the fp32 conv oracle."""
     g = random_grid(W, H, W + H)
     gens = 2 * 48 + 11
     want = life_step_torch(g, gens, device="cuda")
-    sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=48), engine="hip")
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=48, tune=tune), engine="hip")
     assert sim.describe()["tmax"] == 48
     sim.load(g)
     sim.advance(gens)
     assert (sim.tile() == want).all()
 
 
-def test_pipelined_byte_pass_t48_termination_and_ranks(gpu):
+def test_pipelined_byte_pass_t48_termination_and_ranks(gpu, tune):
     """The T = 48 pass with lazy termination (exact Generations), and in a
     1x2 multi-subdomain run whose early-boundary strips are dual launches."""
     grid = np.zeros((1600, 512), dtype=np.uint8)
@@ -762,7 +769,7 @@ def test_pipelined_byte_pass_t48_termination_and_ranks(gpu):
     g = random_grid(W, H, 3)
     want = life_step_torch(g, gens, device="cuda")
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x2", layout="u8", tmax=48, epoch=480,
-                                    overlap="on"), 2, engine="hip", devices=[0])
+                                    overlap="on", tune=tune), 2, engine="hip", devices=[0])
     assert grp.sims[0].describe()["tmax"] == 48
     grp.load(g)
     reps = grp.advance(gens)
@@ -772,27 +779,27 @@ def test_pipelined_byte_pass_t48_termination_and_ranks(gpu):
 
 @pytest.mark.parametrize("W,H", [(32768, 1024), (4096, 700), (2048 * 3, 333), (32 * 100, 1000)])
 @pytest.mark.parametrize("xlane,tmax", [(0, 16), (0, 8), (3, 12), (0, 12)])
-def test_linked_launches_vs_torch(gpu, monkeypatch, W, H, xlane, tmax):
+def test_linked_launches_vs_torch(gpu, tune, W, H, xlane, tmax):
     """Linked launches (GOL_LINK=1, LifeBlockParams::link_*): consecutive
     grouped launches of an epoch run on two streams at once and order their
     rows through per-group completion words; against the fp32 conv oracle,
     with several epochs, the drifting adder window and partial epochs."""
-    monkeypatch.setenv("GOL_LINK", "1")
-    monkeypatch.setenv("GOL_ROW_RING", "0")  # ring epochs are single blocks: nothing to link
-    monkeypatch.setenv("GOL_XLANE", str(xlane))
+    tune["link"] = "1"
+    tune["row_ring"] = "0"  # ring epochs are single blocks: nothing to link
+    tune["xlane"] = str(xlane)
     g = random_grid(W, H, W + 3 * H + tmax)
     gens = 10 * tmax + 7
     want = life_step_torch(g, gens, device="cuda")
-    sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax), engine="hip")
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, tmax=tmax, tune=tune), engine="hip")
     sim.load(g)
     rep = sim.advance(gens)
     assert (sim.tile() == want).all()
     assert rep.linked_launches > 0
 
 
-def test_linked_launches_termination_and_subdomains(gpu, monkeypatch):
-    monkeypatch.setenv("GOL_ROW_RING", "0")
-    monkeypatch.setenv("GOL_LINK", "1")
+def test_linked_launches_termination_and_subdomains(gpu, tune):
+    tune["row_ring"] = "0"
+    tune["link"] = "1"
     grid = np.zeros((1024, 2048), dtype=np.uint8)
     W, H, seed, density = CONVERGING[5]
     grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
@@ -803,7 +810,8 @@ def test_linked_launches_termination_and_subdomains(gpu, monkeypatch):
     W, H, gens = 32 * 64, 4 * 300, 400
     g = random_grid(W, H, 12)
     want = life_step_torch(g, gens, device="cuda")
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x4", tmax=16), 4, engine="hip", devices=[0])
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x4", tmax=16, tune=tune), 4, engine="hip",
+                         devices=[0])
     grp.load(g)
     grp.advance(gens)
     assert (grp.gather() == want).all()
@@ -813,10 +821,10 @@ def test_linked_launches_termination_and_subdomains(gpu, monkeypatch):
 
 @pytest.mark.parametrize("W,H,gens,tmax", [(32, 1, 40, 0), (96, 70, 77, 4), (2048, 40, 200, 0), (6400, 700, 131, 8),
                                            (8192, 1024, 1000, 0)])
-def test_u8_via_bits_default_vs_torch(gpu, monkeypatch, W, H, gens, tmax):
-    monkeypatch.delenv("GOL_U8_VIA_BITS", raising=False)
+def test_u8_via_bits_default_vs_torch(gpu, tune, W, H, gens, tmax):
+    tune.pop("u8_via_bits", None)
     g = random_grid(W, H, W + H + gens)
-    sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=tmax), engine="hip")
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, layout="u8", tmax=tmax, tune=tune), engine="hip")
     d = sim.describe()
     assert d["u8_compute"] == "bits" and d["layout"] == "u8"
     sim.load(g)
@@ -824,11 +832,11 @@ def test_u8_via_bits_default_vs_torch(gpu, monkeypatch, W, H, gens, tmax):
     assert (sim.tile() == life_step_torch(g, gens, device="cuda")).all()
 
 
-def test_u8_via_bits_ragged_width_falls_back(gpu, monkeypatch):
-    monkeypatch.delenv("GOL_U8_VIA_BITS", raising=False)
+def test_u8_via_bits_ragged_width_falls_back(gpu, tune):
+    tune.pop("u8_via_bits", None)
     W, H = 1000, 64
     g = random_grid(W, H, 3)
-    sim = Simulation(LifeConfig(W, H, gen_limit=50, layout="u8"), engine="hip")
+    sim = Simulation(LifeConfig(W, H, gen_limit=50, layout="u8", tune=tune), engine="hip")
     assert sim.describe()["u8_compute"] == "bytes"
     sim.load(g)
     sim.advance(50)
@@ -837,11 +845,12 @@ def test_u8_via_bits_ragged_width_falls_back(gpu, monkeypatch):
 
 @pytest.mark.parametrize("W,H,seed,density", [(32, 16, 1, 0.2), (64, 20, 1, 0.2), (128, 12, 11, 0.2)] +
                          [c for c in CONVERGING if c[0] % 32 == 0])
-def test_u8_via_bits_termination(gpu, W, H, seed, density):
+def test_u8_via_bits_termination(gpu, tune, W, H, seed, density):
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
     for tmax, epoch in [(0, 0), (4, 7), (1, 1)]:
-        sim = Simulation(LifeConfig(W, H, layout="u8", u8_compute="bits", tmax=tmax, epoch=epoch), engine="hip")
+        sim = Simulation(LifeConfig(W, H, layout="u8", u8_compute="bits", tmax=tmax, epoch=epoch, tune=tune),
+                         engine="hip")
         sim.load(g)
         rep = sim.run()
         assert rep.generations == rgens, (tmax, epoch)
@@ -849,26 +858,26 @@ def test_u8_via_bits_termination(gpu, W, H, seed, density):
 
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("2x2", 4), ("1x4", 4)])
-def test_u8_via_bits_subdomains_one_gpu(gpu, spec, P):
+def test_u8_via_bits_subdomains_one_gpu(gpu, tune, spec, P):
     W, H = 4096, 512
     g = random_grid(W, H, 41)
     want = life_step_torch(g, 300, device="cuda")
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=300, decomp=spec, layout="u8", u8_compute="bits",
-                                    check_similarity=False), P, engine="hip")
+                                    check_similarity=False, tune=tune), P, engine="hip")
     grp.load(g)
     grp.parallel(lambda s: s.advance(300))
     assert all(s.native_engine.via_bits for s in grp.sims)
     assert (grp.gather() == want).all()
 
 
-def test_u8_via_bits_graphs_and_chunked_runs(gpu):
+def test_u8_via_bits_graphs_and_chunked_runs(gpu, tune):
     """Captured epochs alternate over the bit-word pair (graphs keyed by its
     parity); each run packs and unpacks once, so chunked runs and read-outs in
     between stay exact."""
     W, H = 4096, 1024
     g = random_grid(W, H, 12)
     sim = Simulation(LifeConfig(W, H, gen_limit=2000, layout="u8", u8_compute="bits", graphs="on",
-                                check_similarity=False), engine="hip")
+                                check_similarity=False, tune=tune), engine="hip")
     assert sim.native_engine.graphs()
     sim.load(g)
     want = g
@@ -881,16 +890,16 @@ def test_u8_via_bits_graphs_and_chunked_runs(gpu):
     assert graphs > 0
 
 
-def test_u8_via_bits_graphs_survive_drift_rotation(gpu, monkeypatch):
+def test_u8_via_bits_graphs_survive_drift_rotation(gpu, tune):
     """A drifting (adder-window) kernel leaves the byte tile drifted; every
     read-out rotates the drift out, which flips the byte buffer pair and so
     moves the bit scratch.  Equal-length chunks must not replay a graph
     captured against the other buffer (graphs are keyed by both parities)."""
-    monkeypatch.setenv("GOL_XLANE", "3")  # kXlaneAdd: the drifting adder window
+    tune["xlane"] = "3"  # kXlaneAdd: the drifting adder window
     W, H = 4096, 1024
     g = random_grid(W, H, 21)
     sim = Simulation(LifeConfig(W, H, gen_limit=4000, layout="u8", u8_compute="bits", graphs="on",
-                                check_similarity=False), engine="hip")
+                                check_similarity=False, tune=tune), engine="hip")
     eng = sim.native_engine
     assert eng.graphs() and eng.drifting
     sim.load(g)
@@ -908,19 +917,20 @@ def test_u8_via_bits_graphs_survive_drift_rotation(gpu, monkeypatch):
 
 # ---- resident epochs (life_resident_impl.hpp) -------------------------------
 
-def _resident_sim(monkeypatch, W, H, k=8, D=0, rccl_self=False, **kw):
+def _resident_sim(tune, W, H, k=8, D=0, rccl_self=False, **kw):
     import gc
 
     from gol_amd import make_backend, native
     gc.collect()  # a stale backend on the device would turn resident epochs off
-    monkeypatch.setenv("GOL_RESIDENT", "1")
-    monkeypatch.setenv("GOL_RES_K", str(k))
+    tune["resident"] = "1"
+    tune["res_k"] = str(k)
     if D:
-        monkeypatch.setenv("GOL_RES_D", str(D))
-    cfg = LifeConfig(W, H, self_exchange=rccl_self, **kw)
+        tune["res_d"] = str(D)
+    cfg = LifeConfig(W, H, self_exchange=rccl_self, **kw, tune=tune)
     if rccl_self:  # the multi-rank epoch schedule against a 1-rank RCCL communicator
         C = native()
-        sim = Simulation(cfg, transport=C.rccl_transport(C.rccl_unique_id(), 0, 1, 0), backend=make_backend("hip", 0))
+        sim = Simulation(cfg, transport=C.rccl_transport(C.rccl_unique_id(), 0, 1, 0, tune=make_tuning(tune)),
+                         backend=make_backend("hip", 0, tune=tune))
     else:
         sim = Simulation(cfg, engine="hip")
     assert sim.native_engine.resident, "resident epochs did not engage"
@@ -930,25 +940,25 @@ def _resident_sim(monkeypatch, W, H, k=8, D=0, rccl_self=False, **kw):
 @experimental
 @pytest.mark.parametrize("W,H,k,D", [(4096, 1024, 8, 0), (32 * 200, 700, 16, 48), (2048, 333, 4, 64),
                                      (32768, 512, 8, 128), (96, 70, 8, 40)])
-def test_resident_epochs_vs_torch(gpu, monkeypatch, W, H, k, D):
+def test_resident_epochs_vs_torch(gpu, tune, W, H, k, D):
     """Whole epochs in one launch with the tile in registers: bands, strips,
     halo refreshes every k generations and the drifting frame, exact against
     the fp32 oracle over several epochs (and a partial one)."""
     g = random_grid(W, H, W + H + k)
-    sim = _resident_sim(monkeypatch, W, H, k=k, D=D, gen_limit=400, check_similarity=False)
+    sim = _resident_sim(tune, W, H, k=k, D=D, gen_limit=400, check_similarity=False)
     sim.load(g)
     sim.advance(301)
     assert (sim.tile() == life_step_torch(g, 301, device="cuda")).all()
 
 
 @experimental
-def test_resident_chunked_runs_and_rehearsal(gpu, monkeypatch):
+def test_resident_chunked_runs_and_rehearsal(gpu, tune):
     """Chunked runs (partial epochs at every chunk end) and the multi-rank
     epoch schedule against a self-exchanging transport (deep halo rows)."""
     W, H = 8192, 1536
     g = random_grid(W, H, 5)
     for self_exchange in (False, True):
-        sim = _resident_sim(monkeypatch, W, H, gen_limit=2000, check_similarity=False, rccl_self=self_exchange)
+        sim = _resident_sim(tune, W, H, gen_limit=2000, check_similarity=False, rccl_self=self_exchange)
         sim.load(g)
         want = g
         for n in (300, 517, 96):
@@ -960,13 +970,13 @@ def test_resident_chunked_runs_and_rehearsal(gpu, monkeypatch):
 
 @experimental
 @pytest.mark.parametrize("case", [c for c in CONVERGING if c[0] % 32 == 0] + [(256, 512, 77, 0.5)])
-def test_resident_termination_matches_reference(gpu, monkeypatch, case):
+def test_resident_termination_matches_reference(gpu, tune, case):
     """The per-generation change flags of resident launches (one LDS slot per
     generation, flushed every 64) give the reference's Generations count."""
     W, H, seed, density = case
     g = random_grid(W, H, seed, density)
     ref, gens, _ = reference_run(g)
-    sim = _resident_sim(monkeypatch, W, H, D=40, poll_gens=80)
+    sim = _resident_sim(tune, W, H, D=40, poll_gens=80)
     sim.load(g)
     rep = sim.run()
     assert rep.generations == gens
@@ -974,14 +984,14 @@ def test_resident_termination_matches_reference(gpu, monkeypatch, case):
 
 
 @experimental
-def test_resident_termination_large_still_life(gpu, monkeypatch):
+def test_resident_termination_large_still_life(gpu, tune):
     """A soup that dies out inside a long epoch: the first unchanged
     generation lies deep inside one resident launch."""
     W, H = 4096, 2048
     g = np.zeros((H, W), np.uint8)
     g[100:102, 200:202] = 1          # block (still life)
     g[1000, 3000:3003] = 1           # blinker: similarity every 2 generations
-    sim = _resident_sim(monkeypatch, W, H, D=200)
+    sim = _resident_sim(tune, W, H, D=200)
     sim.load(g)
     rep = sim.run()
     ref, gens, _ = reference_run(g)
@@ -990,12 +1000,12 @@ def test_resident_termination_large_still_life(gpu, monkeypatch):
 
 
 @experimental
-def test_resident_u8_via_bits_and_graphs(gpu, monkeypatch):
-    monkeypatch.setenv("GOL_U8_VIA_BITS", "1")
+def test_resident_u8_via_bits_and_graphs(gpu, tune):
+    tune["u8_via_bits"] = "1"
     W, H = 4096, 1024
     g = random_grid(W, H, 9)
     for graphs in ("off", "on"):
-        sim = _resident_sim(monkeypatch, W, H, layout="u8", graphs=graphs, gen_limit=1000, check_similarity=False)
+        sim = _resident_sim(tune, W, H, layout="u8", graphs=graphs, gen_limit=1000, check_similarity=False)
         sim.load(g)
         sim.advance(700)
         assert (sim.tile() == life_step_torch(g, 700, device="cuda")).all(), graphs
@@ -1003,13 +1013,14 @@ def test_resident_u8_via_bits_and_graphs(gpu, monkeypatch):
 
 
 @experimental
-def test_resident_off_when_ranks_share_the_gpu(gpu, monkeypatch):
+def test_resident_off_when_ranks_share_the_gpu(gpu, tune):
     """Four in-process ranks on one device: a resident launch could not get
     every CU, so the engines fall back to the grouped kernels (still exact)."""
-    monkeypatch.setenv("GOL_RESIDENT", "1")
+    tune["resident"] = "1"
     W, H = 4096, 1024
     g = random_grid(W, H, 3)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=300, decomp="1x4", check_similarity=False), 4, engine="hip")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=300, decomp="1x4", check_similarity=False, tune=tune), 4,
+                         engine="hip")
     assert not any(s.native_engine.resident for s in grp.sims)
     grp.load(g)
     grp.parallel(lambda s: s.advance(300))
@@ -1020,13 +1031,13 @@ def test_resident_off_when_ranks_share_the_gpu(gpu, monkeypatch):
 
 @pytest.mark.parametrize("W,H", [(8192, 4096), (32768, 1024), (16384, 2048), (4096, 8192)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_row_ring_vs_torch(gpu, W, H, layout):
+def test_row_ring_vs_torch(gpu, tune, W, H, layout):
     """Single-rank tiles whose row halos are second mappings of their own
     owned rows (three physical pieces mapped [C | A B C | A]; B may be empty):
     no fills, every block over exactly the owned rows.  Chunked runs with
     read-outs (drift rotations) in between, against the fp32 oracle."""
     g = random_grid(W, H, W // 32 + H)
-    sim = Simulation(LifeConfig(W, H, layout=layout, gen_limit=1000), engine="hip")
+    sim = Simulation(LifeConfig(W, H, layout=layout, gen_limit=1000, tune=tune), engine="hip")
     d = sim.describe()
     assert d["row_ring"] is True, d
     sim.load(g)
@@ -1038,17 +1049,17 @@ def test_row_ring_vs_torch(gpu, W, H, layout):
     assert sim.last_report.exchanges > 0
 
 
-def test_row_ring_termination_and_off_switch(gpu, monkeypatch):
+def test_row_ring_termination_and_off_switch(gpu, tune):
     """Exact Generations through the ring: a block split by the wrap row is a
     still life only if the halos alias correctly (reference: 2 generations);
     a lone cell dies (1).  Same with the ring off."""
     for ring in ("1", "0"):
-        monkeypatch.setenv("GOL_ROW_RING", ring)
+        tune["row_ring"] = ring
         for cells, want in (([(4095, 10), (4095, 11), (0, 10), (0, 11)], 2), ([(0, 8191)], 1)):
             grid = np.zeros((4096, 8192), dtype=np.uint8)
             for r, c in cells:
                 grid[r, c] = 1
-            sim = Simulation(LifeConfig(8192, 4096, poll_gens=16), engine="hip")
+            sim = Simulation(LifeConfig(8192, 4096, poll_gens=16, tune=tune), engine="hip")
             assert sim.describe()["row_ring"] is (ring == "1")
             sim.load(grid)
             rep = sim.run()
@@ -1056,10 +1067,10 @@ def test_row_ring_termination_and_off_switch(gpu, monkeypatch):
             assert (sim.tile() == (grid if want == 2 else 0)).all(), (ring, cells)
 
 
-def test_row_ring_graphs(gpu):
+def test_row_ring_graphs(gpu, tune):
     W, H = 8192, 4096
     g = random_grid(W, H, 77)
-    sim = Simulation(LifeConfig(W, H, gen_limit=400, graphs="on", check_similarity=False), engine="hip")
+    sim = Simulation(LifeConfig(W, H, gen_limit=400, graphs="on", check_similarity=False, tune=tune), engine="hip")
     assert sim.describe()["row_ring"] is True and sim.native_engine.graphs()
     sim.load(g)
     sim.advance(200)
@@ -1067,7 +1078,7 @@ def test_row_ring_graphs(gpu):
     assert (sim.tile() == life_step_torch(g, 200, device="cuda")).all()
 
 
-def test_rank_tile_multirank_schedule_links_by_default(gpu):
+def test_rank_tile_multirank_schedule_links_by_default(gpu, tune):
     """The 8-GPU rank tile (32768 x 4096) in the multi-rank schedule (row
     halos through a 1-rank RCCL communicator, epoch trapezoids): the blocks of
     an epoch run linked by default, every exchange and poll joins the two
@@ -1077,8 +1088,9 @@ def test_rank_tile_multirank_schedule_links_by_default(gpu):
     g = random_grid(W, H, 17)
     gens = 600  # past two epochs of 16T = 256 and two termination polls
     want = life_step_torch(g, gens, device="cuda")
-    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0)
-    sim = Simulation(LifeConfig(W, H, gen_limit=gens, self_exchange=True), transport=tr, backend=C.hip_backend(0))
+    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0, tune=make_tuning(tune))
+    sim = Simulation(LifeConfig(W, H, gen_limit=gens, self_exchange=True, tune=tune), transport=tr,
+                     backend=C.hip_backend(0, tune=make_tuning(tune)))
     d = sim.describe()
     assert d["tmax"] == 16 and d["row_ring"] is False
     sim.load(g)
@@ -1087,17 +1099,17 @@ def test_rank_tile_multirank_schedule_links_by_default(gpu):
     assert (sim.tile() == want).all()
 
 
-def test_small_ring_tiles_link_launches_by_default(gpu, monkeypatch):
+def test_small_ring_tiles_link_launches_by_default(gpu, tune):
     """Small single-rank ring tiles (the small-tile T rule, >= 1.5 waves per
     SIMD per launch) run consecutive blocks linked by default
     (KernelChoice::link): exact against the fp32 oracle, bits and u8 (the
     GPU default for bytes: computed on bit words)."""
-    monkeypatch.delenv("GOL_U8_VIA_BITS", raising=False)
+    tune.pop("u8_via_bits", None)
     W = H = 8192
     g = random_grid(W, H, 88)
     want = life_step_torch(g, 200, device="cuda")
     for layout in ("bits", "u8"):
-        sim = Simulation(LifeConfig(W, H, layout=layout, gen_limit=1000), engine="hip")
+        sim = Simulation(LifeConfig(W, H, layout=layout, gen_limit=1000, tune=tune), engine="hip")
         assert sim.describe()["row_ring"] is True and sim.describe()["tmax"] == 8
         sim.load(g)
         rep = sim.advance(200)
@@ -1105,16 +1117,16 @@ def test_small_ring_tiles_link_launches_by_default(gpu, monkeypatch):
         assert (sim.tile() == want).all(), layout
 
 
-def test_linked_ring_late_seam_producers_vs_torch(gpu, monkeypatch):
+def test_linked_ring_late_seam_producers_vs_torch(gpu, tune):
     """Linked launches on a row ring (the round-4 race): with
     GOL_FAULT_DELAY_SPINS the first and last groups of every launch publish
     ~1 ms late, so a group at the other end of the torus that read their rows
     without waiting for them (link_wait before it wrapped the rows) would see
     the previous generation."""
-    monkeypatch.setenv("GOL_LINK", "1")
-    monkeypatch.setenv("GOL_FAULT_DELAY_SPINS", "300")
+    tune["link"] = "1"
+    tune["fault_delay_spins"] = "300"
     W, H = 8192, 8192
-    sim = Simulation(LifeConfig(W, H, tmax=8, gen_limit=10_000), engine="hip")
+    sim = Simulation(LifeConfig(W, H, tmax=8, gen_limit=10_000, tune=tune), engine="hip")
     assert sim.describe()["row_ring"]
     g = random_grid(W, H, 8)
     sim.load(g)
@@ -1124,7 +1136,7 @@ def test_linked_ring_late_seam_producers_vs_torch(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("overlap", ["off", "on"])
-def test_rank_tile_links_only_without_comm_stream_work(gpu, overlap):
+def test_rank_tile_links_only_without_comm_stream_work(gpu, tune, overlap):
     """Linked launches assume the device to themselves (the "two launches
     fit" cap counts only the pair): the engine links blocks of
     the multi-rank schedule only while no transport work can run beside them
@@ -1133,8 +1145,8 @@ def test_rank_tile_links_only_without_comm_stream_work(gpu, overlap):
     early-boundary one - and exact either way."""
     native = gpu
     W, H = 32768, 4096
-    tr = native.rccl_transport(native.rccl_unique_id(), 0, 1, 0)
-    sim = Simulation(LifeConfig(W, H, gen_limit=100_000, overlap=overlap, self_exchange=True, epoch=256),
+    tr = native.rccl_transport(native.rccl_unique_id(), 0, 1, 0, tune=make_tuning(tune))
+    sim = Simulation(LifeConfig(W, H, gen_limit=100_000, overlap=overlap, self_exchange=True, epoch=256, tune=tune),
                      engine="hip", transport=tr)
     g = random_grid(W, H, 77)
     sim.load(g)

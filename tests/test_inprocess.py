@@ -4,6 +4,7 @@ The same tests run on one GPU in test_gpu.py."""
 import pytest
 
 from gol_amd import LifeConfig, random_grid, reference_run
+from gol_amd.models.life import make_tuning
 from gol_amd.parallel import InProcessGroup
 
 from golden import CONVERGING
@@ -13,11 +14,12 @@ DECOMPS = [("1x2", 2), ("2x1", 2), ("1x4", 4), ("2x2", 4), ("1x8", 8), ("2x4", 8
 
 @pytest.mark.parametrize("spec,P", DECOMPS)
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_decompositions_match_serial(native, spec, P, layout):
+def test_decompositions_match_serial(native, tune, spec, P, layout):
     W, H = 160, 96
     g = random_grid(W, H, 1234)
     ref, rgens, _ = reference_run(g, 120)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=120, decomp=spec, layout=layout, tmax=8), P, engine="cpu")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=120, decomp=spec, layout=layout, tmax=8, tune=tune), P,
+                         engine="cpu")
     grp.load(g)
     reps = grp.run()
     assert all(r.generations == rgens for r in reps)
@@ -26,30 +28,31 @@ def test_decompositions_match_serial(native, spec, P, layout):
 
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING[:4])
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("2x2", 4)])
-def test_distributed_termination(native, W, H, seed, density, spec, P):
+def test_distributed_termination(native, tune, W, H, seed, density, spec, P):
     if spec == "2x2" and W < 64:
         pytest.skip("tiles narrower than 32 cells")
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
-    grp = InProcessGroup(LifeConfig(W, H, decomp=spec, layout="u8", epoch=3, poll_gens=2), P, engine="cpu")
+    grp = InProcessGroup(LifeConfig(W, H, decomp=spec, layout="u8", epoch=3, poll_gens=2, tune=tune), P, engine="cpu")
     grp.load(g)
     reps = grp.run()
     assert {r.generations for r in reps} == {rgens}
     assert (grp.gather() == ref).all()
 
 
-def test_uneven_tiles_u8(native):
+def test_uneven_tiles_u8(native, tune):
     W, H = 100, 37  # 100 not a multiple of 32 -> u8 with cell-granular splits
     g = random_grid(W, H, 5)
     ref, rgens, _ = reference_run(g, 64)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=64, decomp="1x3", layout="u8", epoch=12), 3, engine="cpu")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=64, decomp="1x3", layout="u8", epoch=12, tune=tune), 3,
+                         engine="cpu")
     grp.load(g)
     grp.run()
     assert (grp.gather() == ref).all()
 
 
-def test_random_init_decomposition_independent(native):
-    grp = InProcessGroup(LifeConfig(128, 64, decomp="2x2"), 4, engine="cpu")
+def test_random_init_decomposition_independent(native, tune):
+    grp = InProcessGroup(LifeConfig(128, 64, decomp="2x2", tune=tune), 4, engine="cpu")
     grp.init_random(99)
     assert (grp.gather() == random_grid(128, 64, 99)).all()
 
@@ -58,7 +61,7 @@ def test_random_init_decomposition_independent(native):
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("tmax,epoch", [(4, 8), (8, 8), (4, 12), (2, 5)])
 @pytest.mark.parametrize("mode", ["on", "edges"])
-def test_overlapped_exchange_matches_serial(native, spec, P, layout, tmax, epoch, mode):
+def test_overlapped_exchange_matches_serial(native, tune, spec, P, layout, tmax, epoch, mode):
     """Overlapped epochs are bit-identical to the serial reference, including
     a short final epoch (gens not a multiple of the epoch depth):
       on     early boundary rows: the last block of an epoch computes the 2D
@@ -69,7 +72,7 @@ def test_overlapped_exchange_matches_serial(native, spec, P, layout, tmax, epoch
     g = random_grid(W, H, 77 + tmax)
     gens = 3 * epoch + epoch // 2 + 1
     ref, _, _ = reference_run(g, gens)
-    cfg = LifeConfig(W, H, gen_limit=gens, decomp=spec, layout=layout, tmax=tmax, epoch=epoch, overlap=mode)
+    cfg = LifeConfig(W, H, gen_limit=gens, decomp=spec, layout=layout, tmax=tmax, epoch=epoch, overlap=mode, tune=tune)
     grp = InProcessGroup(cfg, P, engine="cpu")
     grp.load(g)
     reps = grp.run()
@@ -81,11 +84,11 @@ def test_overlapped_exchange_matches_serial(native, spec, P, layout, tmax, epoch
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
 @pytest.mark.parametrize("lagged", [True, False])
 @pytest.mark.parametrize("mode", ["on", "edges"])
-def test_overlapped_termination(native, W, H, seed, density, lagged, mode):
+def test_overlapped_termination(native, tune, W, H, seed, density, lagged, mode):
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
     cfg = LifeConfig(W, H, decomp="1x2", layout="u8", tmax=2, epoch=3, poll_gens=4, overlap=mode,
-                     lagged_poll=lagged)
+                     lagged_poll=lagged, tune=tune)
     grp = InProcessGroup(cfg, 2, engine="cpu")
     grp.load(g)
     reps = grp.run()
@@ -94,7 +97,7 @@ def test_overlapped_termination(native, W, H, seed, density, lagged, mode):
     assert (grp.gather() == ref).all()
 
 
-def test_overlap_modes(native):
+def test_overlap_modes(native, tune):
     """on = early boundary rows on row strips with H > 2D; edges = the
     round-1 edge-strip schedule; auto only moves the transport operations to
     the comm stream; column decompositions do not overlap."""
@@ -102,7 +105,7 @@ def test_overlap_modes(native):
         cfg = dict(decomp="1x2", tmax=4, epoch=16)
         cfg.update(kw)
         H = cfg.pop("H", 512)
-        return InProcessGroup(LifeConfig(64, H, **cfg), 2, engine="cpu").sims[0].native_engine.overlap()
+        return InProcessGroup(LifeConfig(64, H, **cfg, tune=tune), 2, engine="cpu").sims[0].native_engine.overlap()
     assert ov(overlap="on") and ov(overlap="edges")
     assert not ov() and not ov(overlap="off")
     assert not ov(H=40, overlap="on")  # tile rows 20 <= 2D
@@ -110,14 +113,14 @@ def test_overlap_modes(native):
 
 
 @pytest.mark.parametrize("lagged", [True, False])
-def test_early_boundary_across_runs_and_readouts(native, lagged):
+def test_early_boundary_across_runs_and_readouts(native, tune, lagged):
     """Chunked runs (run_until) and read-outs between them: an exchange sent at
     the end of one run is consumed by the next, and a read-out in between
     (tile(), which may rotate a drift out) never sees stale halos."""
     W, H = 128, 160
     g = random_grid(W, H, 5)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=10_000, decomp="1x2", tmax=4, epoch=8, poll_gens=8,
-                                    lagged_poll=lagged), 2, engine="cpu")
+                                    lagged_poll=lagged, tune=tune), 2, engine="cpu")
     grp.load(g)
     want = g
     done = 0
@@ -129,36 +132,36 @@ def test_early_boundary_across_runs_and_readouts(native, lagged):
 
 
 @pytest.mark.parametrize("overlap", ["off", "on"])
-def test_random_transport_delays_do_not_change_results(native, monkeypatch, overlap):
+def test_random_transport_delays_do_not_change_results(native, tune, overlap):
     """Fault injection: random delays before every publish and
     consume shake the message interleaving; results must stay exact."""
-    monkeypatch.setenv("GOL_FAULT_DELAY_US", "300")
+    tune["fault_delay_us"] = "300"
     W, H = 128, 120
     g = random_grid(W, H, 8)
     ref, _, _ = reference_run(g, 40)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=40, decomp="2x3", layout="u8", tmax=2, epoch=6,
-                                    overlap=overlap), 6, engine="cpu")
+                                    overlap=overlap, tune=tune), 6, engine="cpu")
     grp.load(g)
     grp.run()
     assert (grp.gather() == ref).all()
 
 
-def test_garbled_halo_is_detected(native, monkeypatch):
+def test_garbled_halo_is_detected(native, tune):
     """Fault injection: a corrupted halo message must show up as
     a mismatch against the serial reference - the golden comparison catches
     communication faults."""
-    monkeypatch.setenv("GOL_FAULT_GARBLE", "3")
+    tune["fault_garble"] = "3"
     W, H = 96, 96
     g = random_grid(W, H, 21)
     ref, _, _ = reference_run(g, 30)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=30, decomp="1x2", layout="u8", tmax=2, epoch=4,
-                                    overlap="off"), 2, engine="cpu")
+                                    overlap="off", tune=tune), 2, engine="cpu")
     grp.load(g)
     grp.run()
     assert (grp.gather() != ref).any()
 
 
-def test_thread_transport_pair_matching_two_ranks(native):
+def test_thread_transport_pair_matching_two_ranks(native, tune):
     """The row-phase op order of Engine::halo_exchange (engine.cpp) with
     Py = 2, where north and south are the same peer: messages between a pair
     must match in issue order (send N <-> recv S, send S <-> recv N), the
@@ -169,8 +172,8 @@ def test_thread_transport_pair_matching_two_ranks(native):
 
     C = native
     hub = C.ThreadHub(2)
-    bes = [C.cpu_backend(1) for _ in range(2)]
-    trs = [C.thread_transport(hub, r, bes[r]) for r in range(2)]
+    bes = [C.cpu_backend(1, tune=make_tuning(tune)) for _ in range(2)]
+    trs = [C.thread_transport(hub, r, bes[r], tune=make_tuning(tune)) for r in range(2)]
     n = 4096
     rng = np.random.default_rng(0)
     top = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(2)]
@@ -194,7 +197,7 @@ def test_thread_transport_pair_matching_two_ranks(native):
 
 
 @pytest.mark.parametrize("mode", ["auto", "edges"])
-def test_overlap_decision_is_global_on_uneven_tiles(native, mode):
+def test_overlap_decision_is_global_on_uneven_tiles(native, tune, mode):
     """37 rows over 3 ranks = tiles of 12, 12, 13 rows; with D = 6 only the
     13-row tile has H > 2D.  Every rank must take the same schedule (a rank
     that exchanges early while the others reduce flags would deadlock), so
@@ -202,8 +205,8 @@ def test_overlap_decision_is_global_on_uneven_tiles(native, mode):
     W, H = 96, 37
     g = random_grid(W, H, 3)
     ref, rgens, _ = reference_run(g, 50)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=50, decomp="1x3", layout="u8", tmax=2, epoch=6, overlap=mode), 3,
-                         engine="cpu")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=50, decomp="1x3", layout="u8", tmax=2, epoch=6, overlap=mode,
+                                    tune=tune), 3, engine="cpu")
     assert len({s.native_engine.overlap() for s in grp.sims}) == 1
     grp.load(g)
     reps = grp.run()
@@ -213,7 +216,7 @@ def test_overlap_decision_is_global_on_uneven_tiles(native, mode):
 
 @pytest.mark.parametrize("overlap", ["off", "on", "edges"])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_self_exchange_rehearsal(native, overlap, layout):
+def test_self_exchange_rehearsal(native, tune, overlap, layout):
     """One rank rehearsing the multi-rank row-strip schedule (bench.py
     --rehearse-rccl): halos go through the transport to itself, with the
     multi-rank epoch depth and overlap; results equal the serial loop."""
@@ -221,7 +224,7 @@ def test_self_exchange_rehearsal(native, overlap, layout):
     g = random_grid(W, H, 12)
     ref, rgens, _ = reference_run(g, 120)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=120, layout=layout, tmax=4, epoch=16, overlap=overlap,
-                                    self_exchange=True), 1, engine="cpu")
+                                    self_exchange=True, tune=tune), 1, engine="cpu")
     grp.load(g)
     (rep,) = grp.run()
     assert rep.generations == rgens

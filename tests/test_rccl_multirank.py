@@ -33,6 +33,7 @@ def _env():
     env = dict(os.environ)
     env["PYTHONPATH"] = str(REPO) + os.pathsep + env.get("PYTHONPATH", "")
     env["OMP_NUM_THREADS"] = "1"
+    env.pop("GOL_HOST_THREADS", None)  # conftest's CPU-tier setting: the rank processes run with no knobs set
     return env
 
 
@@ -104,7 +105,7 @@ def test_bench_node_rehearsal_8_ranks_full_grid(gpu):
         # A rehearsal is labelled as one (VERDICT r04 Weak 5), and every rank
         # ran on a CU partition of its own with no hand-set knobs.
         assert rec["headline"] is False and rec["config_id"] is None and "rehearsal: 8 ranks on" in rec["metric"]
-        assert cfg["env_knobs"] == {} and cfg["cu_partition"]
+        assert cfg["env_knobs"] == {} and cfg["tuning_changed"] == {} and cfg["cu_partition"]
         assert "cu-partition" in cfg["engine"]
     else:
         assert rec["headline"] is True and rec["config_id"] == 3

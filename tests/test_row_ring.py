@@ -13,20 +13,21 @@ from gol_amd import LifeConfig, Simulation, life_step_numpy, random_grid, refere
 from golden import CONVERGING
 
 
-@pytest.fixture(autouse=True)
-def _ring(monkeypatch):
-    monkeypatch.setenv("GOL_CPU_RING", "1")
+@pytest.fixture
+def tune():
+    """Tuning passed through LifeConfig.tune (gol/tuning.hpp): the CPU backend emulates row rings."""
+    return {"cpu_ring": "1"}
 
 
-def _sim(W, H, **kw):
-    sim = Simulation(LifeConfig(W, H, **kw), engine="cpu")
+def _sim(tune, W, H, **kw):
+    sim = Simulation(LifeConfig(W, H, tune=tune, **kw), engine="cpu")
     return sim
 
 
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("W,H,tmax", [(128, 64, 4), (256, 160, 8), (96, 48, 16), (512, 256, 12)])
-def test_ring_matches_oracle(native, layout, W, H, tmax):
-    sim = _sim(W, H, layout=layout, tmax=tmax, gen_limit=300)
+def test_ring_matches_oracle(native, tune, layout, W, H, tmax):
+    sim = _sim(tune, W, H, layout=layout, tmax=tmax, gen_limit=300)
     assert sim.describe()["row_ring"] is True
     assert sim.describe()["epoch"] == sim.describe()["tmax"]
     g = random_grid(W, H, W + H + tmax)
@@ -41,12 +42,12 @@ def test_ring_matches_oracle(native, layout, W, H, tmax):
 
 
 @pytest.mark.parametrize("drift", ["0", "1"])
-def test_ring_with_drifting_frame_and_u8_compute(native, monkeypatch, drift):
-    monkeypatch.setenv("GOL_CPU_DRIFT", drift)
+def test_ring_with_drifting_frame_and_u8_compute(native, tune, drift):
+    tune["cpu_drift"] = drift
     W, H = 256, 128
     g = random_grid(W, H, 5)
     for layout, u8c in (("bits", "auto"), ("u8", "bits"), ("u8", "bytes")):
-        sim = _sim(W, H, layout=layout, u8_compute=u8c, tmax=8, gen_limit=500)
+        sim = _sim(tune, W, H, layout=layout, u8_compute=u8c, tmax=8, gen_limit=500)
         assert sim.describe()["row_ring"] is True, (layout, u8c)
         sim.load(g)
         sim.advance(77)
@@ -54,19 +55,19 @@ def test_ring_with_drifting_frame_and_u8_compute(native, monkeypatch, drift):
 
 
 @pytest.mark.parametrize("W,H,seed,density", [c for c in CONVERGING if c[1] % 16 == 0])
-def test_ring_termination_is_exact(native, W, H, seed, density):
+def test_ring_termination_is_exact(native, tune, W, H, seed, density):
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
-    sim = _sim(W, H, tmax=4)
+    sim = _sim(tune, W, H, tmax=4)
     sim.load(g)
     rep = sim.run()
     assert rep.generations == rgens
     assert (sim.tile() == ref).all()
 
 
-def test_ring_off_for_geometries_the_pages_do_not_fit(native):
+def test_ring_off_for_geometries_the_pages_do_not_fit(native, tune):
     # 30 rows of 256-byte bit rows: 7680 bytes is not a whole number of pages.
-    sim = _sim(128, 30, tmax=4)
+    sim = _sim(tune, 128, 30, tmax=4)
     assert sim.describe()["row_ring"] is False
     g = random_grid(128, 30, 1)
     sim.load(g)
@@ -74,13 +75,13 @@ def test_ring_off_for_geometries_the_pages_do_not_fit(native):
     assert (sim.tile() == life_step_numpy(g, 20)).all()
 
 
-def test_ring_halo_rows_alias_owned_rows(native):
+def test_ring_halo_rows_alias_owned_rows(native, tune):
     """The mapping itself: the top halo reads the last owned rows and the
     bottom halo the first ones, through the engine's current buffer."""
     import ctypes
 
     W, H = 128, 64
-    sim = _sim(W, H, layout="u8", u8_compute="bytes", tmax=4)
+    sim = _sim(tune, W, H, layout="u8", u8_compute="bytes", tmax=4)
     g = random_grid(W, H, 9)
     sim.load(g)
     eng = sim.native_engine
@@ -94,11 +95,11 @@ def test_ring_halo_rows_alias_owned_rows(native):
     assert not (a[Dv:Dv + H] == 0).all()
 
 
-def test_ring_allocation_failure_falls_back_to_fills(native, monkeypatch, capfd):
+def test_ring_allocation_failure_falls_back_to_fills(native, tune, capfd):
     """A backend that promises a ring but cannot map it (GOL_CPU_RING=fail):
     the engine warns, allocates plain buffers and fills the row halos."""
-    monkeypatch.setenv("GOL_CPU_RING", "fail")
-    sim = _sim(128, 64, tmax=4, gen_limit=100)
+    tune["cpu_ring"] = "fail"
+    sim = _sim(tune, 128, 64, tmax=4, gen_limit=100)
     assert sim.describe()["row_ring"] is False
     assert "row ring unavailable" in capfd.readouterr().err
     g = random_grid(128, 64, 3)

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from gol_amd import LifeConfig, Simulation, life_step_numpy, random_grid, reference_run
+from gol_amd.models.life import make_tuning
 from gol_amd.parallel import InProcessGroup
 
 from golden import CONVERGING
@@ -36,16 +37,16 @@ def test_via_bits_matches_oracle(native, W, H, tmax, epoch):
     assert sim.alive_count() == int(life_step_numpy(g, 77).sum())
 
 
-def test_selection_rules(native, monkeypatch):
+def test_selection_rules(native, tune):
     # CPU default: the byte kernels; a ragged width cannot use bit words.
-    assert Simulation(LifeConfig(64, 8, layout="u8"), engine="cpu").describe()["u8_compute"] == "bytes"
-    assert Simulation(LifeConfig(100, 8, layout="u8", u8_compute="bits"),
+    assert Simulation(LifeConfig(64, 8, layout="u8", tune=tune), engine="cpu").describe()["u8_compute"] == "bytes"
+    assert Simulation(LifeConfig(100, 8, layout="u8", u8_compute="bits", tune=tune),
                       engine="cpu").describe()["u8_compute"] == "bytes"
-    assert Simulation(LifeConfig(64, 8, layout="bits"), engine="cpu").describe()["u8_compute"] is None
-    monkeypatch.setenv("GOL_U8_VIA_BITS", "1")
-    assert Simulation(LifeConfig(64, 8, layout="u8"), engine="cpu").describe()["u8_compute"] == "bits"
+    assert Simulation(LifeConfig(64, 8, layout="bits", tune=tune), engine="cpu").describe()["u8_compute"] is None
+    tune["u8_via_bits"] = "1"
+    assert Simulation(LifeConfig(64, 8, layout="u8", tune=tune), engine="cpu").describe()["u8_compute"] == "bits"
     # An explicit choice wins over the environment.
-    assert Simulation(LifeConfig(64, 8, layout="u8", u8_compute="bytes"),
+    assert Simulation(LifeConfig(64, 8, layout="u8", u8_compute="bytes", tune=tune),
                       engine="cpu").describe()["u8_compute"] == "bytes"
 
 
@@ -80,13 +81,14 @@ def test_via_bits_termination_matches_reference(native, W, H, seed, density):
 
 
 @pytest.mark.parametrize("tmax,epoch", [(16, 0), (8, 24), (3, 7)])
-def test_via_bits_drifting_frame(native, tmax, epoch):
+def test_via_bits_drifting_frame(native, tune, tmax, epoch):
     """A drifting bit kernel leaves the byte grid drifted by the same amount;
     the read-out rotates it out (Engine::normalize on the byte grid)."""
     W, H = 256, 90
     g = random_grid(W, H, 17 + tmax)
     ref, rgens, _ = reference_run(g, 300)
-    sim = Simulation(u8_bits(W, H, gen_limit=300, tmax=tmax, epoch=epoch), backend=native.cpu_backend(2, 1))
+    sim = Simulation(u8_bits(W, H, gen_limit=300, tmax=tmax, epoch=epoch, tune=tune),
+                     backend=native.cpu_backend(2, 1, tune=make_tuning(tune)))
     assert sim.native_engine.drifting
     sim.load(g)
     rep = sim.run()
@@ -112,7 +114,7 @@ def test_via_bits_decompositions(native, spec, P):
 
 
 @pytest.mark.parametrize("spec", ["1x2", "2x1"])
-def test_via_bits_exchanges_bit_rows(native, spec):
+def test_via_bits_exchanges_bit_rows(native, tune, spec):
     """The same run on the byte tiles sends ~8x the halo bytes (4x at least
     after the 256-byte pitch rounding of both)."""
     W, H = 2048, 64
@@ -121,7 +123,7 @@ def test_via_bits_exchanges_bit_rows(native, spec):
     sent = {}
     for mode in ("bits", "bytes"):
         grp = InProcessGroup(LifeConfig(W, H, gen_limit=40, decomp=spec, tmax=4, epoch=8, layout="u8",
-                                        u8_compute=mode, check_similarity=False), 2, engine="cpu")
+                                        u8_compute=mode, check_similarity=False, tune=tune), 2, engine="cpu")
         grp.load(g)
         reps = grp.parallel(lambda s: s.advance(40))
         assert (grp.gather() == want).all()
