@@ -309,7 +309,7 @@ void launch_deep(const LifeBlockParams& p, int64_t out_rows, const LifeTuning& t
 // 2 waves per SIMD, no spills) while the pass reads and writes the byte
 // grid once per 48 generations:
 // two thirds of the HBM traffic per generation of the T = 32 pass, which is
-// HBM-bound at 32768^2 (docs/PERFORMANCE.md "Byte layout").  32 + 32 levels
+// HBM-bound at 32768^2 (docs/HISTORY.md "Byte layout").  32 + 32 levels
 // (T = 64) spill at 2 waves per SIMD (1064 VGPRs; 26 + 26 still 131).  Four
 // pairs per workgroup (108 KB of LDS).  A dual launch (the early-boundary
 // schedule's two strips) runs as two launches.

@@ -864,7 +864,7 @@ class HipBackend final : public Backend {
   // Resident epochs: on when forced (GOL_RESIDENT=1) and the plan fits;
   // auto (-1) also needs the tile to leave the grouped kernel short of four
   // waves per SIMD (the adder window's occupancy), where the resident launch
-  // measured faster (docs/PERFORMANCE.md, "Resident epochs").
+  // measured faster (docs/HISTORY.md, "Resident epochs").
   int resident_epoch(Layout l, int64_t rows, int64_t cols, int D_req, bool multi) const override {
 #ifndef GOL_EXPERIMENTAL
     (void)l, (void)rows, (void)cols, (void)D_req, (void)multi;
