@@ -39,10 +39,65 @@ def from_db(db_path: str) -> None:
               f"{len(ks)} dispatches).\n")
 
 
+def from_trace(path: str) -> None:
+    """rocprofv3 --kernel-trace --output-format csv: per-kernel time of the
+    framework's own dispatches (the fp32 PyTorch oracle of bench.py's verify
+    step is left out), and how busy the device was between the first and the
+    last temporal-block kernel."""
+    rows = list(csv.DictReader(open(path)))
+    ours = [r for r in rows if not r["Kernel_Name"].startswith(("void at::", "at::"))]
+    life = [r for r in ours if "life_" in r["Kernel_Name"]]
+    if not life:
+        return
+    # The timed steps (with the prewarm and warmup before them) are one run of
+    # back-to-back temporal-block dispatches; the verify step and the setup are
+    # separated from it by host work.  Take the longest run with gaps < 20 ms.
+    life.sort(key=lambda r: int(r["Start_Timestamp"]))
+    runs, cur = [], [life[0]]
+    for r in life[1:]:
+        if int(r["Start_Timestamp"]) - int(cur[-1]["End_Timestamp"]) > 20_000_000:
+            runs.append(cur)
+            cur = []
+        cur.append(r)
+    runs.append(cur)
+    best = max(runs, key=len)
+    t0 = int(best[0]["Start_Timestamp"])
+    t1 = max(int(r["End_Timestamp"]) for r in best)
+    win = [r for r in ours if int(r["Start_Timestamp"]) >= t0 and int(r["End_Timestamp"]) <= t1]
+    agg = collections.OrderedDict()
+    for r in sorted(win, key=lambda r: int(r["Start_Timestamp"])):
+        k = short(r["Kernel_Name"])
+        a = agg.setdefault(k, {"n": 0, "ns": 0, "lds": r["LDS_Block_Size"],
+                               "grid": int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))})
+        a["n"] += 1
+        a["ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    tot = sum(a["ns"] for a in agg.values()) or 1
+    print("## Kernel time over the generation loop (rocprofv3 --kernel-trace: the longest run of "
+          "back-to-back temporal-block dispatches, i.e. prewarm + warmup + timed steps)\n")
+    print("| kernel | calls | total ms | avg us | % | LDS B / WG | workgroups |")
+    print("|---|---:|---:|---:|---:|---:|---:|")
+    for k, a in sorted(agg.items(), key=lambda kv: -kv[1]["ns"]):
+        print(f"| `{k}` | {a['n']} | {a['ns'] / 1e6:.3f} | {a['ns'] / a['n'] / 1e3:.2f} | "
+              f"{100.0 * a['ns'] / tot:.2f} | {a['lds']} | {a['grid']} |")
+    busy, end = 0, t0
+    for r in sorted(win, key=lambda r: int(r["Start_Timestamp"])):
+        a_, b_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if b_ > end:
+            busy += b_ - max(a_, end)
+            end = b_
+    print(f"\nWindow {(t1 - t0) / 1e6:.2f} ms, {len(win)} dispatches; some kernel running "
+          f"{100.0 * busy / max(1, t1 - t0):.1f} % of it (linked launches overlap, so summed kernel "
+          f"time can exceed the window).\n")
+
+
 def main(d: str) -> None:
     db = os.path.join(d, "run_results.db")
     if os.path.exists(db):
         from_db(db)
+        return
+    trace = os.path.join(d, "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        from_trace(trace)
         return
     stats = os.path.join(d, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
