@@ -166,3 +166,11 @@ def test_bench_records_tuning(native):
     assert cfg["env_knobs"] == {}
     assert cfg["tuning_changed"] == {"cpu_ring": "1 (set)", "host_threads": "2 (set)"}
     assert cfg["tuning"]["row_ring"] == "1" and rec["verified"] is True
+
+
+def test_tuning_doc_lists_every_key(native):
+    """docs/TUNING.md is generated from the table; a key added without
+    regenerating it fails here."""
+    doc = (REPO / "docs" / "TUNING.md").read_text()
+    for k in native.tuning_keys():
+        assert f"| `{k['key']}` | `{k['env']}` |" in doc, k["key"]
