@@ -13,11 +13,15 @@ const std::vector<TuningKey>& tuning_keys() {
       {"xlane", "GOL_XLANE", "-1", 'i', "tune",
        "cross-lane window of the bit kernels: -1 auto (adder where the frame may drift, else DPP), 0 DPP, "
        "3 adder (1 ds_bpermute, 2 carry chain: experimental)"},
-      {"group", "GOL_GROUP", "8", 'i', "tune", "waves per workgroup of the grouped schedule: 8 or 4; 0 the classic (ungrouped) schedule; -1 the model's choice"},
+      {"group", "GOL_GROUP", "8", 'i', "tune",
+       "waves per workgroup of the grouped schedule: 8 or 4; 0 the classic (ungrouped) schedule; -1 the model's "
+       "choice"},
       {"group_small", "GOL_GROUP_SMALL", "4", 'i', "tune",
        "waves per group of bit-layout blocks with T <= 8 (follows group when only group is set)"},
-      {"target_waves", "GOL_TARGET_WAVES", "0", 'i', "tune", "waves per launch the segment planner aims at (0: its makespan model decides)"},
-      {"min_seg_rows", "GOL_MIN_SEG_ROWS", "16", 'i', "tune", "shortest row segment a wave of the classic schedule is given"},
+      {"target_waves", "GOL_TARGET_WAVES", "0", 'i', "tune",
+       "waves per launch the segment planner aims at (0: its makespan model decides)"},
+      {"min_seg_rows", "GOL_MIN_SEG_ROWS", "16", 'i', "tune",
+       "shortest row segment a wave of the classic schedule is given"},
       {"chain", "GOL_CHAIN", "-1", 'i', "tune",
        "chained groups: -1 timed per launch shape, 0 off, 1 on (2 timing probe: experimental)"},
       {"chain_spin", "GOL_CHAIN_SPIN", "16", 'i', "tune", "log2 of a chained wave's spin budget"},
