@@ -75,6 +75,15 @@ class Backend {
   }
   virtual void* stream_mark(void* /*from*/) { return nullptr; }
   virtual void stream_wait(void* /*on*/, void* /*mark*/) {}
+  // A side stream for a termination poll that does not join the compute
+  // streams: returned after it has been made to wait for everything enqueued
+  // so far on every compute stream (a linked chain's second stream
+  // included), so the change flags of the generations computed so far are
+  // final on it, while a linked chain continues across the poll.  The poll's
+  // reduction, copy and event go on it (copy_d2h_async_on / event_record_on
+  // with a side stream do not join the compute streams).  nullptr: none (the
+  // engine joins and polls on the compute stream).
+  virtual void* poll_side() { return nullptr; }
 
   // Phase timing: timing_mark() records a timestamp on
   // `stream` (nullptr = the compute stream); timing_ms(a, b) is the time

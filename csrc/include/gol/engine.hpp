@@ -321,6 +321,7 @@ class Engine {
   void* bitbuf_[2] = {nullptr, nullptr};  // own bit scratch when the spare byte buffer cannot hold it
   int bpar_ = 0;             // bit_scratch(bpar_) holds the current generation during a run
   bool poll_side_ = false;   // termination polls reduce on the comm stream (Transport::side_reduce)
+  bool polled_side_ = false;  // a poll of this run went to Backend::poll_side()
   int64_t drift_ = 0;
   int64_t graph_drift_[4] = {0, 0, 0, 0};
   // Overlap auto trial.

@@ -220,6 +220,8 @@ class HipBackend final : public Backend {
     if (err_host_) hipHostFree(err_host_);
     for (auto& e : marks_)
       if (e) hipEventDestroy(e);
+    for (auto& e : tail_)
+      if (e) hipEventDestroy(e);
     if (comm_) hipStreamDestroy(comm_);
     for (auto& e : link_.before)
       if (e) hipEventDestroy(e);
@@ -452,7 +454,7 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
   }
   void copy_d2h_async_on(void* d, const void* s, size_t n, void* stream) override {
-    join_streams();
+    if (!stream) join_streams();  // a side stream was ordered by its caller (stream_wait / poll_side)
     GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream ? static_cast<hipStream_t>(stream) : stream_));
   }
@@ -475,7 +477,7 @@ class HipBackend final : public Backend {
   }
   void* event_record() override { return event_record_on(nullptr); }
   void* event_record_on(void* stream) override {
-    join_streams();
+    if (!stream) join_streams();
     GOL_ON_DEVICE();
     hipEvent_t e;
     HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -584,6 +586,21 @@ class HipBackend final : public Backend {
       }
     }
     return comm_;
+  }
+  // The comm stream, after the tails of both compute streams (no join: the
+  // linked chain keeps its state).  Not inside a capture: polls are issued
+  // between captured epochs.
+  void* poll_side() override {
+    hipStream_t side = static_cast<hipStream_t>(comm_stream());
+    GOL_ON_DEVICE();
+    const hipStream_t tails[2] = {stream_, link_.stream[1]};
+    for (int i = 0; i < 2; ++i) {
+      if (!tails[i]) continue;
+      if (!tail_[i]) HIP_CHECK(hipEventCreateWithFlags(&tail_[i], hipEventDisableTiming));
+      HIP_CHECK(hipEventRecord(tail_[i], tails[i]));
+      HIP_CHECK(hipStreamWaitEvent(side, tail_[i], 0));
+    }
+    return side;
   }
   // Marks come from a small ring of reusable timing-free events: a mark is
   // only waited on by the next few operations of an epoch.
@@ -1197,6 +1214,7 @@ class HipBackend final : public Backend {
   uint64_t* pair_trace_[2] = {nullptr, nullptr};
   int pair_T_ = 0;
   std::array<hipEvent_t, 16> marks_{};
+  hipEvent_t tail_[2] = {nullptr, nullptr};  // poll_side(): the compute streams' tails
   size_t mark_next_ = 0;
   void* stage_ = nullptr;
   int64_t stage_bytes_ = 0;

@@ -811,12 +811,18 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   p.to = to;
   const int64_t n = to - from;
   if (n <= 0) return p;
-  be_->join_streams();  // transports enqueue on the compute stream directly
   uint32_t* dev = flags_ + (from + 1 - flags_base_);
-  if (poll_side_) {
-    // Flags of (from, to] are complete at the compute stream's current mark.
-    void* side = be_->comm_stream();
-    be_->stream_wait(side, be_->stream_mark(nullptr));
+  // A side stream that waits for the compute streams' tails without joining
+  // them: side polls (the reduction on the flags communicator), and on one
+  // rank the copy alone (nothing to reduce) - a linked chain then continues
+  // across the poll instead of restarting behind a join (8192^2: four polls
+  // per 1000 generations, each ~23 us of idle GPU on the compute stream).
+  // Phase timing keeps the compute-stream path (it times the reduction there).
+  void* side = nullptr;
+  if (!comm_route_ && !early_ && (poll_side_ || (tr_->size() == 1 && !cfg_.self_exchange && !phase_timing_)))
+    side = be_->poll_side();
+  if (side) {
+    polled_side_ = true;
     void* t = phase_begin(side);
     // The one-rank RCCL rehearsal reduces too, through its 1-rank communicator.
     if (tr_->size() > 1 || cfg_.self_exchange) tr_->allreduce_max_u32(dev, size_t(n), side);
@@ -826,6 +832,7 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
     ++polls_;
     return p;
   }
+  be_->join_streams();  // transports enqueue on the compute stream directly
   // Early-boundary schedule: reduce and copy on the comm stream, off the
   // compute stream's critical path, in issue order with the halo exchanges.
   void* comm = (comm_route_ || early_) ? be_->comm_stream() : nullptr;
@@ -855,7 +862,12 @@ bool Engine::poll_check(Poll& p, int64_t* first_unchanged) {
       // Fine-grained while the wait is short (the last poll of a run waits
       // for the run's last blocks: a coarse sleep there idles the GPU before
       // the next run), coarser later.
-      std::this_thread::sleep_for(std::chrono::microseconds(s < 0.002 ? 2 : s < 0.05 ? 20 : 500));
+      // Spin (yield) for the first 2 ms: a sleep overshoots by the kernel's
+      // timer slack (~50 us), which idled the GPU at every run boundary.
+      if (s < 0.002)
+        std::this_thread::yield();
+      else
+        std::this_thread::sleep_for(std::chrono::microseconds(s < 0.05 ? 20 : 500));
     }
   }
   be_->event_wait(p.ev);
@@ -1008,9 +1020,11 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   }
   if (have_pending) poll_check(pending, &found);
   if (via_bits_) unpack_bits();
-  // A poll issued just before an early stop may still run on the side stream;
-  // the final alive reduction below uses the same communicator.
-  if (poll_side_) be_->synchronize_stream(be_->comm_stream());
+  // A poll issued just before an early stop may still run on the side stream
+  // (the final alive reduction below uses the same communicator, and the
+  // next run may reallocate the flags it reads).
+  if (polled_side_) be_->synchronize_stream(be_->comm_stream());
+  polled_side_ = false;
   be_->synchronize();
   be_->check_device_errors();
   if (auto_open_) {  // an auto-trial epoch span does not continue into the next run

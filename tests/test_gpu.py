@@ -1117,6 +1117,36 @@ def test_small_ring_tiles_link_launches_by_default(gpu, tune):
         assert (sim.tile() == want).all(), layout
 
 
+@pytest.mark.parametrize("seed,density", [(5, 0.5), (77, 0.004), (3, 0.01)])
+def test_linked_chain_continues_across_polls(gpu, tune, seed, density):
+    """Termination polls of a single-rank run copy their flag window on a side
+    stream that waits for both compute streams' tails (Backend::poll_side),
+    so a linked chain is not restarted at every poll: a run that reaches its
+    limit is one chain (every launch but the first linked).  Exact against
+    the same run with linking off (whose termination the serial-loop tests
+    pin) - sparse soups settle or die inside the run - and, at the limit,
+    against the fp32 oracle."""
+    tune.pop("u8_via_bits", None)
+    W = H = 8192
+    g = random_grid(W, H, seed, density)
+    reps, tiles = [], []
+    for link in ("-1", "0"):
+        t = dict(tune, link=link)
+        sim = Simulation(LifeConfig(W, H, gen_limit=600, poll_gens=64, tune=t), engine="hip")
+        assert sim.describe()["tmax"] == 8
+        sim.load(g)
+        reps.append(sim.run())
+        tiles.append(sim.tile())
+    (a, b), (ta, tb) = reps, tiles
+    assert (a.generations, a.stop_reason) == (b.generations, b.stop_reason)
+    assert (ta == tb).all()
+    assert b.linked_launches == 0
+    if a.stop_reason == "limit":
+        assert (ta == life_step_torch(g, 600, device="cuda")).all()
+        # 75 launches of T = 8, 9 polls every 64 generations: one chain.
+        assert a.kernel_launches == 75 and a.linked_launches == 74 and a.polls >= 9, a
+
+
 def test_linked_ring_late_seam_producers_vs_torch(gpu, tune):
     """Linked launches on a row ring (the round-4 race): with
     GOL_FAULT_DELAY_SPINS the first and last groups of every launch publish
