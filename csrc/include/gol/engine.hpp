@@ -96,7 +96,7 @@ struct EngineConfig {
   // (wherever the backend has the kernel), 0 off, 1 on (same as auto).
   int flow = -1;
   // Runtime tuning (gol/tuning.hpp): the engine's own knobs (u8_via_bits,
-  // side_poll, watchdog_s, pitch_pad, overlap_auto) come from here; the
+  // side_poll, poll_copy_side, watchdog_s, pitch_pad, overlap_auto) come from here; the
   // backend's from the Tuning it was constructed with.  Default: the table's
   // defaults under the GOL_* environment overrides.
   Tuning tune = Tuning::from_env();
@@ -322,6 +322,7 @@ class Engine {
   int bpar_ = 0;             // bit_scratch(bpar_) holds the current generation during a run
   bool poll_side_ = false;   // termination polls reduce on the comm stream (Transport::side_reduce)
   bool polled_side_ = false;  // a poll of this run went to Backend::poll_side()
+  bool poll_copy_side_ = true;  // tuning poll_copy_side: single-rank polls on Backend::poll_side()
   int64_t drift_ = 0;
   int64_t graph_drift_[4] = {0, 0, 0, 0};
   // Overlap auto trial.

@@ -271,6 +271,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // Opt-in (tuning side_poll=1): in the one-GPU RCCL rehearsal the cross-stream
   // hop cost ~10 us per poll, more than the 1-rank reduction it hides
   // (profiles/r02/side_poll_ab.jsonl); with 8 ranks the reduction is longer.
+  poll_copy_side_ = cfg_.tune.on("poll_copy_side");
   poll_side_ = tr_->side_reduce() && be_->is_device() && !early_ && !comm_route_ && !use_graphs_ &&
                !auto_overlap_ && cfg_.tune.on("side_poll");
   gen_ = cfg_.start_gen;
@@ -819,7 +820,8 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   // per 1000 generations, each ~23 us of idle GPU on the compute stream).
   // Phase timing keeps the compute-stream path (it times the reduction there).
   void* side = nullptr;
-  if (!comm_route_ && !early_ && (poll_side_ || (tr_->size() == 1 && !cfg_.self_exchange && !phase_timing_)))
+  if (!comm_route_ && !early_ &&
+      (poll_side_ || (tr_->size() == 1 && !cfg_.self_exchange && !phase_timing_ && poll_copy_side_)))
     side = be_->poll_side();
   if (side) {
     polled_side_ = true;
