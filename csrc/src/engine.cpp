@@ -271,7 +271,14 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // Opt-in (tuning side_poll=1): in the one-GPU RCCL rehearsal the cross-stream
   // hop cost ~10 us per poll, more than the 1-rank reduction it hides
   // (profiles/r02/side_poll_ab.jsonl); with 8 ranks the reduction is longer.
-  poll_copy_side_ = cfg_.tune.on("poll_copy_side");
+  // Single-rank poll copies on a side stream (poll_issue): a linked chain
+  // continues across the poll (the rank tile's ring: 2.24 -> 2.17 ms per 1000
+  // generations), but the side stream's waits on both compute streams cost
+  // host API calls, and with blocks of T <= 8 (small tiles, ~13 us per linked
+  // launch) the host's enqueue rate is the bound: 8192^2 ran 5-10 % slower
+  // (profiles/r05/poll_side.jsonl).  Auto: deeper blocks only.
+  const int pcs = cfg_.tune.i("poll_copy_side");
+  poll_copy_side_ = pcs > 0 || (pcs < 0 && tmax_ > 8);
   poll_side_ = tr_->side_reduce() && be_->is_device() && !early_ && !comm_route_ && !use_graphs_ &&
                !auto_overlap_ && cfg_.tune.on("side_poll");
   gen_ = cfg_.start_gen;

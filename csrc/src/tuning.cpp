@@ -42,8 +42,9 @@ const std::vector<TuningKey>& tuning_keys() {
       {"u8_via_bits", "GOL_U8_VIA_BITS", "-1", 'i', "tune",
        "byte layout computes on bit words: -1 auto, 0 bytes, 1 bits (EngineConfig::u8_compute wins when set)"},
       {"side_poll", "GOL_SIDE_POLL", "0", 'i', "tune", "multi-rank polls reduce on the comm stream"},
-      {"poll_copy_side", "GOL_POLL_COPY_SIDE", "1", 'i', "tune",
-       "single-rank polls copy their flags on a side stream (0: join the compute streams and copy there)"},
+      {"poll_copy_side", "GOL_POLL_COPY_SIDE", "-1", 'i', "tune",
+       "single-rank polls copy their flags on a side stream, linked chains continuing across them: -1 where "
+       "blocks are deeper than 8 generations, 1 always, 0 never (join the compute streams, copy there)"},
       {"watchdog_s", "GOL_WATCHDOG_S", "0", 'i', "tune", "poll watchdog in seconds (0: 900; EngineConfig wins)"},
       {"host_threads", "GOL_HOST_THREADS", "0", 'i', "tune", "host thread pool size (0: min(cores, 16))"},
       {"cu_partition", "GOL_CU_PARTITION", "", 's', "tune",

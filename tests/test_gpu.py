@@ -1131,7 +1131,7 @@ def test_linked_chain_continues_across_polls(gpu, tune, seed, density):
     g = random_grid(W, H, seed, density)
     reps, tiles = [], []
     for link in ("-1", "0"):
-        t = dict(tune, link=link)
+        t = dict(tune, link=link, poll_copy_side="1")  # forced: auto keeps T <= 8 tiles on the join path
         sim = Simulation(LifeConfig(W, H, gen_limit=600, poll_gens=64, tune=t), engine="hip")
         assert sim.describe()["tmax"] == 8
         sim.load(g)
