@@ -248,8 +248,7 @@ class HipBackend final : public Backend {
   int run_flow(const FlowArgs& f) override {
     GOL_ON_DEVICE();
     join_streams();
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    const bool capturing = hipStreamIsCapturing(stream_, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+    const bool capturing = capturing_;  // capture_begin / capture_end (no query per launch)
     if (capturing) return Backend::run_flow(f);
     if (check_dev_) {
       check_ptr(f.buf[0], "run_flow buffer 0");
@@ -547,10 +546,12 @@ class HipBackend final : public Backend {
     join_streams();
     GOL_ON_DEVICE();
     HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    capturing_ = true;
   }
   void* capture_end() override {
     GOL_ON_DEVICE();
     hipGraph_t g = nullptr;
+    capturing_ = false;
     HIP_CHECK(hipStreamEndCapture(stream_, &g));
     hipGraphExec_t exec = nullptr;
     HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
@@ -636,8 +637,7 @@ class HipBackend final : public Backend {
       check_ptr(a.in, "run_block input");
       check_ptr(a.out, "run_block output");
     }
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    const bool capturing = hipStreamIsCapturing(stream_, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+    const bool capturing = capturing_;  // capture_begin / capture_end (no query per launch)
     // A launch may join a linked chain only on the compute stream, outside a
     // capture, for one row range of the bit layout; anything else first joins.
     const bool linkable = (link_on_ || (a.link && link_mode_ < 0)) && link_.stream[1] && !a.stream && !capturing &&
@@ -1215,6 +1215,7 @@ class HipBackend final : public Backend {
   int pair_T_ = 0;
   std::array<hipEvent_t, 16> marks_{};
   hipEvent_t tail_[2] = {nullptr, nullptr};  // poll_side(): the compute streams' tails
+  bool capturing_ = false;                    // between capture_begin and capture_end
   size_t mark_next_ = 0;
   void* stage_ = nullptr;
   int64_t stage_bytes_ = 0;
