@@ -822,9 +822,9 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   uint32_t* dev = flags_ + (from + 1 - flags_base_);
   // A side stream that waits for the compute streams' tails without joining
   // them: side polls (the reduction on the flags communicator), and on one
-  // rank the copy alone (nothing to reduce) - a linked chain then continues
-  // across the poll instead of restarting behind a join (8192^2: four polls
-  // per 1000 generations, each ~23 us of idle GPU on the compute stream).
+  // rank the copy alone (nothing to reduce, poll_copy_side_) - a linked chain
+  // then continues across the poll instead of restarting behind a join (a
+  // join, the copy and the restart left the GPU idle ~20 us per poll).
   // Phase timing keeps the compute-stream path (it times the reduction there).
   void* side = nullptr;
   if (!comm_route_ && !early_ &&
