@@ -28,7 +28,7 @@ BIN = REPO / "bin"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("GOL_OFFLOAD_ARCH", "gfx950")
 # GOL_EXPERIMENTAL=1: also compile the variants and schedules that were
-# measured slower than the defaults (docs/PERFORMANCE.md "What was tried"):
+# measured slower than the defaults (docs/HISTORY.md "What was tried"):
 # resident epochs, split / skewed / short-segment / linked / bit-layout
 # pipelined schedules, the ds_bpermute and carry-chain windows, two words per
 # lane, the packed LDS tile's adder window.  The default build leaves them out
