@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(512) linked_spin(unsigned* counters, int b, un
   if (b > 0) {
     if (threadIdx.x == 0) {
       unsigned seen = 0;
-      for (int i = 0; i < (1 << 22); ++i) {
+      for (int i = 0; i < (1 << 15); ++i) {  // bounded: ~30-60 ms
         seen = __hip_atomic_load(counters + b - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         if (seen >= G) break;
         __builtin_amdgcn_s_sleep(2);
@@ -117,8 +117,15 @@ int main(int argc, char** argv) {
     for (int b = 0; b < K; ++b)
       hipLaunchKernelGGL(linked_spin, dim3(G), dim3(512), 0, s[0], counters, b, G, ticks, err_dev);
   };
+  auto say = [&](const char* what) {
+    std::fprintf(stderr, "[ubench_graph_link] %s (error word %u)\n", what, *err);
+    std::fflush(stderr);
+  };
+  say("start");
   timed(serial);
+  say("serial warm-up done");
   timed(enqueue);  // warm up
+  say("two-stream warm-up done");
   std::vector<Run> rs, rl, rg;
   for (int r = 0; r < R; ++r) rs.push_back(timed(serial));
   for (int r = 0; r < R; ++r) rl.push_back(timed(enqueue));
@@ -131,7 +138,9 @@ int main(int argc, char** argv) {
   size_t nodes = 0;
   CK(hipGraphGetNodes(g, nullptr, &nodes));
   CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  say("graph instantiated");
   timed([&]() { CK(hipGraphLaunch(ge, s[0])); });  // warm up
+  say("graph warm-up done");
   for (int r = 0; r < R; ++r) rg.push_back(timed([&]() { CK(hipGraphLaunch(ge, s[0])); }));
 
   auto med = [](std::vector<Run> v, bool host) {
