@@ -45,7 +45,7 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   if (s != L.stream[0]) return false;
   LifeBlockParams q = p0;  // keeps launch_T's folded last strip (q.fold): a folded block publishes
                            // the completion words of all its groups
-  if (plan_group<T, M>(q, out_rows, simds, group_waves_per_simd<T, LIO, M>(), tune.target_waves, IO::XL) <= 0)
+  if (plan_group_memo<T, M>(q, out_rows, simds, group_waves_per_simd<T, LIO, M>(), tune.target_waves, IO::XL) <= 0)
     return false;
   const int64_t blocks = q.fold > 1 ? int64_t(q.ncolw - 1) * q.nseg + ceil_div(int64_t(q.nseg), int64_t(q.fold))
                                     : int64_t(q.ncolw) * q.nseg;
@@ -159,12 +159,12 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       // charged its redundant triangle, T-1 rows, at the triangles' ILP).
       LifeBlockParams g4 = p, g8 = p;
       const double c4 = (group == 4 || group < 0)
-                            ? plan_group<T, 4>(g4, out_rows, simds, group_waves_per_simd<T, IO, 4>(),
-                                               tune.target_waves, IO::XL)
+                            ? plan_group_memo<T, 4>(g4, out_rows, simds, group_waves_per_simd<T, IO, 4>(),
+                                                    tune.target_waves, IO::XL)
                             : -1.0;
       const double c8 = (group == 8 || group < 0)
-                            ? plan_group<T, 8>(g8, out_rows, simds, group_waves_per_simd<T, IO, 8>(),
-                                               tune.target_waves, IO::XL)
+                            ? plan_group_memo<T, 8>(g8, out_rows, simds, group_waves_per_simd<T, IO, 8>(),
+                                                    tune.target_waves, IO::XL)
                             : -1.0;
       double cc = -1.0;
       if (group < 0) {

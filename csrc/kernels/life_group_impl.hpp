@@ -549,6 +549,34 @@ double plan_group(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int 
   return best;
 }
 
+// plan_group behind a one-entry memo per thread and instantiation:
+// consecutive blocks of a tile plan the same launch, and the host path of a
+// block is what bounds the smallest tiles (8192^2: ~11 us of host time per
+// linked launch against ~13 us on the device, profiles/r05/host_probe.txt).
+template <int T, int M>
+double plan_group_memo(LifeBlockParams& p, int64_t out_rows, int simds, int occ, int target_waves, int xl) {
+  struct Memo {
+    int64_t rows = -1;
+    int simds = 0, occ = 0, target = 0, xl = 0, fold = 0, ncolw = 0;
+    double cost = -1.0;
+    int nseg = 0, seg_rows = 0, seg_rem = 0, grp_q = 0;
+  };
+  thread_local Memo m;
+  if (m.rows == out_rows && m.simds == simds && m.occ == occ && m.target == target_waves && m.xl == xl &&
+      m.fold == p.fold && m.ncolw == p.ncolw) {
+    if (m.cost > 0) {
+      p.nseg = m.nseg;
+      p.seg_rows = m.seg_rows;
+      p.seg_rem = m.seg_rem;
+      p.grp_q = m.grp_q;
+    }
+    return m.cost;
+  }
+  const double c = plan_group<T, M>(p, out_rows, simds, occ, target_waves, xl);
+  m = Memo{out_rows, simds, occ, target_waves, xl, p.fold, p.ncolw, c, p.nseg, p.seg_rows, p.seg_rem, p.grp_q};
+  return c;
+}
+
 // Plan of a chained launch (LifeBlockParams::chain_buf): n groups per strip,
 // waves of q or q + 3 rows (q >= 2T, (q - 2T) % 3 == 0; the first x take
 // q + 3) except the strip's last wave, which takes the remaining
