@@ -273,10 +273,9 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // (profiles/r02/side_poll_ab.jsonl); with 8 ranks the reduction is longer.
   // Single-rank poll copies on a side stream (poll_issue): a linked chain
   // continues across the poll (the rank tile's ring: 2.24 -> 2.17 ms per 1000
-  // generations), but the side stream's waits on both compute streams cost
-  // host API calls, and with blocks of T <= 8 (small tiles, ~13 us per linked
-  // launch) the host's enqueue rate is the bound: 8192^2 ran 5-10 % slower
-  // (profiles/r05/poll_side.jsonl).  Auto: deeper blocks only.
+  // generations, 32768^2 -0.5 %), but with blocks of T <= 8 (8192^2, ~13 us
+  // per linked block) it measured 5-10 % slower (profiles/r05/poll_side.jsonl).
+  // Auto: deeper blocks only.
   const int pcs = cfg_.tune.i("poll_copy_side");
   poll_copy_side_ = pcs > 0 || (pcs < 0 && tmax_ > 8);
   poll_side_ = tr_->side_reduce() && be_->is_device() && !early_ && !comm_route_ && !use_graphs_ &&
