@@ -41,7 +41,7 @@ SMALL = ["--engine", "cpu", "--size", 256, "--steps", 3, "--warmup", 1, "--gens-
          "--verify", 40]
 
 
-@pytest.mark.parametrize("gpus", [1, 4])
+@pytest.mark.parametrize("gpus", [1, 4, 8])
 def test_bench_gpus_n_launches_n_ranks_itself(native, gpus):
     r = _bench(["--gpus", gpus, *SMALL])
     assert r.returncode == 0, r.stderr[-3000:]
