@@ -1147,6 +1147,38 @@ def test_linked_chain_continues_across_polls(gpu, tune, seed, density):
         assert a.kernel_launches == 75 and a.linked_launches == 74 and a.polls >= 9, a
 
 
+@pytest.mark.parametrize("part", ["0/2", "1/4", "3/8"])
+def test_cu_partition_single_process(gpu, tune, part):
+    """tuning cu_partition=k/n (ranks sharing a GPU): the backend's streams
+    are CU-masked to the k-th of n slices, launches are planned for the
+    slice's CUs, and chained groups and linked launches stay off (a time-
+    sliced queue could outlast their bounded waits).  Exact against the fp32
+    oracle on a small ring tile that links by default and on the rank tile's
+    multi-rank schedule."""
+    from gol_amd import native
+    tune.pop("u8_via_bits", None)
+    t = dict(tune, cu_partition=part)
+    W = H = 8192
+    g = random_grid(W, H, 13)
+    sim = Simulation(LifeConfig(W, H, gen_limit=1000, tune=t), engine="hip")
+    assert "cu-partition=" + part in sim.backend.name()
+    assert sim.describe()["tuning"]["cu_partition"] == part
+    sim.load(g)
+    rep = sim.advance(160)
+    assert rep.linked_launches == 0
+    assert (sim.tile() == life_step_torch(g, 160, device="cuda")).all()
+    C = native()
+    W2, H2 = 32768, 1024
+    g2 = random_grid(W2, H2, 14)
+    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0, tune=make_tuning(t))
+    sim2 = Simulation(LifeConfig(W2, H2, gen_limit=1000, self_exchange=True, tune=t), transport=tr,
+                      backend=C.hip_backend(0, tune=make_tuning(t)))
+    sim2.load(g2)
+    rep2 = sim2.advance(300)
+    assert rep2.linked_launches == 0 and rep2.exchanges > 0
+    assert (sim2.tile() == life_step_torch(g2, 300, device="cuda")).all()
+
+
 def test_linked_ring_late_seam_producers_vs_torch(gpu, tune):
     """Linked launches on a row ring (the round-4 race): with
     GOL_FAULT_DELAY_SPINS the first and last groups of every launch publish
