@@ -168,7 +168,11 @@ class Engine {
   int64_t generation() const { return gen_; }
   void set_generation(int64_t g) { gen_ = g; }
   Backend* backend() const { return be_; }
-  void* current_buffer() const { return buf_[cur_]; }
+  // The byte (or bit) tile's current buffer, brought up to date first.
+  void* current_buffer() {
+    sync_bytes();
+    return buf_[cur_];
+  }
   // Storage-frame drift (cells, mod W) left by drifting kernels
   // (Backend::drifts): stored column x holds true column x - drift.
   int64_t drift() const { return drift_; }
@@ -241,6 +245,7 @@ class Engine {
   void epoch_via_bits(int64_t d);
   void pack_bits();
   void unpack_bits();
+  void sync_bytes();  // unpack a live bit image into the byte tile (pack_bits in engine.cpp)
   void* bit_scratch(int i) const;
   // Stream carrying this engine's transport operations (comm stream in the
   // early-boundary schedule, else the compute stream), and the two orderings.
@@ -320,6 +325,7 @@ class Engine {
   TileGeom gb_;              // the tile in the bit layout (same rows, halos, words)
   void* bitbuf_[2] = {nullptr, nullptr};  // own bit scratch when the spare byte buffer cannot hold it
   int bpar_ = 0;             // bit_scratch(bpar_) holds the current generation during a run
+  bool bits_live_ = false;   // ... and after it, until the byte tile is read (sync_bytes)
   bool poll_side_ = false;   // termination polls reduce on the comm stream (Transport::side_reduce)
   bool polled_side_ = false;  // a poll of this run went to Backend::poll_side()
   bool poll_copy_side_ = true;  // tuning poll_copy_side: single-rank polls on Backend::poll_side()

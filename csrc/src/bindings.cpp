@@ -327,7 +327,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("via_bits", &Engine::via_bits)
       .def_property_readonly("resident", &Engine::resident)
       .def("normalize", &Engine::normalize, py::call_guard<py::gil_scoped_release>())
-      .def("current_buffer", [](const Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })
+      .def("current_buffer", [](Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })
       .def("load_cells",
            [](Engine& e, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> a) {
              const uint8_t* p = grid_ptr(a, e.rows().size(), e.cols().size());

@@ -153,3 +153,41 @@ def test_via_bits_phase_timing_and_counters(native):
     assert rep.phase_timed and rep.compute_ms > 0
     assert (sim.tile() == life_step_numpy(random_grid(W, H, 2), 200)).all()
     assert np.array_equal(sim.tile(), sim.tile())
+
+
+@pytest.mark.parametrize("drift", [0, 1])
+def test_bit_image_stays_live_across_runs(native, drift):
+    """A run leaves its result in the bit image and unpacks it only when the
+    byte tile is next read (Engine::sync_bytes): back-to-back runs, reads
+    between them (tile, alive count, row bands, raw buffer), a reload and a
+    random init in the middle, all against the numpy oracle; with the CPU
+    backend's drifting frame the unpacked bytes are rotated on read."""
+    W, H = 256, 96
+    g = random_grid(W, H, 21)
+    sim = Simulation(u8_bits(W, H, gen_limit=10_000, tmax=8, epoch=16),
+                     backend=native.cpu_backend(2, drift))
+    sim.load(g)
+    want = g
+    for n in (40, 17, 64):  # three runs with nothing read in between
+        sim.advance(n)
+        want = life_step_numpy(want, n)
+    assert sim.alive_count() == int(want.sum())  # counted on the live bit image
+    assert (sim.tile() == want).all()
+    sim.advance(33)
+    want = life_step_numpy(want, 33)
+    rows = np.asarray(sim.native_engine.store_rows(20, 10, False)).reshape(10, W)
+    assert (rows == want[20:30]).all()
+    sim.advance(9)
+    want = life_step_numpy(want, 9)
+    assert sim.native_engine.current_buffer() != 0  # a raw view syncs the bytes first
+    assert (sim.tile() == want).all()
+    g2 = random_grid(W, H, 22)  # a reload makes the byte tile the state again
+    sim.advance(12)
+    sim.load(g2)
+    sim.advance(25)
+    assert (sim.tile() == life_step_numpy(g2, 25)).all()
+    sim.init_random(5, 0.3)  # so does an init on the device
+    g3 = sim.tile()
+    sim.advance(30)
+    sim.advance(2)
+    assert (sim.tile() == life_step_numpy(g3, 32)).all()
