@@ -48,6 +48,20 @@ class DeviceScope {
   int dev_, prev_ = -1;
 };
 
+// Release paths (destructors, frees) cannot throw, so they ignore their calls'
+// results - but HIP keeps a failed call's error as the thread's last error,
+// and the next launch check (HIP_CHECK(hipGetLastError()) after a kernel
+// launch), in another object and much later, would report it as its own
+// (with Python's garbage collector deciding when a release runs, at a
+// different place on every run).  Release paths end with this: a failure is
+// reported on stderr under the release's name and cleared.  `quiet` clears
+// without a report: third-party setup and teardown (RCCL's), whose own
+// results are checked, may leave errors of internal probes behind.
+inline void clear_release_error(const char* where, bool quiet = false) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess && !quiet) std::fprintf(stderr, "gol: %s: ignored HIP error: %s\n", where, hipGetErrorString(e));
+}
+
 // CU partition of this process on its device (tuning cu_partition = "k/n":
 // the k-th of n equal, disjoint slices of the CUs).  Ranks that share one GPU
 // in a rehearsal (bench.py --share-gpus) each take a slice, so each rank's

@@ -227,6 +227,7 @@ class HipBackend final : public Backend {
       if (e) hipEventDestroy(e);
     if (link_.stream[1]) hipStreamDestroy(link_.stream[1]);
     if (stream_) hipStreamDestroy(stream_);
+    clear_release_error("~HipBackend");
   }
 
   // Linked launches: everything on the second stream precedes what comes
@@ -323,9 +324,10 @@ class HipBackend final : public Backend {
     if (it != rings_.end()) {
       release_ring(it->second);
       rings_.erase(it);
-      return;
+    } else {
+      hipFree(p);
     }
-    hipFree(p);
+    clear_release_error("HipBackend::release");
   }
   // Row ring (Backend::row_ring_halo): three physical allocations A (first
   // Dv owned rows), B (the rest but the last Dv), C (last Dv), mapped as
@@ -429,6 +431,7 @@ class HipBackend final : public Backend {
   void release_host(void* p) override {
     DeviceScope device_scope(dev_);
     if (p) hipHostFree(p);
+    clear_release_error("HipBackend::release_host");
   }
   void memset_async(void* p, int v, size_t bytes) override {
     join_streams();
@@ -490,6 +493,7 @@ class HipBackend final : public Backend {
   void event_destroy(void* ev) override {
     DeviceScope device_scope(dev_);
     hipEventDestroy(static_cast<hipEvent_t>(ev));
+    clear_release_error("HipBackend::event_destroy");
   }
   bool event_query(void* ev) override {
     GOL_ON_DEVICE();
@@ -566,6 +570,7 @@ class HipBackend final : public Backend {
   void graph_destroy(void* g) override {
     DeviceScope device_scope(dev_);
     if (g) hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
+    clear_release_error("HipBackend::graph_destroy");
   }
   void i64_async(int64_t* dev, int64_t v, bool add) override {
     join_streams();

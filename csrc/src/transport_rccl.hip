@@ -29,6 +29,7 @@
     if (r_ != ncclSuccess)                                                                    \
       ::gol::fail(std::string("RCCL error in ") + __FILE__ + ":" + std::to_string(__LINE__) + \
                   " (" #expr "): " + ncclGetErrorString(r_));                                 \
+    ::gol::clear_release_error("RCCL", true); /* RCCL's probes' HIP errors are not ours */    \
   } while (0)
 
 namespace gol {
@@ -107,8 +108,10 @@ class RcclTransport final : public Transport {
     DeviceScope on(dev_);
     if (barrier_buf_) hipFree(barrier_buf_);
     if (barrier_stream_) hipStreamDestroy(barrier_stream_);
+    clear_release_error("~RcclTransport");
     if (flags_comm_) ncclCommDestroy(flags_comm_);
     if (comm_) ncclCommDestroy(comm_);
+    clear_release_error("~RcclTransport (RCCL)", true);
   }
   int rank() const override { return rank_; }
   int size() const override { return size_; }

@@ -1,6 +1,7 @@
 """GPU tier (MI355X): the CDNA4 kernels against the PyTorch fp32 oracle and the
 CPU backend, golden semantics on the device, multi-subdomain runs on one GPU
 (T3) and the RCCL / torch.distributed transport plumbing."""
+import gc
 import numpy as np
 import pytest
 
@@ -1177,6 +1178,10 @@ def test_cu_partition_single_process(gpu, tune, part):
     rep2 = sim2.advance(300)
     assert rep2.linked_launches == 0 and rep2.exchanges > 0
     assert (sim2.tile() == life_step_torch(g2, 300, device="cuda")).all()
+    # Masked streams are HIP queues of their own: release them here, not at
+    # an arbitrary later collection.
+    del sim, sim2, tr
+    gc.collect()
 
 
 def test_linked_ring_late_seam_producers_vs_torch(gpu, tune):
