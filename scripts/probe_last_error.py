@@ -21,19 +21,19 @@ def main():
     print("clean start:", name(hip.hipGetLastError()))
     bad = hip.hipSetDevice(9999)
     p = ctypes.c_void_p()
-    ok = hip.hipMalloc(ctypes.byref(p), 1 << 20)
-    ok2 = hip.hipMemset(p, 0, 1 << 20)
+    ok = hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 20))
+    ok2 = hip.hipMemset(p, 0, ctypes.c_size_t(1 << 20))
     print(f"failed call {name(bad)}, then hipMalloc {ok}, hipMemset {ok2}")
     print("last error after the successes:", name(hip.hipGetLastError()))
     print("and again:", name(hip.hipGetLastError()))
     hip.hipFree(p)
     # hipErrorNotReady: a stream kept busy by a long memset on a big buffer
     big = ctypes.c_void_p()
-    assert hip.hipMalloc(ctypes.byref(big), 1 << 31) == 0
+    assert hip.hipMalloc(ctypes.byref(big), ctypes.c_size_t(1 << 31)) == 0
     s = ctypes.c_void_p()
     assert hip.hipStreamCreate(ctypes.byref(s)) == 0
     for _ in range(8):
-        hip.hipMemsetAsync(big, 1, 1 << 31, s)
+        hip.hipMemsetAsync(big, 1, ctypes.c_size_t(1 << 31), s)
     q = hip.hipStreamQuery(s)
     print("hipStreamQuery on a busy stream:", name(q))
     print("last error after it:", name(hip.hipGetLastError()))
