@@ -37,10 +37,9 @@ constexpr int kSplitMaxRowsPerT = 8;
 // stream, after an event recorded just before the previous launch (so it
 // starts no earlier than that one), and waits for its input rows group by
 // group.
-template <int T, class IO>
+template <int T, class IO, int M = 8>
 bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const LifeTuning& tune, hipStream_t s) {
   using LIO = Sc1IO<IO>;
-  constexpr int M = 8;
   LinkState& L = *tune.link;
   if (s != L.stream[0]) return false;
   LifeBlockParams q = p0;  // keeps launch_T's folded last strip (q.fold): a folded block publishes
@@ -58,9 +57,15 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
     L.prev_valid = false;
     return false;
   }
+  // Both launches fit at once: each one's share of the CUs (its workgroups
+  // over how many of them fit, whatever resource binds) sums to at most 1,
+  // which bounds every resource's use, also when the two launches are
+  // different kernels (a T = 16 block of 8-wave groups, then a T = 8 block of
+  // 4-wave groups).
+  const double share = double(blocks) / double(cap);
   const bool link = L.prev_valid && L.prev_out == q.in && L.prev.ncolw == q.ncolw && L.prev.wrap_w == q.wrap_w &&
                     L.prev.pitch == q.pitch && L.prev.link_ring_rows == q.link_ring_rows &&
-                    L.prev_blocks + blocks <= cap;
+                    L.prev_share + share <= 1.0;
   // Completion words of this launch: the third buffer back, so neither the
   // previous launch's words (read by this one) nor the ones before it (read by
   // the previous launch, which may still run) are overwritten.
@@ -108,6 +113,7 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   L.prev = q;
   L.prev_out = q.out;
   L.prev_blocks = blocks;
+  L.prev_share = share;
   L.prev_valid = true;
   return true;
 }
@@ -143,8 +149,19 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
   if (tune.link) {
     if constexpr (IO::kBits && IO::W == 1 && (T == 8 || T == 12 || T == 16) &&
                   (IO::XL == kXlaneDpp || IO::XL == kXlaneAdd)) {
-      if (tune.group != 0 && tune.split == 0 && !tune.skew && dual == 1 && launch_linked<T, IO>(p, out_rows, simds, tune, s))
-        return;
+      if (tune.group != 0 && tune.split == 0 && !tune.skew && dual == 1) {
+        // Blocks of T <= 8 link 4-wave groups where the unlinked path would
+        // group 4 waves (tune group_small).
+        if constexpr (T <= 8) {
+          if (tune.group_small == 4) {
+            if (launch_linked<T, IO, 4>(p, out_rows, simds, tune, s)) return;
+          } else if (launch_linked<T, IO>(p, out_rows, simds, tune, s)) {
+            return;
+          }
+        } else if (launch_linked<T, IO>(p, out_rows, simds, tune, s)) {
+          return;
+        }
+      }
     }
     link_join(*tune.link);
   }

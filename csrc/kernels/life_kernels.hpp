@@ -192,6 +192,7 @@ struct LinkState {
   bool prev_valid = false;                      // the last launch may be linked to
   const void* prev_out = nullptr;               // its output buffer
   int64_t prev_blocks = 0;                      // its workgroups
+  double prev_share = 0.0;                      // its workgroups / how many of them fit on the CUs
   LifeBlockParams prev{};                       // its plan and completion words
   uint32_t* flags[3] = {nullptr, nullptr, nullptr};  // completion words, rotating per launch
   size_t flag_words = 0;
