@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -57,9 +58,18 @@ class DeviceScope {
 // reported on stderr under the release's name and cleared.  `quiet` clears
 // without a report: third-party setup and teardown (RCCL's), whose own
 // results are checked, may leave errors of internal probes behind.
+// The reported ones are counted (hip_release_errors(), tests/conftest.py
+// prints the count of a GPU test session).
+inline std::atomic<int64_t>& release_error_count() {
+  static std::atomic<int64_t> n{0};
+  return n;
+}
 inline void clear_release_error(const char* where, bool quiet = false) {
   const hipError_t e = hipGetLastError();
-  if (e != hipSuccess && !quiet) std::fprintf(stderr, "gol: %s: ignored HIP error: %s\n", where, hipGetErrorString(e));
+  if (e != hipSuccess && !quiet) {
+    ++release_error_count();
+    std::fprintf(stderr, "gol: %s: ignored HIP error: %s\n", where, hipGetErrorString(e));
+  }
 }
 
 // CU partition of this process on its device (tuning cu_partition = "k/n":

@@ -145,6 +145,8 @@ std::vector<uint8_t> rccl_unique_id();
 bool rccl_available();
 // PCI bus id ("0000:05:00.0") of a HIP device: which physical GPU a rank ran on.
 std::string hip_pci_bus_id(int device);
+// HIP errors the release paths ignored and reported (hip_util.hpp clear_release_error).
+int64_t hip_release_errors();
 std::string hip_uuid(int device);
 
 }  // namespace gol

@@ -408,7 +408,16 @@ class HipBackend final : public Backend {
       acc.location.type = hipMemLocationTypeDevice;
       acc.location.id = dev_;
       acc.flags = hipMemAccessFlagsProtReadWrite;
-      HIP_CHECK(hipMemSetAccess(r.va, r.bytes, &acc, 1));
+      // Mapping by mapping: one call over the whole range (two of whose
+      // handles are mapped twice) once failed with "invalid argument" on a
+      // fresh ring, after other rings had come and gone in the process.
+      for (const auto& m : r.mapped) {
+        const hipError_t e = hipMemSetAccess(m.first, m.second, &acc, 1);
+        if (e != hipSuccess)
+          fail(std::string("row ring: hipMemSetAccess(") + std::to_string(m.second) + " bytes at offset " +
+               std::to_string(static_cast<uint8_t*>(m.first) - b) + " of " + std::to_string(r.bytes) +
+               ", granularity " + std::to_string(gran) + "): " + hipGetErrorString(e));
+      }
       HIP_CHECK(hipMemsetAsync(b + halo, 0, owned, stream_));
       HIP_CHECK(hipStreamSynchronize(stream_));
     } catch (...) {
@@ -1125,12 +1134,13 @@ class HipBackend final : public Backend {
     std::vector<std::pair<void*, size_t>> mapped;
   };
   void release_ring(Ring& r) {
-    for (auto& m : r.mapped) (void)hipMemUnmap(m.first, m.second);
+    for (auto& m : r.mapped)
+      if (hipMemUnmap(m.first, m.second) != hipSuccess) clear_release_error("row ring: hipMemUnmap");
     r.mapped.clear();
-    if (r.va) (void)hipMemAddressFree(r.va, r.bytes);
+    if (r.va && hipMemAddressFree(r.va, r.bytes) != hipSuccess) clear_release_error("row ring: hipMemAddressFree");
     r.va = nullptr;
     for (auto& h : r.h) {
-      if (h) (void)hipMemRelease(h);
+      if (h && hipMemRelease(h) != hipSuccess) clear_release_error("row ring: hipMemRelease");
       h = {};
     }
   }

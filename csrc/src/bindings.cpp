@@ -172,6 +172,7 @@ PYBIND11_MODULE(_gol, m) {
         py::arg("device") = 0, py::arg("tune") = py::none());
   m.def("hip_available", &hip_available);
   m.def("hip_pci_bus_id", &hip_pci_bus_id);
+  m.def("hip_release_errors", &hip_release_errors);
   m.def("hip_uuid", &hip_uuid);
   m.def("experimental_build", &experimental_build);
 

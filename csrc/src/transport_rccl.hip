@@ -184,6 +184,8 @@ std::vector<uint8_t> rccl_unique_id() {
 
 bool rccl_available() { return true; }
 
+int64_t hip_release_errors() { return release_error_count().load(); }
+
 std::string hip_pci_bus_id(int device) {
   char id[64] = {0};
   HIP_CHECK(hipDeviceGetPCIBusId(id, int(sizeof(id)), device));

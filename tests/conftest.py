@@ -35,6 +35,14 @@ def pytest_runtest_setup(item):
             pytest.skip("not an experimental build (GOL_EXPERIMENTAL=1 python -m gol_amd.native_build)")
 
 
+def pytest_terminal_summary(terminalreporter):
+    """GPU sessions: how many HIP errors the native release paths ignored
+    (destructors, frees; reported one by one on the tests' stderr)."""
+    mod = next((m for n, m in sys.modules.items() if n.endswith("._gol") and hasattr(m, "hip_release_errors")), None)
+    if mod is not None and mod.hip_available():
+        terminalreporter.write_line(f"gol: HIP errors ignored by native release paths: {mod.hip_release_errors()}")
+
+
 @pytest.fixture(scope="session")
 def native():
     import gol_amd  # noqa: PLC0415
