@@ -373,6 +373,44 @@ class HipBackend final : public Backend {
     }
     return fr;
   }
+  struct Ring {
+    void* va = nullptr;
+    size_t bytes = 0;
+    hipMemGenericAllocationHandle_t h[3] = {};
+    std::vector<std::pair<void*, size_t>> mapped;
+  };
+  // One attempt at a ring's mappings [C | A B C | A] (alloc_row_ring).
+  uint8_t* map_ring(Ring& r, size_t halo, size_t owned, size_t gran) {
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev_;
+    const size_t sizes[3] = {halo, owned - 2 * halo, halo};
+    for (int i = 0; i < 3; ++i)
+      if (sizes[i]) HIP_CHECK(hipMemCreate(&r.h[i], sizes[i], &prop, 0));
+    HIP_CHECK(hipMemAddressReserve(&r.va, r.bytes, gran, nullptr, 0));
+    auto* b = static_cast<uint8_t*>(r.va);
+    const struct {
+      size_t at;
+      int piece;
+    } maps[5] = {{0, 2}, {halo, 0}, {2 * halo, 1}, {owned, 2}, {owned + halo, 0}};
+    for (const auto& m : maps) {
+      if (!sizes[m.piece]) continue;
+      HIP_CHECK(hipMemMap(b + m.at, sizes[m.piece], 0, r.h[m.piece], 0));
+      r.mapped.push_back({b + m.at, sizes[m.piece]});
+    }
+    hipMemAccessDesc acc{};
+    acc.location.type = hipMemLocationTypeDevice;
+    acc.location.id = dev_;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    const hipError_t e = hipMemSetAccess(r.va, r.bytes, &acc, 1);
+    if (e != hipSuccess)
+      fail(std::string("row ring: hipMemSetAccess(") + std::to_string(r.bytes) + " bytes, granularity " +
+           std::to_string(gran) + "): " + hipGetErrorString(e));
+    HIP_CHECK(hipMemsetAsync(b + halo, 0, owned, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    return b;
+  }
   void* alloc_row_ring(const TileGeom& g) override {
     if (!ring_on_) return nullptr;
     join_streams();
@@ -381,51 +419,28 @@ class HipBackend final : public Backend {
     const size_t gran = ring_granularity();
     GOL_REQUIRE(gran != size_t(-1) && halo % gran == 0 && owned % gran == 0 && owned >= 2 * halo && halo > 0,
                 "row ring: geometry does not fit the mapping granularity (Backend::row_ring_halo)");
+    // HIP's bookkeeping of a handle mapped twice is fragile: setting access
+    // mapping by mapping fails on the first mapping of a doubly mapped handle,
+    // and a whole-range call on a fresh ring failed once after other rings had
+    // come and gone in the process (possibly at an address an earlier ring had used).
+    // So a ring's address range is never given back (release_ring keeps the
+    // reservation; only the memory is freed), and a failed attempt is retried
+    // once on a new range.
     Ring r;
-    r.bytes = owned + 2 * halo;
-    hipMemAllocationProp prop{};
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = dev_;
-    const size_t sizes[3] = {halo, owned - 2 * halo, halo};
-    auto* b = static_cast<uint8_t*>(nullptr);
-    try {
-      for (int i = 0; i < 3; ++i)
-        if (sizes[i]) HIP_CHECK(hipMemCreate(&r.h[i], sizes[i], &prop, 0));
-      HIP_CHECK(hipMemAddressReserve(&r.va, r.bytes, gran, nullptr, 0));
-      b = static_cast<uint8_t*>(r.va);
-      // [C | A B C | A]
-      const struct {
-        size_t at;
-        int piece;
-      } maps[5] = {{0, 2}, {halo, 0}, {2 * halo, 1}, {owned, 2}, {owned + halo, 0}};
-      for (const auto& m : maps) {
-        if (!sizes[m.piece]) continue;
-        HIP_CHECK(hipMemMap(b + m.at, sizes[m.piece], 0, r.h[m.piece], 0));
-        r.mapped.push_back({b + m.at, sizes[m.piece]});
+    uint8_t* b = nullptr;
+    for (int attempt = 0;; ++attempt) {
+      r = Ring{};
+      r.bytes = owned + 2 * halo;
+      try {
+        b = map_ring(r, halo, owned, gran);
+        break;
+      } catch (...) {
+        // A partial ring (out of memory or address space, or the above) gives
+        // back its memory, so the engine's fallback to plain buffers has it.
+        release_ring(r);
+        (void)hipGetLastError();
+        if (attempt > 0) throw;
       }
-      hipMemAccessDesc acc{};
-      acc.location.type = hipMemLocationTypeDevice;
-      acc.location.id = dev_;
-      acc.flags = hipMemAccessFlagsProtReadWrite;
-      // Mapping by mapping: one call over the whole range (two of whose
-      // handles are mapped twice) once failed with "invalid argument" on a
-      // fresh ring, after other rings had come and gone in the process.
-      for (const auto& m : r.mapped) {
-        const hipError_t e = hipMemSetAccess(m.first, m.second, &acc, 1);
-        if (e != hipSuccess)
-          fail(std::string("row ring: hipMemSetAccess(") + std::to_string(m.second) + " bytes at offset " +
-               std::to_string(static_cast<uint8_t*>(m.first) - b) + " of " + std::to_string(r.bytes) +
-               ", granularity " + std::to_string(gran) + "): " + hipGetErrorString(e));
-      }
-      HIP_CHECK(hipMemsetAsync(b + halo, 0, owned, stream_));
-      HIP_CHECK(hipStreamSynchronize(stream_));
-    } catch (...) {
-      // A partial ring (out of memory or address space) gives back what it
-      // took, so the engine's fallback to plain buffers has it.
-      release_ring(r);
-      (void)hipGetLastError();
-      throw;
     }
     if (check_dev_) check_ptr(b + halo, "row ring");
     rings_[r.va] = r;
@@ -1127,18 +1142,11 @@ class HipBackend final : public Backend {
   }
 
  private:
-  struct Ring {
-    void* va = nullptr;
-    size_t bytes = 0;
-    hipMemGenericAllocationHandle_t h[3] = {};
-    std::vector<std::pair<void*, size_t>> mapped;
-  };
   void release_ring(Ring& r) {
     for (auto& m : r.mapped)
       if (hipMemUnmap(m.first, m.second) != hipSuccess) clear_release_error("row ring: hipMemUnmap");
     r.mapped.clear();
-    if (r.va && hipMemAddressFree(r.va, r.bytes) != hipSuccess) clear_release_error("row ring: hipMemAddressFree");
-    r.va = nullptr;
+    r.va = nullptr;  // the reservation is kept (alloc_row_ring): address space only
     for (auto& h : r.h) {
       if (h && hipMemRelease(h) != hipSuccess) clear_release_error("row ring: hipMemRelease");
       h = {};
