@@ -434,12 +434,13 @@ class HipBackend final : public Backend {
       try {
         b = map_ring(r, halo, owned, gran);
         break;
-      } catch (...) {
+      } catch (const std::exception& ex) {
         // A partial ring (out of memory or address space, or the above) gives
         // back its memory, so the engine's fallback to plain buffers has it.
         release_ring(r);
         (void)hipGetLastError();
         if (attempt > 0) throw;
+        std::fprintf(stderr, "gol: row ring: %s; retrying on a new address range\n", ex.what());
       }
     }
     if (check_dev_) check_ptr(b + halo, "row ring");
