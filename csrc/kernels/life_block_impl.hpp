@@ -466,10 +466,27 @@ struct Sc1IO : IO {
 
 // Row reader with a 3-deep register prefetch: the row for step k sits in
 // slot k % 3 and is replaced by the load for step k + 3 when consumed.
+// Rows in flight per wave: sets of 3 (the window's slots), the oldest set
+// consumed first.  The adder window's waves (4 per SIMD, SALU round trips in
+// every level body) hide a deeper prefetch: 32768^2 10.41 -> 10.13 ms with
+// two sets (profiles/r05/prefetch6.jsonl); the DPP window's 2-wave tiles lose
+// with it (the 8-GPU tile's ring +1 %).
+#ifndef GOL_PREFETCH_SETS_ADD
+#define GOL_PREFETCH_SETS_ADD 2
+#endif
+template <class IO>
+constexpr int prefetch_sets() {
+  return IO::XL == kXlaneAdd ? GOL_PREFETCH_SETS_ADD : 1;
+}
+
+// Row reader with a register prefetch of 3 N rows (N = prefetch_sets): the
+// row for step k sits in slot k % 3 of the oldest set and, when consumed, the
+// newer sets move down and the load for step k + 3 N fills the newest.
 template <class IO>
 struct RowReader {
   static constexpr int W = IO::W;
-  typename IO::Raw buf[3];
+  static constexpr int N = prefetch_sets<IO>();
+  typename IO::Raw buf[N][3];
   const uint8_t* base;
   int64_t pitch;
   int kmax;
@@ -477,12 +494,16 @@ struct RowReader {
   bool ok[W];
   __device__ __forceinline__ void init() {
 #pragma unroll
-    for (int s = 0; s < 3; ++s) buf[s] = IO::load_raw(base + int64_t(min(s, kmax)) * pitch, off);
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) buf[n][s] = IO::load_raw(base + int64_t(min(3 * n + s, kmax)) * pitch, off);
   }
   template <int S>
   __device__ __forceinline__ Vec<W> take(int k) {
-    const typename IO::Raw r = buf[S];
-    buf[S] = IO::load_raw(base + int64_t(min(k + 3, kmax)) * pitch, off);
+    const typename IO::Raw r = buf[0][S];
+#pragma unroll
+    for (int n = 0; n + 1 < N; ++n) buf[n][S] = buf[n + 1][S];
+    buf[N - 1][S] = IO::load_raw(base + int64_t(min(k + 3 * N, kmax)) * pitch, off);
     return IO::convert(r, ok);
   }
 };
