@@ -184,6 +184,20 @@ def band_oracle(snap, r0: int, gens: int, device: str):
     return life_step_torch_roll(snap[rows], gens, device=device)[gens:gens + b]
 
 
+def grid_digest(parts) -> str:
+    """sha256 of the verified final cells (0/1 bytes, row-major): the same seed
+    and step count must give the same digest on any schedule or build, so two
+    trees can be compared bit for bit (e.g. before and after a refactor)."""
+    import hashlib  # noqa: PLC0415
+
+    import numpy as np  # noqa: PLC0415
+
+    h = hashlib.sha256()
+    for p in parts:
+        h.update(np.ascontiguousarray(p, dtype=np.uint8).tobytes())
+    return h.hexdigest()
+
+
 def check_ranks(world: int, shared: bool, comm_count: int, infos: list[dict]) -> str | None:
     """What RCCL saw must be what the bench reports (the reference's
     MPI_Comm_size, src/game_mpi.c:159): the communicator holds `world` ranks,
@@ -438,8 +452,10 @@ def main() -> int:
             del want, cone
         del snaps
         verified = ok_torch
+        digest = grid_digest([eng.store_rows(r0, b) for r0 in starts])
         verify = {"generations": int(done), "from_generation": int(g_snap), "stop_reason": rv.stop_reason,
                   "oracle": f"{len(starts)} row bands of {b} read from the device (light cones of {done} rows)",
+                  "final_sha256": digest, "digest_of": "the checked row bands",
                   "vs_torch_fp32_oracle": ok_torch, "vs_u8_layout": None,
                   "seconds": round(time.perf_counter() - t_v, 2)}
     elif a.verify > 0 and S * Hg > VERIFY_MAX_CELLS:
@@ -483,6 +499,7 @@ def main() -> int:
         verified = bool(ok_torch and ok_u8)
         verify = {"generations": int(done), "from_generation": int(g_snap), "stop_reason": rv.stop_reason,
                   "oracle": oracle,
+                  "final_sha256": grid_digest([final]) if rank == 0 else None, "digest_of": "the whole grid",
                   "vs_torch_fp32_oracle": ok_torch, "vs_u8_layout": ok_u8,
                   "seconds": round(time.perf_counter() - t_v, 2)}
         if dist is not None:
@@ -533,10 +550,7 @@ def main() -> int:
                 "polls_per_step": rs[-1].polls if rs else 0,
                 "kernel_launches_per_step": rs[-1].kernel_launches if rs else 0,
                 "linked_launches_per_step": rs[-1].linked_launches if rs else 0,
-                "flow": desc["flow"],
-                "flow_launches_per_step": rs[-1].flow_launches if rs else 0,
-                "flow_blocks_per_step": rs[-1].flow_blocks if rs else 0,
-                "flow_plan": desc["flow_plan"],
+                "row_ring": desc["row_ring"],
                 # Knobs set by hand: GOL_* variables, and every tuning key off
                 # its default with its source (bench.py's own rehearsal
                 # partition aside); the effective values of the tune class.

@@ -110,15 +110,6 @@ class Backend {
   // (BlockArgs::allow_drift): the output's column x holds the cell the input
   // frame had at x - drift.
   virtual int run_block(const BlockArgs& a) = 0;
-  // A run of temporal blocks (FlowArgs) as one launch where the backend has a
-  // persistent dataflow kernel for it (has_flow); returns the total drift.
-  // The default runs the blocks one by one through run_block, with the same
-  // result, so the engine's flow bookkeeping is the same on every backend.
-  virtual int run_flow(const FlowArgs& f);
-  // Whether run_flow of T-generation blocks is one launch for this layout.
-  virtual bool has_flow(Layout /*l*/, int /*T*/) const { return false; }
-  // Description of the last flow launch (kernel plan), or "".
-  virtual std::string flow_desc() const { return ""; }
   // Whether run_block may drift the frame for this layout when allowed
   // (the engine then sizes the left halo for the one-sided light cone).
   virtual bool drifts(Layout) const { return false; }
@@ -155,16 +146,6 @@ class Backend {
   virtual KernelChoice choose_kernel(Layout l, int64_t /*rows*/, int64_t /*cols*/, int tmax_req) const {
     return {tmax_req > 0 ? tmax_req : preferred_tmax(l), drifts(l)};
   }
-  // Resident epochs: the epoch depth D (> 16) at which this backend runs a
-  // whole epoch of a rows x cols whole-width bit tile as ONE launch that keeps
-  // the tile in the register file (BlockArgs::resident, any T <= D), or 0.
-  // D_req > 0: the caller's epoch depth; multi: halos come from other ranks.
-  virtual int resident_epoch(Layout /*l*/, int64_t /*rows*/, int64_t /*cols*/, int /*D_req*/,
-                             bool /*multi*/) const {
-    return 0;
-  }
-  // Allocates what resident launches on tile g need (outside any capture).
-  virtual void reserve_resident(const TileGeom& /*g*/) {}
   // Fewest output rows a run_block of T generations accepts (the pipelined
   // deep byte pass plans whole wave-pair groups); the engine keeps every
   // block at least this tall or uses a smaller T.
@@ -219,12 +200,9 @@ class Backend {
 // testable on the CPU; -1: the tuning's cpu_drift.
 std::unique_ptr<Backend> make_cpu_backend(int threads, int drift = -1, const Tuning& tune = Tuning::from_env());
 // Defined in backend_hip.hip; throws if no device or the kernels are missing,
-// or if `tune` selects a kernel this build does not carry.
+// or if `tune` selects a kernel that does not exist.
 std::unique_ptr<Backend> make_hip_backend(int device, const Tuning& tune = Tuning::from_env());
 bool hip_available();
-// Whether the HIP kernels were built with GOL_EXPERIMENTAL (the measured-
-// slower variants and schedules; docs/PERFORMANCE.md).
-bool experimental_build();
 
 // Counter-based RNG used by init_random (host and device agree bit-for-bit).
 GOL_HD inline uint64_t splitmix64(uint64_t x) {

@@ -89,12 +89,6 @@ struct EngineConfig {
   //   -1 auto: bits on a device backend with the plain or auto schedule
   //      (GOL_U8_VIA_BITS=0|1 overrides), else bytes.
   int u8_compute = -1;
-  // Persistent dataflow launches (Backend::has_flow / run_flow): a run of
-  // equal temporal blocks - a halo epoch, or on a row ring the blocks of a
-  // termination-poll window - as ONE launch whose work items wait for the
-  // items of the block before them instead of a launch boundary.  -1 auto
-  // (wherever the backend has the kernel), 0 off, 1 on (same as auto).
-  int flow = -1;
   // Runtime tuning (gol/tuning.hpp): the engine's own knobs (u8_via_bits,
   // side_poll, poll_copy_side, watchdog_s, pitch_pad, overlap_auto) come from here; the
   // backend's from the Tuning it was constructed with.  Default: the table's
@@ -116,8 +110,6 @@ struct RunResult {
   int64_t graph_launches = 0;    // epochs replayed from a captured HIP graph
   int64_t halo_bytes = 0;        // bytes this rank sent in halo exchanges
   int64_t linked_launches = 0;   // launches that overlapped the previous one (GOL_LINK)
-  int64_t flow_launches = 0;     // persistent dataflow launches (EngineConfig::flow)
-  int64_t flow_blocks = 0;       // temporal blocks they ran
   // Per-phase device time of this run (Engine::set_phase_timing; SURVEY
   // 5.1/5.5): temporal-block kernels, halo exchanges (pack / send / recv /
   // unpack), periodic halo fills, termination-flag reductions (all-reduce +
@@ -180,13 +172,9 @@ class Engine {
   bool drifting() const { return drift_ok_; }
   // Whether byte-layout epochs compute on bit words (EngineConfig::u8_compute).
   bool via_bits() const { return via_bits_; }
-  // Whether every epoch runs as one resident launch (Backend::resident_epoch).
-  bool resident() const { return resident_; }
   // Whether the tile is a row ring (Backend::row_ring_halo): no row fills,
   // one temporal block per epoch over the owned rows.
   bool row_ring() const { return rows_ring_; }
-  // Whether runs of equal blocks go to Backend::run_flow (EngineConfig::flow).
-  bool flow() const { return flow_; }
   // Rotates the drift out of the current buffer (owned rows); every
   // read-out (store_cells) does this first.
   void normalize();
@@ -231,13 +219,6 @@ class Engine {
   int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base,
              void* stream = nullptr, int64_t dual_offset = 0, bool prio_boost = false);
   void add_drift(int64_t cells);
-  // n consecutive blocks of T generations from `in` (block j: in/out
-  // alternate), block 0 over [row_lo, row_hi), as one Backend::run_flow;
-  // returns the drift.
-  int flow_blocks(void* in, void* out, const TileGeom& g, int T, int n, int64_t row_lo, int64_t row_hi,
-                  int64_t gen_base);
-  // Blocks of T a run of d generations hands to flow_blocks (0 or >= 2).
-  int flow_count(int T, int64_t d, bool keep_last) const;
   void exchange_columns(void* buf, const TileGeom& g);
   void halo_exchange_on(void* buf, const TileGeom& g);
   // Byte layout on bit words (EngineConfig::u8_compute = 1): one epoch on
@@ -318,10 +299,7 @@ class Engine {
   bool rows_wrapped_ = false; // single-rank torus read modulo its rows (no fills at all)
   bool rows_ring_ = false;    // row halos are second mappings of the owned rows (Backend::row_ring_halo)
   bool link_ = false;         // blocks may run linked (Backend::KernelChoice::link; ring tiles only)
-  bool flow_ = false;         // runs of equal blocks as one persistent launch (EngineConfig::flow)
-  int64_t flow_launches_ = 0, flow_blocks_ = 0;
   bool via_bits_ = false;    // byte layout computed on bit words (epoch_via_bits)
-  bool resident_ = false;    // one launch per epoch, tile resident in registers (Backend::resident_epoch)
   TileGeom gb_;              // the tile in the bit layout (same rows, halos, words)
   void* bitbuf_[2] = {nullptr, nullptr};  // own bit scratch when the spare byte buffer cannot hold it
   int bpar_ = 0;             // bit_scratch(bpar_) holds the current generation during a run

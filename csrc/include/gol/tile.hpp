@@ -94,9 +94,6 @@ struct BlockArgs {
   // wrap column reads within the owned words instead of reading halo columns,
   // which it then neither reads nor writes.
   bool full_width = false;
-  // The engine runs resident epochs (Backend::resident_epoch): any T, one
-  // launch that keeps the tile in the register file.
-  bool resident = false;
   // The backend may link this launch to the previous one (run both at once,
   // ordered by per-group completion words): Backend::KernelChoice::link, on
   // a single-rank ring tile whose epochs move no data between launches.
@@ -105,28 +102,6 @@ struct BlockArgs {
   // owned rows: rows outside them are the torus wrapped around, which a
   // linked launch's dependency waits must follow (life_group_impl.hpp).
   bool ring = false;
-};
-
-// A run of `nblk` temporal blocks of T generations as ONE persistent
-// dataflow launch (Backend::run_flow): block j reads buf[j & 1] and writes
-// buf[(j & 1) ^ 1]; its output rows are [row_lo + j*shrink, row_hi -
-// j*shrink) (shrink = T: the trapezoid of a deep-halo epoch; 0: a row ring,
-// every block over the owned rows, ring = true).  Same semantics as nblk
-// consecutive run_block calls (flags of generation gen_base + 1 + t at
-// changed[gen_base + 1 + t - flags_base]); returns the total drift.
-struct FlowArgs {
-  void* buf[2] = {nullptr, nullptr};
-  TileGeom g;
-  int T = 1;
-  int nblk = 0;
-  int64_t row_lo = 0, row_hi = 0;
-  int shrink = 0;
-  bool ring = false;
-  int64_t gen_base = 0;
-  uint32_t* changed = nullptr;
-  int64_t flags_base = 0;
-  bool allow_drift = false;
-  bool full_width = false;
 };
 
 }  // namespace gol

@@ -14,9 +14,9 @@
 //
 // Classes:
 //   tune          performance knobs of the default build;
-//   experimental  measured-slower kernels, schedules and timing probes: off
-//                 their default they need an experimental build
-//                 (GOL_EXPERIMENTAL=1 python -m gol_amd.native_build);
+//   probe         timing probes of the default kernels (exact but measured
+//                 slower, or wrong cells by design); the measured-slower
+//                 variants themselves were removed in round 6 (HISTORY.md);
 //   diag          traces, logs and consistency checks;
 //   fault         fault injection (tests);
 //   emul          the CPU backend emulating a device feature (tests).
@@ -37,8 +37,8 @@ struct TuningKey {
   const char* key;
   const char* env;
   const char* dflt;
-  char type;        // 'i' integer, 's' string
-  const char* cls;  // tune | experimental | diag | fault | emul
+  char type;        // 'i' integer, 'f' number, 's' string
+  const char* cls;  // tune | probe | diag | fault | emul
   const char* doc;
 };
 const std::vector<TuningKey>& tuning_keys();
@@ -49,11 +49,15 @@ class Tuning {
   // Defaults overlaid by the GOL_* variables that are set (non-empty).
   static Tuning from_env();
 
-  // key=value (unknown keys and non-integer values of integer keys fail).
+  // key=value (unknown keys, and values that do not parse as the key's type,
+  // fail with the key and its GOL_* variable named).  from_env() validates
+  // every GOL_* variable that is set, so a malformed one fails whichever
+  // component reads the tuning first.
   Tuning& set(const std::string& key, const std::string& value);
   Tuning& set(const std::string& kv);
 
   int i(const std::string& key) const;
+  double f(const std::string& key) const;
   const std::string& s(const std::string& key) const;
   bool on(const std::string& key) const { return i(key) != 0; }
   bool is_default(const std::string& key) const;
@@ -64,9 +68,6 @@ class Tuning {
   std::map<std::string, std::string> changed() const;
   // "key=value[source] ..." of the changed keys ("defaults" when none).
   std::string summary() const;
-  // Fails when an experimental-class key is off its default and the build
-  // does not carry the experimental kernels.
-  void require_build(bool experimental_build) const;
 
  private:
   std::map<std::string, std::string> v_, src_;

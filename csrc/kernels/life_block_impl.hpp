@@ -7,7 +7,7 @@
 //
 // What this kernel does instead (CDNA4-first design):
 //   * Cells are processed 32 at a time as bit planes: a lane owns W adjacent
-//     32-cell words of a row (W = 1 in the default build); a wave64 owns 64*W
+//     32-cell words of a row (W = 1); a wave64 owns 64*W
 //     adjacent words (its outermost word(s) are halo).  The neighbour count is
 //     a bit-sliced adder tree built from v_bitop3_b32 (any 3-input boolean
 //     function in ONE full-rate VALU op on gfx950).  The two bits that cross a
@@ -27,8 +27,6 @@
 //     from HBM once per T generations and every output row written once
 //     (0.03 B/cell-update at T=8 vs 2 B/cell-update for a byte-per-cell
 //     single-step stencil).  Input rows are prefetched 3 row-steps ahead.
-//   * Optional skewed (software-pipelined) level schedule: iteration i
-//     evaluates level L at row step i-L, so the T levels are independent.
 //   * The per-generation "changed" flags that replace the reference's
 //     compare/empty kernels (src/game_cuda.cu:76-126) are fused: one bitop3
 //     per word per level, reduced with __ballot at the end of the wave.
@@ -77,36 +75,10 @@ constexpr int kCpolSc1 = 16;
 // Words of the neighbouring lanes: lane i gets lane i-1's last word (left)
 // and lane i+1's first word (right).  Edge lanes receive don't-care values;
 // they only feed the wave's halo words.
-template <int XL, int W>
+template <int W>
 __device__ __forceinline__ void neighbours(const Vec<W>& c, uint32_t& lw, uint32_t& rw) {
-  if constexpr (XL == kXlaneBpermute) {
-    const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    lw = uint32_t(__builtin_amdgcn_ds_bpermute((lane - 1) * 4, int(c.w[W - 1])));
-    rw = uint32_t(__builtin_amdgcn_ds_bpermute((lane + 1) * 4, int(c.w[0])));
-  } else {
-    lw = __builtin_amdgcn_mov_dpp(c.w[W - 1], 0x138, 0xF, 0xF, true);  // wave_shr:1
-    rw = __builtin_amdgcn_mov_dpp(c.w[0], 0x130, 0xF, 0xF, true);      // wave_shl:1
-  }
-}
-
-// Cell x-1 for the lane's first word via the carry chain instead of a DPP
-// move: v_add_co (last + last) leaves every lane's top bit in VCC, the SALU
-// shifts the lane mask up by one lane (s_lshl_b64, off the VALU), and
-// v_addc adds it in as bit 0 of (first << 1).  Lane 0 gets 0 (a halo word).
-// Measured (csrc/tools/ubench_xlane.hip): 67 vs 80 cycles per level body at
-// 2 waves/SIMD, because the DPP wave shift stalls the VALU stream.
-__device__ __forceinline__ uint32_t left_in_carry(uint32_t first, uint32_t last) {
-  // Separate statements with SGPR-pair carries (not VCC) so the scheduler
-  // can interleave the chains of different levels.
-  uint32_t t, l;
-  uint64_t m;
-  asm("v_add_co_u32_e64 %0, %1, %2, %2" : "=v"(t), "=s"(m) : "v"(last));
-  m <<= 1;  // s_lshl_b64: lane j <- top bit of lane j-1
-  uint64_t co;
-  asm("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(l), "=s"(co) : "v"(first << 1), "s"(m));
-  (void)t;
-  (void)co;
-  return l;
+  lw = __builtin_amdgcn_mov_dpp(c.w[W - 1], 0x138, 0xF, 0xF, true);  // wave_shr:1
+  rw = __builtin_amdgcn_mov_dpp(c.w[0], 0x130, 0xF, 0xF, true);      // wave_shl:1
 }
 
 // Words produced per wave, and which lane words are the wave's halo: the
@@ -197,7 +169,7 @@ __device__ __forceinline__ LaneCols<IO> lane_cols(const LifeBlockParams& p, int 
 // x.  v_add_co_u32 doubles a word (shift left by one) and leaves every lane's
 // top bit in an SGPR-pair lane mask; s_lshl_b64 moves each mask bit one lane
 // up; v_addc_co_u32 adds it back in as bit 0.  All VALU ops here issue at the
-// full v_bitop3 rate (csrc/tools/ubench_dpp_mix.hip), unlike DPP/v_alignbit.
+// full v_bitop3 rate (ubench_dpp_mix.hip, git e36884f), unlike DPP/v_alignbit.
 #ifndef GOL_ADDER_NOP
 #define GOL_ADDER_NOP 0
 #endif
@@ -239,37 +211,14 @@ __device__ __forceinline__ void adder_window(uint32_t c, uint32_t& l1, uint32_t&
       : "scc");
 }
 
-// The adder window for two words per lane (w0 = cells 0..31, w1 = cells
-// 32..63 of the lane's 64): w1's left neighbour is the lane's own w0, so only
-// w0 needs a lane-shifted carry.  6 VALU + 2 SALU for two words instead of
-// 8 + 4: the carry out of (w0 << 1 | cin) is w0's top bit, which is exactly
-// w1's carry in.
-__device__ __forceinline__ void adder_window2(uint32_t w0, uint32_t w1, uint32_t& a0, uint32_t& a1, uint32_t& b0,
-                                              uint32_t& b1) {
-  uint32_t t1, t2;
-  uint64_t m1, m0, m3, m2, mz;
-  asm("v_add_co_u32_e64 %[t1], %[m1], %[w1], %[w1]\n\t"          // m1 = top bits of w1
-      "s_lshl_b64 %[m1], %[m1], 1\n\t"                           // lane j <- lane j-1
-      "v_addc_co_u32_e64 %[a0], %[m0], %[w0], %[w0], %[m1]\n\t"  // a0 = x-1 of w0; m0 = top bits of w0
-      "v_addc_co_u32_e64 %[a1], %[mz], %[w1], %[w1], %[m0]\n\t"  // a1 = x-1 of w1
-      "v_add_co_u32_e64 %[t2], %[m3], %[a1], %[a1]\n\t"          // m3 = top bits of a1
-      "s_lshl_b64 %[m3], %[m3], 1\n\t"
-      "v_addc_co_u32_e64 %[b0], %[m2], %[a0], %[a0], %[m3]\n\t"  // b0 = x-2 of w0
-      "v_addc_co_u32_e64 %[b1], %[mz], %[a1], %[a1], %[m2]"        // b1 = x-2 of w1
-      : [a0] "=&v"(a0), [a1] "=&v"(a1), [b0] "=&v"(b0), [b1] "=&v"(b1), [t1] "=&v"(t1), [t2] "=&v"(t2),
-        [m1] "=&s"(m1), [m0] "=&s"(m0), [m3] "=&s"(m3), [m2] "=&s"(m2), [mz] "=&s"(mz)
-      : [w0] "v"(w0), [w1] "v"(w1)
-      : "scc");
-}
-
 // Horizontal 3-sums (h1:h0) = left + centre + right for every word, and the
 // word of the cells the rule treats as centre (the input word itself, or for
 // the one-sided adder window the word shifted by one cell, ctr = x-1).
 template <int XL, int W>
 __device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1, Vec<W>& ctr) {
   if constexpr (XL == kXlaneAdd) {
-    static_assert(W == 1 || W == 2, "adder window: one or two words per lane");
-    if constexpr (W == 1) {
+    static_assert(W == 1, "adder window: one word per lane");
+    {
       uint32_t l1, l2;
 #if GOL_ADDER_FAKE
       // Timing probe only (WRONG cells): the window's shifts without the
@@ -288,33 +237,16 @@ __device__ __forceinline__ void hsum(const Vec<W>& c, Vec<W>& h0, Vec<W>& h1, Ve
       h0.w[0] = bop3<tt::XOR3>(l2, l1, c.w[0]);
       h1.w[0] = bop3<tt::MAJ>(l2, l1, c.w[0]);
       ctr.w[0] = l1;
-    } else {
-      uint32_t a0, a1, b0, b1;
-      adder_window2(c.w[0], c.w[1], a0, a1, b0, b1);
-      h0.w[0] = bop3<tt::XOR3>(b0, a0, c.w[0]);
-      h1.w[0] = bop3<tt::MAJ>(b0, a0, c.w[0]);
-      h0.w[1] = bop3<tt::XOR3>(b1, a1, c.w[1]);
-      h1.w[1] = bop3<tt::MAJ>(b1, a1, c.w[1]);
-      ctr.w[0] = a0;
-      ctr.w[1] = a1;
     }
     return;
   }
   ctr = c;
-  uint32_t lw = 0, rw;
-  if constexpr (XL == kXlaneCarry) {
-    rw = __builtin_amdgcn_mov_dpp(c.w[0], 0x130, 0xF, 0xF, true);  // wave_shl:1
-  } else {
-    neighbours<XL>(c, lw, rw);
-  }
+  uint32_t lw, rw;
+  neighbours(c, lw, rw);
 #pragma unroll
   for (int i = 0; i < W; ++i) {
     const uint32_t hi = i == W - 1 ? rw : c.w[i + 1];
-    uint32_t l;
-    if (XL == kXlaneCarry && i == 0)
-      l = left_in_carry(c.w[0], c.w[W - 1]);
-    else
-      l = __builtin_amdgcn_alignbit(c.w[i], i == 0 ? lw : c.w[i - 1], 31);  // cell x-1
+    const uint32_t l = __builtin_amdgcn_alignbit(c.w[i], i == 0 ? lw : c.w[i - 1], 31);  // cell x-1
     const uint32_t r = __builtin_amdgcn_alignbit(hi, c.w[i], 1);            // cell x+1
     h0.w[i] = bop3<tt::XOR3>(l, c.w[i], r);
     h1.w[i] = bop3<tt::MAJ>(l, c.w[i], r);
@@ -513,8 +445,7 @@ struct RowReader {
 template <int T, int W>
 struct Levels {
   Vec<W> h0[T][3], h1[T][3], cc[T][3];
-  Vec<W> acc[T];   // per word: OR of (new ^ old) per produced level L+1
-  Vec<W> pipe[T];  // skewed schedule: pending input row of level L
+  Vec<W> acc[T];  // per word: OR of (new ^ old) per produced level L+1
 };
 
 // Level L at a step in slot S: push the new level-L row `cur` into the
@@ -570,8 +501,8 @@ __device__ __forceinline__ void prologue_tri(Levels<T, IO::W>& st, RD& rd, const
     constexpr int S = K % 3;
     constexpr int nfull = K / 2;
     const Vec<IO::W> cur = levels_full<T, IO, S, 0, nfull>(st, rd.template take<S>(K));
-    // Split schedule: level `nfull` rows in0 + nfull (K even) and
-    // in0 + nfull + 1 (K odd) are the top boundary state.
+    // Level `nfull` rows in0 + nfull (K even) and in0 + nfull + 1 (K odd):
+    // the grouped kernel shares them with the wave above (life_group_impl.hpp).
     if constexpr (nfull >= 1 && nfull < T) save(nfull, K - 2 * nfull, cur);
     if constexpr (nfull < T) level_store<T, IO, S, nfull>(st, cur);
     prologue_tri<T, IO, K + 1>(st, rd, save, bottom);
@@ -586,58 +517,6 @@ struct NoSave {
 struct NoBottom {
   template <int S, class St>
   __device__ __forceinline__ void at(const St&, int) const {}
-};
-
-// Boundary level states of the split schedule.  side 0 = bottom of the
-// segment above boundary bnd (level L rows b-L-2, b-L-1 as j = 0, 1), side 1
-// = top of the segment below (rows b+L, b+L+1).  Row-major: one state row
-// holds the words of every column, so a wave's store / load of a state is
-// 256 contiguous bytes (a column-major layout made each of them touch 64
-// cache lines and was HBM-bound).
-template <int T>
-__device__ __forceinline__ uint32_t* state_row(const LifeBlockParams& p, int bnd, int side, int L, int j) {
-  return p.state + ((((int64_t(bnd) * 2 + side) * (T - 1) + (L - 1)) * 2 + j) * p.state_pitch);
-}
-
-// Lanes without a real target (no boundary, wave-halo or out-of-tile words)
-// store into a dummy boundary slot (index nseg - 1) instead of branching.
-template <int T, int W>
-struct StateSaver {
-  const LifeBlockParams* p;
-  int bnd;      // wave-uniform boundary index (dummy slot when none)
-  int off[W];   // word column (own words) or the same column of the dummy slot
-  int dummy_bnd;
-  bool real[W];
-  __device__ __forceinline__ void operator()(int L, int j, const Vec<W>& v) const {
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-      uint32_t* r = state_row<T>(*p, real[i] ? bnd : dummy_bnd, 1, L, j);
-      r[off[i]] = v.w[i];
-    }
-  }
-};
-
-// Bottom boundary state: after step k = kend-2 (kend-1) window slot S holds
-// level L row s1-2-L (s1-1-L) for every level; saved as j = 0 (1).
-template <int T, int W>
-struct BottomSaver {
-  const LifeBlockParams* p;
-  int bnd;  // wave-uniform; < 0: none
-  int off[W];
-  bool own[W];
-  int kend;
-  template <int S, class St>
-  __device__ __forceinline__ void at(const St& st, int k) const {
-    if (bnd < 0 || k < kend - 2) return;  // wave-uniform
-    const int j = k - (kend - 2);
-#pragma unroll
-    for (int L = 1; L < T; ++L) {
-      uint32_t* r = state_row<T>(*p, bnd, 0, L, j);
-#pragma unroll
-      for (int i = 0; i < W; ++i)
-        if (own[i]) r[off[i]] = st.cc[L][S].w[i];
-    }
-  }
 };
 
 // Output of one row: lanes store the words they own (not the wave halos).
@@ -668,90 +547,18 @@ struct Writer {
   }
 };
 
-// ---- skewed (software-pipelined) schedule ----------------------------------
-// Iteration i evaluates level L at row step i - L; level L's input is level
-// L-1's output from the previous iteration (pipe[L]).  Phases after the 2T
-// straight prologue steps: ramp r = 1..T-1 (step 2T-1+r for levels
-// 0..T-1-r), steady i = 3T-1..kend-1, drain (levels L > i-kend only).
-template <int U, int L>
-constexpr int skew_slot() {
-  return ((U - L) % 3 + 3) % 3;
-}
-
-template <int T, class IO, int U, int L, int LO, int W = IO::W>
-__device__ __forceinline__ Vec<W> skew_levels(Levels<T, W>& st, const Vec<W>& row0, Vec<W> top) {
-  if constexpr (L < LO) {
-    return top;
-  } else {
-    const Vec<W> o = level_full<T, IO, skew_slot<U, L>(), L>(st, L == 0 ? row0 : st.pipe[L]);
-    if constexpr (L == T - 1) {
-      top = o;
-    } else {
-      st.pipe[L + 1] = o;
-    }
-    return skew_levels<T, IO, U, L - 1, LO>(st, row0, top);
-  }
-}
-
-template <int T, class IO, int R>
-__device__ __forceinline__ void ramp(Levels<T, IO::W>& st, RowReader<IO>& rd) {
-  if constexpr (R < T) {
-    constexpr int K = 2 * T - 1 + R;
-    constexpr int S = K % 3;
-    st.pipe[T - R] = levels_full<T, IO, S, 0, T - R>(st, rd.template take<S>(K));
-    ramp<T, IO, R + 1>(st, rd);
-  }
-}
-
-template <int T, class IO, int D, int U>
-__device__ __forceinline__ void drain_all(Levels<T, IO::W>& st, int i, const Writer<IO>& wr) {
-  if constexpr (D < T - 1) {
-    const Vec<IO::W> zero{};
-    wr.row(i - (T - 1) - T, skew_levels<T, IO, U, T - 1, D + 1>(st, zero, zero));
-    drain_all<T, IO, D + 1, (U + 1) % 3>(st, i + 1, wr);
-  }
-}
-
-template <int T, class IO, int U>
-__device__ __forceinline__ void skew_steady_and_drain(Levels<T, IO::W>& st, RowReader<IO>& rd, int kend,
-                                                      const Writer<IO>& wr) {
-  constexpr int W = IO::W;
-  constexpr int U0 = U, U1 = (U + 1) % 3, U2 = (U + 2) % 3;
-  const Vec<W> zero{};
-  int i = 3 * T - 1;
-  for (; i + 3 <= kend; i += 3) {
-    wr.row(i - (T - 1) - T, skew_levels<T, IO, U0, T - 1, 0>(st, rd.template take<U0>(i), zero));
-    wr.row(i + 1 - (T - 1) - T, skew_levels<T, IO, U1, T - 1, 0>(st, rd.template take<U1>(i + 1), zero));
-    wr.row(i + 2 - (T - 1) - T, skew_levels<T, IO, U2, T - 1, 0>(st, rd.template take<U2>(i + 2), zero));
-  }
-  const int rem = kend - i;
-  if (rem == 0) {
-    drain_all<T, IO, 0, U0>(st, i, wr);
-  } else if (rem == 1) {
-    wr.row(i - (T - 1) - T, skew_levels<T, IO, U0, T - 1, 0>(st, rd.template take<U0>(i), zero));
-    drain_all<T, IO, 0, U1>(st, i + 1, wr);
-  } else {
-    wr.row(i - (T - 1) - T, skew_levels<T, IO, U0, T - 1, 0>(st, rd.template take<U0>(i), zero));
-    wr.row(i + 1 - (T - 1) - T, skew_levels<T, IO, U1, T - 1, 0>(st, rd.template take<U1>(i + 1), zero));
-    drain_all<T, IO, 0, U2>(st, i + 2, wr);
-  }
-}
-
-// SPLIT = true: phase 1 of the split schedule.  Segments tile the input rows
-// [row_lo - T, row_hi + T) without overlap; each wave computes the
-// trapezoid its own rows determine (level L on [in0 + L, in1 - L)), stores
-// the level-T rows [in0 + T, in1 - T) and saves, per level, the two rows
-// next to each boundary for phase 2 (life_split_down_kernel).
 // Optional occupancy target for the bit-layout T = 16 kernel (171 VGPRs
 // unconstrained = 2 waves/SIMD).  Forcing 3 waves/SIMD (-DGOL_T16_WAVES=3,
 // <= 168 VGPRs with small spills) measured 3-8% slower, so it is off.
-template <int T, class IO, bool SKEW, bool SPLIT>
+template <int T, class IO>
 constexpr int min_waves_per_eu() {
-  return (T == 16 && IO::W == 1 && IO::kBits && !SKEW) ? GOL_T16_WAVES : 1;
+  return (T == 16 && IO::W == 1 && IO::kBits) ? GOL_T16_WAVES : 1;
 }
 
-template <int T, class IO, bool SKEW, bool SPLIT = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<T, IO, SKEW, SPLIT>())))
+// The classic schedule (life_block_launch.hpp): one wave per (column strip,
+// row segment), its 2T-row prologue redundant with the wave above's rows.
+template <int T, class IO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<T, IO>())))
 void life_block_kernel(const LifeBlockParams p) {
   constexpr int W = IO::W;
   const int lane = threadIdx.x & 63;
@@ -767,12 +574,10 @@ void life_block_kernel(const LifeBlockParams p) {
   const int kcol = gw / p.nseg;
   const int seg = gw - kcol * p.nseg;
   // Balanced segments: the first `seg_rem` segments get one extra row.
-  const int64_t base = (SPLIT ? p.row_lo - T : p.row_lo) + roff;
-  const int64_t s0 = base + int64_t(seg) * p.seg_rows + min(seg, p.seg_rem);
-  const int64_t s1 = s0 + p.seg_rows + (seg < p.seg_rem ? 1 : 0);
-  const int64_t o0 = SPLIT ? s0 + T : s0;  // level-T output rows [o0, o1)
-  const int64_t o1 = SPLIT ? s1 - T : s1;
-  if (!SPLIT && o0 >= o1) return;  // wave-uniform
+  const int64_t base = p.row_lo + roff;
+  const int64_t o0 = base + int64_t(seg) * p.seg_rows + min(seg, p.seg_rem);  // level-T output rows [o0, o1)
+  const int64_t o1 = o0 + p.seg_rows + (seg < p.seg_rem ? 1 : 0);
+  if (o0 >= o1) return;  // wave-uniform
 
   // Lane words (lane_cols): the wave's first and last words are halo words.
   const LaneCols<IO> lc = lane_cols<IO>(p, kcol, lane);
@@ -796,7 +601,7 @@ void life_block_kernel(const LifeBlockParams p) {
     for (int i = 0; i < W; ++i) {
 #pragma unroll
       for (int s = 0; s < 3; ++s) st.h0[L][s].w[i] = st.h1[L][s].w[i] = st.cc[L][s].w[i] = 0u;
-      st.pipe[L].w[i] = st.acc[L].w[i] = 0u;
+      st.acc[L].w[i] = 0u;
     }
   }
 
@@ -813,47 +618,17 @@ void life_block_kernel(const LifeBlockParams p) {
   wr.col = col;
 
   // Prologue: 2T steps, no stores.
-  StateSaver<T, W> saver;
-  BottomSaver<T, W> bottom;
-  saver.p = bottom.p = &p;
-  saver.bnd = seg - 1;
-  saver.dummy_bnd = p.nseg - 1;
-  bottom.bnd = SPLIT && seg < p.nseg - 1 ? seg : -1;
-  bottom.kend = kend;
-#pragma unroll
-  for (int i = 0; i < W; ++i) {
-    saver.off[i] = bottom.off[i] = min(max(col + i, 0), p.Wp - 1);
-    saver.real[i] = seg > 0 && wr.own[i];
-    bottom.own[i] = wr.own[i];
+  prologue_tri<T, IO, 0>(st, rd, NoSave{}, NoBottom{});
+  int k = kPro;
+  constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
+  for (; k + 3 <= kend; k += 3) {
+    wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
+    wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
+    wr.row(k + 2 - T, levels_full<T, IO, S2, 0, T>(st, rd.template take<S2>(k + 2)));
   }
-  if constexpr (SPLIT)
-    prologue_tri<T, IO, 0>(st, rd, saver, bottom);
-  else
-    prologue_tri<T, IO, 0>(st, rd, NoSave{}, NoBottom{});
-
-  if constexpr (SKEW && T > 1) {
-    // Requires o1 - o0 >= T (guaranteed by plan()).
-    ramp<T, IO, 1>(st, rd);
-    skew_steady_and_drain<T, IO, (3 * T - 1) % 3>(st, rd, kend, wr);
-  } else {
-    int k = kPro;
-    constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
-    for (; k + 3 <= kend; k += 3) {
-      wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
-      if constexpr (SPLIT) bottom.template at<S0>(st, k);
-      wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
-      if constexpr (SPLIT) bottom.template at<S1>(st, k + 1);
-      wr.row(k + 2 - T, levels_full<T, IO, S2, 0, T>(st, rd.template take<S2>(k + 2)));
-      if constexpr (SPLIT) bottom.template at<S2>(st, k + 2);
-    }
-    if (k < kend) {
-      wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
-      if constexpr (SPLIT) bottom.template at<S0>(st, k);
-      if (k + 1 < kend) {
-        wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
-        if constexpr (SPLIT) bottom.template at<S1>(st, k + 1);
-      }
-    }
+  if (k < kend) {
+    wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
+    if (k + 1 < kend) wr.row(k + 1 - T, levels_full<T, IO, S1, 0, T>(st, rd.template take<S1>(k + 1)));
   }
 
   // Fused termination flags: one bit per generation level, counting only
@@ -873,167 +648,20 @@ void life_block_kernel(const LifeBlockParams p) {
 }
 
 
-// Phase 2 of the split schedule: the inverted triangle at the boundary b
-// between segments bnd and bnd+1.  Level L+1 (L = 0..T-1) is computed on rows
-// [b-L-1, b+L+1) from level L rows [b-L-2, b+L+2): the inner 2L rows were
-// computed here one level earlier, the two outer rows on each side are
-// phase 1's saved states (level 0: the input rows).  Evaluated level by
-// level with every row of a level in registers, so all rows of a level are
-// independent (the streaming order of phase 1 would chain the levels).
-// Every level-row is computed exactly once over both phases, so the
-// per-generation flags stay exact.
-template <int N, int W>
-struct Rows {
-  Vec<W> r[N];
-};
-
-template <int T, class IO>
-struct DownCtx {
-  static constexpr int W = IO::W;
-  const LifeBlockParams* p;
-  int64_t b;
-  bool ok[W];
-  int off[W];
-  int bnd;
-  uint32_t fmask[W];
-  __device__ __forceinline__ Vec<W> input(int64_t row) const {
-    return IO::convert(IO::load_raw(p->in + row * p->pitch, off), ok);
-  }
-  __device__ __forceinline__ Vec<W> state(int side, int L, int j) const {
-    Vec<W> v;
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-      const uint32_t x = state_row<T>(*p, bnd, side, L, j)[off[i]];  // clamped column: always valid
-      v.w[i] = ok[i] ? x : 0u;
-    }
-    return v;
-  }
-};
-
-// sv[L][0..3]: level L rows b-L-2, b-L-1 (side 0) and b+L, b+L+1 (side 1),
-// all loaded up front: the early levels are a handful of rows each, so
-// loading per level would expose one memory latency per level.
-template <int T, class IO, int L>
-__device__ __forceinline__ void down_level(const DownCtx<T, IO>& ctx, const Writer<IO>& wr,
-                                           const Rows<2 * L + 4, IO::W>& cur, Vec<IO::W> (&acc)[T],
-                                           const Vec<IO::W> (&sv)[T][4]) {
-  constexpr int W = IO::W;
-  constexpr int N = 2 * L + 4;  // level L rows [b-L-2, b+L+2)
-  // Rows are swept in order with a 3-row window of horizontal sums, so only
-  // the cells of the two levels are live (a full h0/h1 array per level needs
-  // > 256 VGPRs at T = 16).  sched_barrier every 8 rows stops the max-ILP
-  // scheduler from hoisting every row's DPP shifts to the top of the level.
-  Rows<N + 2, W> nxt;  // level L+1 rows [b-L-3, b+L+3); inner N-2 computed
-  static_assert(IO::XL != kXlaneAdd, "split schedule: symmetric windows only");
-  Vec<W> ha0, ha1, hb0, hb1, hc0, hc1, cdummy;
-  hsum<IO::XL>(cur.r[0], ha0, ha1, cdummy);
-  hsum<IO::XL>(cur.r[1], hb0, hb1, cdummy);
-#pragma unroll
-  for (int q = 0; q < N - 2; ++q) {
-    hsum<IO::XL>(cur.r[q + 2], hc0, hc1, cdummy);
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-      const uint32_t ctr = cur.r[q + 1].w[i];
-      const uint32_t v = rule(ha0.w[i], ha1.w[i], hb0.w[i], hb1.w[i], hc0.w[i], hc1.w[i], ctr);
-      acc[L].w[i] = bop3<tt::OR_XOR>(acc[L].w[i], v, ctr);
-      nxt.r[q + 2].w[i] = v;
-    }
-    ha0 = hb0;
-    ha1 = hb1;
-    hb0 = hc0;
-    hb1 = hc1;
-    if (q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
-  }
-  if constexpr (L + 1 == T) {
-#pragma unroll
-    for (int q = 0; q < N - 2; ++q) wr.row(ctx.b - T + q, nxt.r[q + 2]);
-  } else {
-    nxt.r[0] = sv[L + 1][0];      // level L+1 row b-L-3
-    nxt.r[1] = sv[L + 1][1];      //                 b-L-2
-    nxt.r[N] = sv[L + 1][2];      //                 b+L+1
-    nxt.r[N + 1] = sv[L + 1][3];  //                 b+L+2
-    down_level<T, IO, L + 1>(ctx, wr, nxt, acc, sv);
-  }
-}
-
-template <int T, class IO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void life_split_down_kernel(
-    const LifeBlockParams p) {
-  constexpr int W = IO::W;
-  constexpr int kWaveOut = wave_out_words<IO::XL, W>();
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nb = p.nseg - 1;
-  if (gw >= p.ncolw * nb) return;  // wave-uniform
-  const int kcol = gw / nb;
-  const int bnd = gw - kcol * nb;
-
-  DownCtx<T, IO> ctx;
-  ctx.p = &p;
-  ctx.bnd = bnd;
-  ctx.b = (p.row_lo - T) + int64_t(bnd + 1) * p.seg_rows + min(bnd + 1, p.seg_rem);
-  const int col = kcol * kWaveOut - 1 + W * lane;
-  Writer<IO> wr;
-#pragma unroll
-  for (int i = 0; i < W; ++i) {
-    const int c = col + i;
-    const bool ok = c >= 0 && c < p.Wp;
-    const bool halo = wave_halo<IO::XL, W>(lane, i);
-    ctx.ok[i] = ok;
-    ctx.off[i] = min(max(c, 0), p.Wp - 1);
-    wr.own[i] = ok && !halo;
-    ctx.fmask[i] = (wr.own[i] && c >= p.own_w0 && c < p.own_w1) ? (c == p.own_w1 - 1 ? p.last_mask : ~0u) : 0u;
-  }
-  wr.out = p.out;
-  wr.pitch = p.pitch;
-  wr.col = col;
-
-  Vec<W> acc[T];
-#pragma unroll
-  for (int L = 0; L < T; ++L)
-#pragma unroll
-    for (int i = 0; i < W; ++i) acc[L].w[i] = 0u;
-  Rows<4, W> lvl0;  // input rows [b-2, b+2)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) lvl0.r[r] = ctx.input(ctx.b - 2 + r);
-  Vec<W> sv[T][4];
-#pragma unroll
-  for (int L = 1; L < T; ++L) {
-    sv[L][0] = ctx.state(0, L, 0);
-    sv[L][1] = ctx.state(0, L, 1);
-    sv[L][2] = ctx.state(1, L, 0);
-    sv[L][3] = ctx.state(1, L, 1);
-  }
-  down_level<T, IO, 0>(ctx, wr, lvl0, acc, sv);
-
-  if (p.changed) {
-    uint32_t mask = 0;
-#pragma unroll
-    for (int L = 0; L < T; ++L) {
-      uint32_t any = 0;
-#pragma unroll
-      for (int i = 0; i < W; ++i) any |= acc[L].w[i] & ctx.fmask[i];
-      mask |= (__ballot(any != 0u) != 0ull ? 1u : 0u) << L;
-    }
-    uint32_t* ch = p.gen_dev ? p.changed + (*p.gen_dev + p.gen_rel) : p.changed;
-    if (lane < T && ((mask >> lane) & 1u)) ch[lane] = 1u;
-  }
-}
-
 // Segment planning.  A wave owns a column strip and a balanced segment of
 // output rows.  Its 2T-row prologue is redundant work (about T/2 rows' worth
 // of level bodies), so segments want to be long; the launch wants every SIMD
 // busy, and two resident waves per SIMD issue ~1.2x faster than one
-// (csrc/tools/ubench_level.hip: 97 vs 80 cycles per level body).  The
+// (ubench_level.hip, git e36884f: 97 vs 80 cycles per level body).  The
 // planner scores each segment count by the makespan of the most loaded SIMD:
 //     rounds * (seg_rows + T/2 + 2) * k * t(k),   k = resident waves/SIMD
 // and keeps the cheapest.  (Filling 1122 waves into 1024 SIMDs would put two
 // waves on a tenth of them and nearly double the kernel time; the model
 // prefers 1020 or 2040 waves there.)
-// Returns whether the skewed schedule applies (every segment >= T rows);
-// *cost_out (optional) receives the model's score of the chosen plan.
+// Returns whether every segment has >= T rows; *cost_out (optional)
+// receives the model's score of the chosen plan.
 // Relative time per level body of a SIMD holding k resident waves (k = 1..4),
-// per kernel family.  DPP/alignbit windows (csrc/tools/ubench_level.hip):
+// per kernel family.  DPP/alignbit windows (ubench_level.hip, git e36884f):
 // ~1.2x slower with one wave, flat from two.  The adder window issues two
 // extra SALU shifts per body and only reaches its rate with four waves per
 // SIMD (bench: 32768 x 16384 tile at T = 12, 2.5 / 3 / 4 waves per SIMD =
@@ -1084,9 +712,9 @@ int occupancy_of(K kernel) {
   return blocks;
 }
 
-template <int T, class IO, bool SKEW, bool SPLIT>
+template <int T, class IO>
 int waves_per_simd() {
-  static const int cached = occupancy_of(life_block_kernel<T, IO, SKEW, SPLIT>);
+  static const int cached = occupancy_of(life_block_kernel<T, IO>);
   return cached;
 }
 

@@ -2,24 +2,16 @@
 // per layout x words-per-lane x cross-lane primitive, life_block_*.hip):
 // chooses the schedule of a temporal block and its launch shape.
 //   grouped  life_group_kernel (life_group_impl.hpp): default for T >= 4 when
-//            the rows allow M segments of 2T rows per group (GOL_GROUP)
-//   short    life_short_kernel (life_short_impl.hpp): grouped, segments of
-//            Q < 2T rows, when the makespan model prefers it (GOL_SHORT)
-//   pipe     life_pipe_kernel (life_pipe_impl.hpp): grouped, each segment's
-//            levels split over a wave pair (GOL_PIPE)
-//   classic  life_block_kernel: T < 4, short tiles, GOL_GROUP=0, GOL_SKEW=1
-//   split    life_block_kernel<SPLIT> + life_split_down_kernel: GOL_SPLIT=1
+//            the rows allow M segments of 2T rows per group (GOL_GROUP);
+//            linked (two launches in flight) or chained where that pays
+//   pipe     life_pipe_kernel (life_pipe_impl.hpp): the byte layout's T = 48
+//            pass, each segment's levels split over a wave pair
+//   classic  life_block_kernel: T < 4, short tiles, GOL_GROUP=0
+// Schedules measured slower and removed in round 6 (docs/HISTORY.md): short
+// segments, bit-layout pipelined pairs, split and skewed schedules.
 #pragma once
 
 #include "life_pipe_impl.hpp"
-#ifdef GOL_EXPERIMENTAL
-// Measured-slower schedules (docs/PERFORMANCE.md): short segments, bit-layout
-// level-pipelined pairs, the split and skewed schedules are
-// compiled only into experimental builds (GOL_EXPERIMENTAL=1 native_build);
-// the default build keeps the grouped / chained / classic kernels and the
-// byte layout's T = 48 pipelined pass.
-#include "life_short_impl.hpp"
-#endif
 
 namespace gol {
 namespace hipk {
@@ -149,7 +141,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
   if (tune.link) {
     if constexpr (IO::kBits && IO::W == 1 && (T == 8 || T == 12 || T == 16) &&
                   (IO::XL == kXlaneDpp || IO::XL == kXlaneAdd)) {
-      if (tune.group != 0 && tune.split == 0 && !tune.skew && dual == 1) {
+      if (tune.group != 0 && dual == 1) {
         // Blocks of T <= 8 link 4-wave groups where the unlinked path would
         // group 4 waves (tune group_small).
         if constexpr (T <= 8) {
@@ -170,7 +162,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
     // group 4 waves by default: 8192^2 at T = 8 1.99 vs 2.06 ms per 1000
     // generations with 8-wave groups (profiles/r04/small_grid_ab.jsonl).
     const int group = (IO::kBits && T <= 8) ? tune.group_small : tune.group;
-    if (group != 0 && (tune.split == 0 || dual == 2) && !tune.skew) {
+    if (group != 0) {
       // M = 4 or 8 waves per workgroup; auto (-1) takes the cheapest of
       // M = 4, M = 8 and the classic plan under the makespan model (classic
       // charged its redundant triangle, T-1 rows, at the triangles' ILP).
@@ -186,42 +178,10 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       double cc = -1.0;
       if (group < 0) {
         LifeBlockParams q = p;
-        plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves,
-             1.2 * (T - 1), &cc, IO::XL);
+        plan(q, T, out_rows, simds, waves_per_simd<T, IO>(), tune.min_seg_rows, tune.target_waves, 1.2 * (T - 1),
+             &cc, IO::XL);
       }
-      // Segments shorter than 2T (compiled for the default T = 16 bit-layout
-      // kernel; the byte layout spills at 4 waves/SIMD): lets small tiles
-      // fill 4 waves per SIMD.
       const auto better = [](double a, double b) { return a > 0 && (b < 0 || a <= b); };
-#ifdef GOL_EXPERIMENTAL
-      if constexpr (IO::kBits && IO::W == 1 &&
-                    ((T == 16 && IO::XL == kXlaneDpp) || (T == 12 && IO::XL == kXlaneAdd))) {
-        LifeBlockParams s8 = p;
-        const double cs = tune.short_seg && dual == 1 && (group == 8 || group < 0)
-                              ? plan_short<T, 8>(s8, out_rows, simds, short_waves_per_simd<T, IO, 8>(),
-                                                 tune.target_waves, IO::XL)
-                              : -1.0;
-        if (cs > 0 && (tune.short_seg == 2 || (better(cs, c4) && better(cs, c8) && better(cs, cc))))
-          return launch_short<T, IO, 8>(s8, s);
-      }
-      // Level-pipelined pairs (T/2 + T/2 levels): twice the waves per SIMD.
-      if constexpr (IO::kBits && IO::W == 1 && (T == 12 || T == 16) &&
-                    (IO::XL == kXlaneDpp || IO::XL == kXlaneAdd)) {
-        constexpr int T1 = T / 2, T2 = T - T / 2;
-        if (tune.pipe && dual == 1) {
-          LifeBlockParams p8 = p, p4 = p;
-          const double cp8 = plan_pipe<T1, T2, 8>(p8, out_rows, simds, pipe_waves_per_simd<T1, T2, IO, 8>(),
-                                                  tune.target_waves, IO::XL);
-          const double cp4 = plan_pipe<T1, T2, 4>(p4, out_rows, simds, pipe_waves_per_simd<T1, T2, IO, 4>(),
-                                                  tune.target_waves, IO::XL);
-          const bool forced = tune.pipe == 2;
-          const bool use8 = cp8 > 0 && (better(cp8, cp4) || cp4 < 0);
-          const double cp = use8 ? cp8 : cp4;
-          if (cp > 0 && (forced || (better(cp, c4) && better(cp, c8) && better(cp, cc))))
-            return use8 ? launch_pipe<T1, T2, IO, 8>(p8, s) : launch_pipe<T1, T2, IO, 4>(p4, s);
-        }
-      }
-#endif  // GOL_EXPERIMENTAL
       // Chained groups (GOL_CHAIN): every group boundary shared through
       // global memory, so no wave carries a redundant triangle but the
       // strip's last.  Stream launches only (the flags count launches, so a
@@ -254,52 +214,11 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       if (better(c4, c8) && better(c4, cc)) return launch_group<T, IO, 4>(g4, s);
       if (better(c8, cc)) return launch_group<T, IO, 8>(g8, s);
     }
-#ifdef GOL_EXPERIMENTAL
-    // The split kernels address boundary states by padded column: halo mode only.
-    bool split = tune.split > 0 && IO::XL != kXlaneAdd && dual == 1 && p.wrap_w == 0;
-    if (tune.split < 0 && !tune.skew && IO::XL != kXlaneAdd && dual == 1 && p.wrap_w == 0) {
-      LifeBlockParams q = p;
-      plan(q, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves);
-      split = q.seg_rows < kSplitMaxRowsPerT * T;
-    }
-    if constexpr (IO::XL != kXlaneAdd) if (split && tune.scratch) {
-      const int64_t in_rows = out_rows + 2 * int64_t(T);
-      // Segments of >= 2T + 2 input rows: the last two steps (bottom state)
-      // then fall in the steady loop, never in the prologue.
-      plan(p, T, in_rows, simds, waves_per_simd<T, IO, false, true>(), std::max(tune.min_seg_rows, 2 * T + 2),
-           tune.target_waves, 0.0);
-      p.state_pitch = round_up(int64_t(p.Wp), int64_t(64));  // words per state row
-      const int64_t nb = p.nseg - 1;
-      // nb boundaries + 1 dummy slot, 2 sides, T-1 levels, 2 rows
-      p.state = static_cast<uint32_t*>(tune.scratch(size_t((nb + 1) * 2 * (T - 1) * 2 * p.state_pitch * 4)));
-      hipLaunchKernelGGL((life_block_kernel<T, IO, false, true>), dim3(unsigned(ceil_div(p.ncolw * p.nseg, 4))),
-                         dim3(256), 0, s, p);
-      if (nb > 0)
-        hipLaunchKernelGGL((life_split_down_kernel<T, IO>), dim3(unsigned(ceil_div(int64_t(p.ncolw) * nb, int64_t(4)))),
-                           dim3(256), 0, s, p);
-      return;
-    }
-#endif  // GOL_EXPERIMENTAL
   }
-#ifdef GOL_EXPERIMENTAL
-  const int occ = tune.skew ? waves_per_simd<T, IO, true, false>() : waves_per_simd<T, IO, false, false>();
-  const bool skew = plan(p, T, out_rows, simds, occ, tune.min_seg_rows, tune.target_waves, -1, nullptr, IO::XL) &&
-                    tune.skew;
-#else
-  const bool skew = false;
-  plan(p, T, out_rows, simds, waves_per_simd<T, IO, false, false>(), tune.min_seg_rows, tune.target_waves, -1,
-       nullptr, IO::XL);
-#endif
+  plan(p, T, out_rows, simds, waves_per_simd<T, IO>(), tune.min_seg_rows, tune.target_waves, -1, nullptr, IO::XL);
   const int waves = p.ncolw * p.nseg * dual;
   const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
-#ifdef GOL_EXPERIMENTAL
-  if (skew) {
-    hipLaunchKernelGGL((life_block_kernel<T, IO, true>), grid, block, 0, s, p);
-    return;
-  }
-#endif
-  (void)skew;
-  hipLaunchKernelGGL((life_block_kernel<T, IO, false>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((life_block_kernel<T, IO>), grid, block, 0, s, p);
 }
 
 // Deep byte-layout passes (T = 24, 32): instantiated in translation units of

@@ -5,9 +5,9 @@
 // The classic schedule starts every wave segment T rows above its output and
 // recomputes the triangle of level rows that the segment above also computes:
 // T(T-1) level-rows per boundary, 240 at T = 16, against 16 x 34 useful
-// level-rows per wave on the 8-GPU per-rank tile (32768 x 4096).  The split
-// schedule (life_split_down_kernel) moves the triangle into a second kernel,
-// which measured slower.  Here a workgroup of M waves owns M consecutive
+// level-rows per wave on the 8-GPU per-rank tile (32768 x 4096).  A split
+// schedule (the triangle in a second kernel) measured slower and was removed.
+// Here a workgroup of M waves owns M consecutive
 // segments of one column strip and shares its M-1 internal boundaries through
 // LDS:
 //   * wave m reads input rows from in0 = G0 + m q - T (G0 = first output row
@@ -299,7 +299,7 @@ __device__ __forceinline__ void epilogue_tri(Levels<T, IO::W>& st, RowReader<IO>
 #endif
 // The adder window's T = 16 grouped kernel lands at ~156 VGPRs (3 waves/SIMD)
 // unconstrained; its level body is 17% cheaper at 4 waves/SIMD than at 3
-// (csrc/tools/ubench_body.hip), so it is held to 128 VGPRs.
+// (ubench_body.hip, git e36884f), so it is held to 128 VGPRs.
 #ifndef GOL_GROUP_T16_ADD_WAVES
 #define GOL_GROUP_T16_ADD_WAVES 4
 #endif
@@ -413,7 +413,7 @@ void life_group_kernel(const LifeBlockParams p) {
     for (int i = 0; i < W; ++i) {
 #pragma unroll
       for (int s = 0; s < 3; ++s) st.h0[L][s].w[i] = st.h1[L][s].w[i] = st.cc[L][s].w[i] = 0u;
-      st.pipe[L].w[i] = st.acc[L].w[i] = 0u;
+      st.acc[L].w[i] = 0u;
     }
   }
 

@@ -26,11 +26,6 @@ struct LifeBlockParams {
   uint32_t* changed;  // changed[L] <-> generation gen_base + 1 + L (after resolving gen_dev)
   const int64_t* gen_dev;  // if set: changed += *gen_dev + gen_rel at run time (graph replay)
   int64_t gen_rel;
-  // Split schedule (life_block_impl.hpp): segments tile the INPUT rows
-  // [row_lo - T, row_hi + T); boundary level states go to `state`
-  // (rows of state_pitch 32-bit words).
-  uint32_t* state;
-  int64_t state_pitch;
   // Grouped schedule (life_group_kernel): nseg = groups per column strip,
   // seg_rows/seg_rem = balanced OUTPUT rows per group, grp_q = output rows of
   // every wave of a group but the last.
@@ -88,84 +83,13 @@ struct LifeBlockParams {
   // the rows a group reads beyond them wrap around the torus (link_wait).
   int64_t link_ring_rows;
   // Fault injection (GOL_FAULT_DELAY_SPINS, tests): producers at the torus
-  // seam - a linked launch's first and last groups, a flow block's first and
-  // last row positions and its folded items - sleep this many s_sleep 127
+  // seam - a linked launch's first and last groups - sleep this many s_sleep 127
   // rounds (~3.4 us each) before publishing, so a missing dependency wait
   // reads stale rows deterministically instead of by chance.
   int fault_delay;
 };
 
 constexpr int64_t kWgTraceWaves = int64_t(1) << 20;
-
-// ---- Persistent dataflow launch (life_flow_impl.hpp) -----------------------
-// Work items of one temporal block: (column strip, group of M wave segments),
-// the grouped schedule's workgroup.  Items are ordered by row position, every
-// strip of a position before the next position; with a folded last strip
-// (fold > 1) its item for groups [f*fold, f*fold + fold) comes right after
-// the other strips of its last group.  slot() is an item's index in that
-// order and names its completion word.
-struct FlowOrder {
-  int nseg;  // groups per strip
-  int nn;    // strips with one group per item (all but a folded last strip)
-  int fold;  // groups per item of the folded last strip (1: none)
-  __host__ __device__ int start(int pos) const { return fold > 1 ? nn * pos + pos / fold : nn * pos; }
-  __host__ __device__ int items() const { return fold > 1 ? nn * nseg + (nseg + fold - 1) / fold : nn * nseg; }
-  __host__ __device__ int fold_pos(int f) const { return (f * fold + fold < nseg ? f * fold + fold : nseg) - 1; }
-  // Item slot of (strip, group); strip == nn is the folded strip.
-  __host__ __device__ int slot(int strip, int g) const {
-    return (fold > 1 && strip == nn) ? start(fold_pos(g / fold)) + nn : start(g) + strip;
-  }
-  // Position (row group) of slot s; *r = s - start(pos) (r == nn: the fold item).
-  __host__ __device__ int pos_of(int s, int* r) const {
-    int p = fold > 1 ? int((int64_t(s) * fold) / (int64_t(nn) * fold + 1)) : s / (nn > 0 ? nn : 1);
-    if (p > nseg - 1) p = nseg - 1;
-    while (p + 1 < nseg && start(p + 1) <= s) ++p;
-    while (p > 0 && start(p) > s) --p;
-    *r = s - start(p);
-    return p;
-  }
-};
-
-// Kernel argument of a flow launch.  `p` carries the tile geometry and the
-// group plan shared by every block (ncolw, nseg, grp_q, fold, wrap_w, ...);
-// the kernel derives each block's in/out, row range and balanced group sizes
-// from it.  Tickets come from a monotonic counter (this launch's first
-// ticket is `base`); completion words are per item slot and monotonic too
-// (block j publishes seq0 + j), so neither is cleared between launches.
-struct FlowParams {
-  LifeBlockParams p;     // block 0's plan (row_lo, seg_rows/rem of block 0)
-  uint8_t* buf[2];       // block j: buf[j & 1] -> buf[(j & 1) ^ 1]
-  uint32_t* changed0;    // flags of block 0's first generation (null: none)
-  uint32_t* done;        // completion word per item slot
-  uint32_t* counter;     // ticket counter
-  int64_t rows0;         // block 0's output rows
-  int64_t ring_rows;     // > 0: rows wrap modulo this (row ring: owned rows)
-  uint32_t seq0;
-  uint32_t base;
-  int shrink;            // rows per side each block's range shrinks by
-  int nblk;
-  int items;             // per block (FlowOrder::items)
-  int nn;                // FlowOrder::nn
-  int rotate;            // ring: block j starts at row position j (dependencies sit a block back)
-  int spin_log2;         // dependency wait bound (log2 of polls)
-  // Diagnostics (GOL_FLOW_TRACE): per item i (local ticket), {workgroup |
-  // XCC_ID << 32 | HW_ID << 40 (CU, SIMD bits), t_dequeued, t_ready (after
-  // the dependency wait), t_done} in s_memrealtime ticks (100 MHz).
-  uint64_t* trace;
-};
-
-// Backend-owned state of flow launches (HipBackend).
-struct FlowState {
-  uint32_t* counter = nullptr;  // one word, zeroed at allocation
-  uint32_t ticket = 0;          // counter value at the next launch
-  uint32_t* done = nullptr;
-  size_t done_words = 0;
-  uint32_t seq = 0;             // last published block sequence number
-  int64_t launches = 0, blocks = 0;
-  std::string last;             // description of the last flow launch (T, M, groups, grid)
-  uint64_t* trace = nullptr;    // GOL_FLOW_TRACE: the traced launch's records (FlowParams::trace)
-  int items = 0;                // items per block of the last launch
-};
 
 // Cross-lane primitive that moves the edge words between lanes.
 //   kXlaneAdd: no cross-lane data op at all.  The horizontal window is
@@ -174,13 +98,13 @@ struct FlowState {
 //   SALU (s_lshl_b64).  Each generation then stores cell x-1 at bit x, so the
 //   tile's storage frame drifts one cell to the right per generation; the
 //   engine tracks the drift and rotates it out before any read-out
-//   (Engine::normalize).  Measured (csrc/tools/ubench_dpp_mix.hip): any DPP,
+//   (Engine::normalize).  Measured (ubench_dpp_mix.hip, git e36884f): any DPP,
 //   v_alignbit or v_cmp in a v_bitop3 stream drops the SIMD from ~2.4 to
 //   ~4.5 cycles per instruction; add-with-carry ops do not.
 //   kXlaneAuto (default): the adder window where the engine allows a drift
 //   (HipBackend::choose_kernel: whole-width tiles that fill four waves per
 //   SIMD at T = 12), the DPP window everywhere else.
-enum Xlane : int { kXlaneAuto = -1, kXlaneDpp = 0, kXlaneBpermute = 1, kXlaneCarry = 2, kXlaneAdd = 3 };
+enum Xlane : int { kXlaneAuto = -1, kXlaneDpp = 0, kXlaneAdd = 3 };
 
 // Backend-owned state of linked launches (GOL_LINK; LifeBlockParams::link_*):
 // consecutive grouped launches of an epoch alternate between two streams and
@@ -226,8 +150,6 @@ struct LifeTuning {
   bool link_force = false;  // GOL_LINK_FORCE=1 (probe): the linked kernel even where two launches do not fit
   int target_waves = 0;     // waves per launch round (0 = occupancy x CUs x 4 SIMDs)
   int min_seg_rows = 16;    // lower bound on rows per wave segment
-  bool skew = false;        // software-pipelined (skewed) level schedule
-  int wpl_bits = 1;         // 32-cell words per lane, bit layout (1 or 2)
   int xlane = kXlaneAuto;   // cross-lane primitive
   bool u8_lds = false;      // byte layout: single-step LDS-tiled kernel (T = 1)
   int lds_rows = 32;        // rows per LDS tile (32 or 64)
@@ -235,11 +157,8 @@ struct LifeTuning {
   bool lds_pack = true;     // LDS-tiled byte kernel evaluates on bit words packed in LDS (T >= 8)
   bool lds_xcd = false;     // packed LDS tiles: XCD-aware workgroup order (column-major runs per XCD)
   int lds_waves = 0;        // packed LDS tiles: waves per workgroup (8, 16; 0 = by grid size)
-  int split = 0;            // split (trapezoid + inverted triangle) schedule: -1 auto, 0 off, 1 on
   int group = 8;            // grouped schedule, waves per workgroup sharing boundaries: 4, 8, -1 auto, 0 off
   int group_small = 4;      // the same for bit-layout blocks of T <= 8 (GOL_GROUP_SMALL; GOL_GROUP sets both)
-  int short_seg = 0;        // short-segment groups (life_short_impl.hpp): 0 off, 1 by the model, 2 forced
-  int pipe = 0;             // level-pipelined wave pairs (life_pipe_impl.hpp): 0 off, 1 by the model, 2 forced
   bool wrap = true;         // wrap mode on whole-width tiles (BlockArgs::full_width, lane_cols)
   bool fold = true;         // folded last strip in wrap mode (life_group_kernel)
   int chain = 0;            // chained groups (LifeBlockParams::chain_buf): 0 off, 1 on, 2 timing probe
@@ -254,125 +173,25 @@ struct LifeTuning {
   uint32_t* err = nullptr;       // LifeBlockParams::err (4 words: code, then a give-up's diagnostics)
   int chain_spin_log2 = 16;      // LifeBlockParams::chain_spin_log2
   bool chain_acquire = true;     // LifeBlockParams::chain_acquire (GOL_CHAIN_ACQUIRE)
-  // Flow launches (life_flow_impl.hpp): waves per item (4 or 8; 0 = by the
-  // planner) and groups per strip (0 = by the planner).
-  int flow_m = 0;
-  int flow_nseg = 0;
-  int flow_spin_log2 = 20;
   int fault_delay = 0;  // LifeBlockParams::fault_delay (GOL_FAULT_DELAY_SPINS)
-  // Device scratch of at least n bytes, valid until the next call (stream-ordered).
-  std::function<void*(size_t)> scratch;
 };
 
 // Returns the storage-frame drift of the launch in cells (T for the adder
 // window, 0 otherwise; BlockArgs::allow_drift).
 int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream);
-// A run of temporal blocks as one persistent dataflow launch
-// (life_flow_impl.hpp).  Returns the drift (nblk * T with the adder
-// window), or -1 when no flow plan fits (nothing launched: the caller runs
-// the blocks one by one).
-int launch_life_flow(const FlowArgs& a, const LifeTuning& tune, FlowState& st, hipStream_t stream);
-// Whether a flow kernel is compiled for T (bit layout, one word per lane).
-bool life_flow_has_T(int T);
-// Compiled flow windows (life_flow_*.hip): plan, launch, and the description
-// of the launch in *desc; false when no plan fits.
-#define GOL_FLOW_VARIANT(name)                                                                             \
-  bool name(const FlowParams& f, int64_t rows_min, int T, const LifeTuning& tune, hipStream_t s, std::string* desc, \
-            int64_t* tickets, int* items)
-#ifdef GOL_EXPERIMENTAL  // measured slower than the grouped launches (docs/PERFORMANCE.md)
-GOL_FLOW_VARIANT(launch_flow_bits_add);
-GOL_FLOW_VARIANT(launch_flow_bits_dpp);
-#endif
 // Description of the kernel variant the tuning selects for a layout.
 std::string life_block_variant(Layout layout, const LifeTuning& tune);
 // Largest T that keeps 2 waves/SIMD for the variant's words-per-lane.
 int life_block_max_T(Layout layout, const LifeTuning& tune);
 
-// Compiled variants (one translation unit each): bit layout with 1 or 2
-// words per lane and DPP / ds_bpermute / carry-chain lane shifts; byte
-// layout with 1.
+// Compiled variants (one translation unit each): the DPP and adder windows,
+// bit and byte layouts, one 32-cell word per lane.
 #define GOL_LIFE_VARIANT(name) \
   void name(const LifeBlockParams& p, int64_t out_rows, int T, const LifeTuning& tune, hipStream_t s)
 GOL_LIFE_VARIANT(launch_bits_w1_dpp);
 GOL_LIFE_VARIANT(launch_u8_w1_dpp);
 GOL_LIFE_VARIANT(launch_bits_w1_add);
 GOL_LIFE_VARIANT(launch_u8_w1_add);
-#ifdef GOL_EXPERIMENTAL  // measured slower (docs/PERFORMANCE.md); experimental builds only
-GOL_LIFE_VARIANT(launch_bits_w1_bperm);
-GOL_LIFE_VARIANT(launch_bits_w2_dpp);
-GOL_LIFE_VARIANT(launch_bits_w1_carry);
-GOL_LIFE_VARIANT(launch_bits_w2_carry);
-GOL_LIFE_VARIANT(launch_u8_w1_carry);
-#endif
-
-// Whether this build carries the measured-slower variants and schedules
-// (GOL_EXPERIMENTAL=1 native_build): resident epochs, split / skewed / short /
-// linked / bit-layout pipelined schedules, bpermute and carry-chain windows,
-// two words per lane.
-constexpr bool kExperimentalBuild =
-#ifdef GOL_EXPERIMENTAL
-    true;
-#else
-    false;
-#endif
-
-// ---- Resident epoch kernel (life_resident_impl.hpp) ------------------------
-// A whole temporal block of T generations (a full halo epoch) in ONE launch,
-// with the tile held in the register file: one 1024-thread workgroup per CU
-// owns a column strip (one wave64 wide: 63 owned words + the left halo lane
-// of the adder window) x a band of rows, 16 waves stacked down the band,
-// RW rows per wave in VGPRs.  Waves trade their edge rows through LDS every
-// generation; workgroups trade k halo rows and the halo lane's words through
-// a global mirror every k generations (sc1 stores, per-workgroup flags).
-// Bit layout, whole-width tiles, adder window (the frame drifts T cells).
-struct ResidentParams {
-  const uint8_t* in;
-  uint8_t* out;
-  uint8_t* mirror[2];     // exchange copies by refresh parity (tile geometry)
-  uint32_t* flags;        // per region: last refresh published (zeroed per launch)
-  uint32_t* changed;      // changed[t] <-> generation gen_base + 1 + t (after gen_dev)
-  const int64_t* gen_dev;
-  int64_t gen_rel;
-  uint32_t* err;          // device error word (4: a workgroup gave up waiting)
-  int64_t pitch;
-  int64_t row0;           // padded row of extended row 0 (= row_lo - T)
-  int ext_rows;           // row_hi - row_lo + 2T
-  int T, k;               // generations; refresh period = halo rows per band side (<= 16)
-  int ww, own_w0;         // owned words per row (wrap width), first owned word of a padded row
-  int ns, sw;             // column strips, owned words per strip
-  int nb, band_rows, band_rem;  // row bands per strip (balanced)
-  int nreg;               // ns * nb workgroups
-  int spin_log2;
-  int probe;              // timing probe: 1 = no refresh waits (wrong rows), 0 = exact
-  // Diagnostics (GOL_RES_TRACE): per region and refresh, s_memrealtime at the
-  // refresh's start, after its stores drained, after the neighbours' flags
-  // arrived and after its loads, then s_memtime (shader clock) at its start
-  // and after its loads: trace[(region * kResTraceRefreshes + m) * 6 + i].
-  uint64_t* trace;
-};
-constexpr int kResTraceRefreshes = 64;
-
-struct ResidentPlan {
-  int ns = 0, sw = 0, nb = 0, band_rows = 0, band_rem = 0, rw = 0, k = 0;
-  int64_t ext_rows = 0;
-};
-
-// Register rows per wave the resident kernel is compiled for (ascending).
-extern const int kResidentRW[];
-extern const int kResidentRWCount;
-constexpr int kResidentWaves = 16;
-// Bytes of one workgroup's exchange record in a resident mirror
-// (life_resident_impl.hpp kRecBytes): 2 x 16 rows of 64 words + 16 x 88 words.
-constexpr int kResidentRecBytes = 2 * 16 * 256 + 4 * kResidentWaves * 88;
-// Plan of a resident launch over a block (false: the tile does not fit the
-// register file at one workgroup per CU, or the block is not eligible).
-// k: refresh period / halo rows (<= 16); 0 = 8, deepened into the slack rows.
-bool plan_resident(const BlockArgs& a, int cus, int k, ResidentPlan* pl);
-// Enqueues the launch (flags zeroed first); returns the drift (T).
-int launch_life_resident(const BlockArgs& a, const ResidentPlan& pl, const LifeTuning& tune, uint8_t* mirror0,
-                         uint8_t* mirror1, uint32_t* flags, int probe, hipStream_t s, uint64_t* trace = nullptr);
-// Per-RW kernels (life_resident_rw*.hip).
-void launch_resident_rw(int rw, const ResidentParams& p, hipStream_t s);
 
 // Single-generation LDS-tiled byte-layout kernel (life_step_lds.hip).
 void launch_life_step_lds(const BlockArgs& a, int lds_rows, bool wrap, hipStream_t stream);

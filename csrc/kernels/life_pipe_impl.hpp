@@ -3,7 +3,7 @@
 //
 // A CDNA4 SIMD issues a wave's VALU instructions no faster than about one per
 // 5 cycles, while the SIMD as a whole takes one per ~2.45 cycles from 4
-// waves (csrc/tools/ubench_body.hip: a level body costs 96 / 51 / 49 / 42
+// waves (ubench_body.hip, git e36884f: a level body costs 96 / 51 / 49 / 42
 // cycles per SIMD at 1 / 2 / 3 / 4 resident waves).  The grouped kernel's
 // wave count is fixed by q >= 2T rows per wave, so the 8-GPU per-rank tile
 // (32768 x 4096) runs at 2-3 waves per SIMD.  Here wave pair m of a workgroup
@@ -184,7 +184,7 @@ __device__ __forceinline__ void zero_levels(Levels<T, W>& st) {
     for (int i = 0; i < W; ++i) {
 #pragma unroll
       for (int s = 0; s < 3; ++s) st.h0[L][s].w[i] = st.h1[L][s].w[i] = st.cc[L][s].w[i] = 0u;
-      st.pipe[L].w[i] = st.acc[L].w[i] = 0u;
+      st.acc[L].w[i] = 0u;
     }
 }
 

@@ -499,9 +499,9 @@ int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, int wave
   const int64_t wrap_h = wrap_w && a.wrap_rows ? g.H : 0;
   GOL_REQUIRE(!a.wrap_rows || wrap_h, "life_lds_bits: row wrap needs a whole-width tile without halo columns");
   GOL_REQUIRE(wrap_w || 32 * g.hw >= a.T, "life_lds_bits: a tile without column wrap needs T halo cells");
-  // The adder window where the engine allows a drifting frame (whole-width
-  // torus rows, read modulo the width); the DPP window elsewhere.
-  const bool add = a.allow_drift && wrap_w != 0;
+  // The DPP window: the packed tile's adder window (template ADD, a drifting
+  // frame on whole-width torus rows) measured 5 % slower and is not launched.
+  constexpr bool add = false;
   // Tiles as in launch_life_lds_multi: owned cells (wrap) or the padded row.
   const int64_t c_first = wrap_w ? g.cell0() : 0;
   const int64_t c_end = wrap_w ? g.cell0() + g.W : g.Wc();
@@ -518,13 +518,6 @@ int launch_life_lds_bits(const BlockArgs& a, bool wrap, bool xcd_order, int wave
                      const int64_t*, int64_t, int64_t, int64_t, int64_t, int64_t, int, int);
   const auto pick = [&](auto nw_c) -> K {
     constexpr int NW = decltype(nw_c)::value;
-#ifdef GOL_EXPERIMENTAL  // the adder window in the packed tile (GOL_LDS_ADD): exact, measured slower
-    if (add)
-      return a.T == 8 ? life_lds_bits_kernel<8, true, NW> : a.T == 16 ? life_lds_bits_kernel<16, true, NW>
-                                                                      : life_lds_bits_kernel<32, true, NW>;
-#else
-    GOL_REQUIRE(!add, "life_lds_bits: the adder window (GOL_LDS_ADD) needs an experimental build");
-#endif
     return a.T == 8 ? life_lds_bits_kernel<8, false, NW> : a.T == 16 ? life_lds_bits_kernel<16, false, NW>
                                                                      : life_lds_bits_kernel<32, false, NW>;
   };

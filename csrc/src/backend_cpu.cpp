@@ -96,16 +96,10 @@ class CpuBackend final : public Backend {
       : Backend(t),
         pool_(threads > 0 ? threads : t.i("host_threads") > 0 ? t.i("host_threads") : default_host_threads()),
         drift_(drift) {
-    resident_ = t.on("cpu_resident");
     const std::string& ring = t.s("cpu_ring");
     ring_ = !ring.empty() && ring != "0";
     ring_fail_ = ring == "fail";  // tests: the mapping fails after the size check
-    flow_ = t.on("cpu_flow");
   }
-  // Tuning cpu_flow=1: the engine hands runs of equal blocks to run_flow (the
-  // HIP backend's persistent dataflow launch); the base class runs them
-  // block by block, so the engine's flow bookkeeping is testable on the CPU.
-  bool has_flow(Layout, int T) const override { return flow_ && T >= 2; }
   ~CpuBackend() override {
     for (auto& kv : rings_) ::munmap(kv.first, kv.second);
   }
@@ -149,14 +143,7 @@ class CpuBackend final : public Backend {
     return va;  // memfd pages start zeroed
   }
   std::string name() const override {
-    return std::string(drift_ ? "cpu [drift]" : "cpu") + (resident_ ? " [resident]" : "");
-  }
-  // GOL_CPU_RESIDENT=1: the engine's resident-epoch schedule (one block of
-  // T = D per epoch) on the host, so that path is testable without a GPU;
-  // run_block evaluates any T.
-  int resident_epoch(Layout l, int64_t, int64_t, int D_req, bool multi) const override {
-    if (!resident_ || l != Layout::Bits) return 0;
-    return D_req > 16 ? D_req : multi ? 256 : 128;
+    return drift_ ? "cpu [drift]" : "cpu";
   }
   bool drifts(Layout) const override { return drift_; }
   void rotate_cols(const void* src, void* dst, const TileGeom& g, int64_t shift) override;
@@ -235,10 +222,8 @@ class CpuBackend final : public Backend {
   }
   ThreadPool pool_;
   bool drift_ = false;
-  bool resident_ = false;  // GOL_CPU_RESIDENT
   bool ring_ = false;      // GOL_CPU_RING
   bool ring_fail_ = false;  // GOL_CPU_RING=fail
-  bool flow_ = false;       // GOL_CPU_FLOW
   std::mutex ring_mu_;
   std::map<void*, size_t> rings_;  // row rings: base -> mapped bytes
 };

@@ -35,25 +35,9 @@ namespace {
   DeviceScope device_scope_(dev_);   \
   if (check_dev_) assert_current(__func__)
 
-// Live HIP backends per device in this process: resident epochs need every
-// CU of the device for one launch, so they are off when ranks share a GPU.
-std::mutex& live_mu() {
-  static std::mutex m;
-  return m;
-}
-std::map<int, int>& live_backends() {
-  static std::map<int, int> n;
-  return n;
-}
-
 class HipBackend final : public Backend {
  public:
   HipBackend(int device, const Tuning& t) : Backend(t), dev_(device) {
-    t.require_build(hipk::kExperimentalBuild);
-    {
-      std::lock_guard<std::mutex> lk(live_mu());
-      ++live_backends()[device];
-    }
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
     GOL_REQUIRE(n > 0, "no HIP device available");
@@ -75,9 +59,9 @@ class HipBackend final : public Backend {
     tune_.cus = cus_;
     tune_.target_waves = t.i("target_waves");
     tune_.min_seg_rows = t.i("min_seg_rows");
-    tune_.skew = t.on("skew");
-    tune_.wpl_bits = t.i("wpl");
     tune_.xlane = t.i("xlane");
+    GOL_REQUIRE(tune_.xlane == hipk::kXlaneAuto || tune_.xlane == hipk::kXlaneDpp || tune_.xlane == hipk::kXlaneAdd,
+                "tuning xlane: -1 (auto), 0 (DPP window) or 3 (adder window)");
     tune_.u8_lds = t.s("u8_kernel") == "lds";
     GOL_REQUIRE(tune_.u8_lds || t.s("u8_kernel") == "auto", "tuning u8_kernel: auto or lds");
     tune_.lds_rows = t.i("lds_rows");
@@ -85,30 +69,16 @@ class HipBackend final : public Backend {
     tune_.lds_xcd = t.on("lds_xcd");
     tune_.lds_waves = t.i("lds_waves");
     GOL_REQUIRE(tune_.lds_waves == 0 || tune_.lds_waves == 8 || tune_.lds_waves == 16, "tuning lds_waves: 0, 8 or 16");
-    lds_add_ = t.on("lds_add");  // packed LDS tile: adder window (drifting frame)
     // 8192^2 per generation: bytes T = 1 26.6, 2 24.9, 4 20.4, 8 17.9 us; packed T = 8 6.5, 16 4.9, 32 4.7
     tune_.lds_T = t.i("lds_t") > 0 ? t.i("lds_t") : tune_.lds_pack ? 32 : 8;
     GOL_REQUIRE(tune_.lds_T == 1 || tune_.lds_T == 2 || tune_.lds_T == 4 || tune_.lds_T == 8 ||
                     (tune_.lds_pack && (tune_.lds_T == 16 || tune_.lds_T == 32)),
                 "tuning lds_t must be 1, 2, 4 or 8 (16 or 32 with the packed tile, lds_pack=1)");
-    tune_.split = t.i("split");  // measured slower so far (profiles/)
     tune_.group = t.i("group");  // grouped schedule (life_group_impl.hpp)
     tune_.group_small = !t.is_default("group") && t.is_default("group_small") ? tune_.group : t.i("group_small");
-    // Short-segment groups (life_short_impl.hpp): exact, but 10-20 % slower
-    // than the grouped kernel on the per-rank tile (profiles/sweep_short_segments.jsonl).
-    tune_.short_seg = t.i("short");
-    tune_.pipe = t.i("pipe");
     tune_.wrap = t.on("wrap");
     tune_.fold = t.on("fold");
     chain_mode_ = t.i("chain");
-    // Resident epochs (life_resident_impl.hpp): resident -1 auto, 0 off, 1 on
-    // where the tile fits; res_k refresh period / halo rows (<= 16); res_d
-    // epoch depth; res_probe=1 timing probe without refreshes.
-    resident_mode_ = t.i("resident");
-    resident_k_ = std::min(16, std::max(0, t.i("res_k")));  // 0: as deep as the band's slack allows
-    resident_D_ = t.i("res_d");
-    resident_probe_ = t.i("res_probe");
-    split_trace(t.s("res_trace"), &res_trace_at_, &res_trace_path_);
     u8_pipe_ = t.on("u8_pipe");
     // Linked launches: consecutive grouped launches of an epoch overlap on
     // two streams, ordered by per-group completion words (LifeBlockParams::
@@ -134,21 +104,12 @@ class HipBackend final : public Backend {
       link_on_ = false;
     }
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
-    // Persistent dataflow launches (life_flow_impl.hpp, experimental builds):
-    // flow_m / flow_nseg pin the planner's waves per item and groups per
-    // strip (sweeps).
-    flow_on_ = t.on("flow");
-    tune_.flow_m = t.i("flow_m");
-    tune_.flow_nseg = t.i("flow_nseg");
-    tune_.flow_spin_log2 = std::min(26, std::max(8, t.i("flow_spin")));
     tune_.fault_delay = std::max(0, std::min(4096, t.i("fault_delay_spins")));
-    split_trace(t.s("flow_trace"), &flow_trace_at_, &flow_trace_path_);
     tune_log_ = t.on("tune_log");
     tune_.chain_seq = &chain_seq_;
-    // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words,
-    // 5..7 resident mirrors and flags, 8 flow completion words, 9 the flow
-    // ticket counter (zeroed when allocated: flags and words are compared with
-    // sequence numbers).
+    // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words
+    // (zeroed when allocated: flags and words are compared with sequence
+    // numbers).
     tune_.chain_mem = [this](int which, size_t n) -> uint32_t* {
       void*& buf = chain_[which];
       size_t& cap = chain_bytes_[which];
@@ -179,23 +140,8 @@ class HipBackend final : public Backend {
     tune_.chain_spin_log2 = std::min(24, std::max(4, t.i("chain_spin")));
     tune_.chain_acquire = t.on("chain_acquire");
     HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&tune_.err), err_host_, 0));
-    tune_.scratch = [this](size_t n) -> void* {
-      if (n > scratch_bytes_) {
-        GOL_ON_DEVICE();
-        HIP_CHECK(hipStreamSynchronize(stream_));  // earlier kernels may still use it
-        if (scratch_) HIP_CHECK(hipFree(scratch_));
-        HIP_CHECK(hipMalloc(&scratch_, n));
-        scratch_bytes_ = n;
-      }
-      if (check_dev_) check_ptr(scratch_, "scratch");
-      return scratch_;
-    };
   }
   ~HipBackend() override {
-    {
-      std::lock_guard<std::mutex> lk(live_mu());
-      --live_backends()[dev_];
-    }
     if (prof_on_ && prof_n_ > 0)
       std::fprintf(stderr, "gol host profile: %lld blocks; per block: engine between blocks %.2f us, run_block %.2f us "
                    "(launch call %.2f us)\n", (long long)prof_n_, prof_gap_ / double(std::max<int64_t>(1, prof_n_ - 1)),
@@ -208,7 +154,6 @@ class HipBackend final : public Backend {
     if (comm_) hipStreamSynchronize(comm_);
     for (auto& kv : rings_) release_ring(kv.second);
     if (stage_) hipFree(stage_);
-    if (scratch_) hipFree(scratch_);
     for (void* c : chain_)
       if (c) hipFree(c);
     for (auto& p : pending_) {
@@ -239,66 +184,11 @@ class HipBackend final : public Backend {
     }
   }
   int64_t linked_launches() const override { return link_.linked; }
-  bool has_flow(Layout l, int T) const override {
-    return flow_on_ && l == Layout::Bits && tune_.wpl_bits < 2 && hipk::life_flow_has_T(T);
-  }
-  std::string flow_desc() const override { return flow_.last; }
-  // One flow launch on the compute stream (never inside a capture: its
-  // tickets and sequence numbers are per launch); falls back to the blocks
-  // one by one when no flow plan fits the rows.
-  int run_flow(const FlowArgs& f) override {
-    GOL_ON_DEVICE();
-    join_streams();
-    const bool capturing = capturing_;  // capture_begin / capture_end (no query per launch)
-    if (capturing) return Backend::run_flow(f);
-    if (check_dev_) {
-      check_ptr(f.buf[0], "run_flow buffer 0");
-      check_ptr(f.buf[1], "run_flow buffer 1");
-    }
-    // GOL_FLOW_TRACE=<flow launch>:<csv>: per-item timestamps of one launch
-    // (scripts/flow_trace.py: waits, item durations, concurrency).
-    const bool traced = flow_trace_at_ >= 0 && flow_.launches == flow_trace_at_;
-    size_t tbytes = 0;
-    if (traced) {
-      HIP_CHECK(hipStreamSynchronize(stream_));
-      tbytes = size_t(f.nblk) * size_t(f.g.Wp() / 62 + 2) * size_t((f.row_hi - f.row_lo) / (2 * f.T) + 1) * 32;  // >= items x 32 B
-      HIP_CHECK(hipMalloc(&flow_.trace, tbytes));
-      HIP_CHECK(hipMemsetAsync(flow_.trace, 0, tbytes, stream_));
-    }
-    const int drift = hipk::launch_life_flow(f, tune_, flow_, stream_);
-    HIP_CHECK(hipGetLastError());
-    if (traced) {
-      std::vector<uint64_t> h(tbytes / 8);
-      HIP_CHECK(hipMemcpyAsync(h.data(), flow_.trace, tbytes, hipMemcpyDeviceToHost, stream_));
-      HIP_CHECK(hipStreamSynchronize(stream_));
-      HIP_CHECK(hipFree(flow_.trace));
-      flow_.trace = nullptr;
-      std::FILE* fp = std::fopen(flow_trace_path_.c_str(), "w");
-      GOL_REQUIRE(fp != nullptr, "GOL_FLOW_TRACE: cannot open " + flow_trace_path_);
-      std::fprintf(fp, "# %s\nitem,block,slot,wg,xcc,hw_id,t_deq,t_ready,t_done\n", flow_.last.c_str());
-      const int64_t n = drift >= 0 ? int64_t(f.nblk) * flow_.items : 0;
-      for (int64_t i = 0; i < n && 4 * i + 3 < int64_t(h.size()); ++i) {
-        const uint64_t* r = &h[size_t(4 * i)];
-        if (!r[3]) continue;
-        std::fprintf(fp, "%lld,%lld,%lld,%llu,%llu,%llu,%llu,%llu,%llu\n", (long long)i, (long long)(i / flow_.items),
-                     (long long)(i % flow_.items), (unsigned long long)(r[0] & 0xFFFFFFFFull),
-                     (unsigned long long)((r[0] >> 32) & 0xFF), (unsigned long long)(r[0] >> 40),
-                     (unsigned long long)r[1], (unsigned long long)r[2], (unsigned long long)r[3]);
-      }
-      std::fclose(fp);
-    }
-    if (drift < 0) return Backend::run_flow(f);
-    launches_ += 1;
-    return drift;
-  }
   std::string name() const override {
     hipk::LifeTuning t = tune_;
     t.chain = chain_mode_;
     return "hip:" + std::to_string(dev_) + ":" + arch_ + cu_part_ + " [" + hipk::life_block_variant(Layout::Bits, t) +
-           "; " + hipk::life_block_variant(Layout::U8, t) + "]" +
-           (resident_mode_ ? " resident=" + std::string(resident_mode_ < 0 ? "auto" : "on") + " k=" +
-                                 std::to_string(resident_k_)
-                           : "");
+           "; " + hipk::life_block_variant(Layout::U8, t) + "]";
   }
   int preferred_tmax(Layout l) const override { return hipk::life_block_max_T(l, tune_); }
   bool is_device() const override { return true; }
@@ -570,7 +460,7 @@ class HipBackend final : public Backend {
     }
     HIP_CHECK(e);
   }
-  bool supports_graphs() const override { return tune_.split == 0; }  // split allocates scratch lazily
+  bool supports_graphs() const override { return true; }
   void capture_begin() override {
     join_streams();
     GOL_ON_DEVICE();
@@ -677,56 +567,6 @@ class HipBackend final : public Backend {
     if (chain_mode_) {  // chained groups: own stream only, never inside a graph capture
       tune_.chain_ok = (!a.stream || a.stream == stream_) && !capturing && !linkable;
     }
-    if (a.resident) {  // the engine runs this epoch as one resident launch
-#ifndef GOL_EXPERIMENTAL
-      fail("resident epochs need an experimental build (GOL_EXPERIMENTAL=1)");
-#else
-      join_streams();
-      ++launches_;
-      hipk::ResidentPlan pl;
-      GOL_REQUIRE(hipk::plan_resident(a, cus_, resident_k_, &pl),
-                  "resident kernel: block of " + std::to_string(a.row_hi - a.row_lo) + " rows x T = " +
-                      std::to_string(a.T) + " does not fit (Backend::resident_epoch)");
-      reserve_resident(a.g);
-      const size_t mb = size_t(cus_) * hipk::kResidentRecBytes;
-      auto* m0 = reinterpret_cast<uint8_t*>(tune_.chain_mem(5, mb));
-      auto* m1 = reinterpret_cast<uint8_t*>(tune_.chain_mem(6, mb));
-      uint32_t* fl = tune_.chain_mem(7, size_t(pl.ns) * pl.nb * 4);
-      hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
-      // GOL_RES_TRACE=<resident launch>:<csv>: refresh phase timestamps of one launch.
-      const bool traced = res_trace_at_ >= 0 && resident_launches_ == res_trace_at_;
-      ++resident_launches_;
-      uint64_t* tr = nullptr;
-      const size_t tbytes = size_t(pl.ns) * pl.nb * hipk::kResTraceRefreshes * 6 * sizeof(uint64_t);
-      if (traced) {
-        HIP_CHECK(hipStreamSynchronize(s));
-        HIP_CHECK(hipMalloc(&tr, tbytes));
-        HIP_CHECK(hipMemsetAsync(tr, 0, tbytes, s));
-      }
-      const int drift = hipk::launch_life_resident(a, pl, tune_, m0, m1, fl, resident_probe_, s, tr);
-      HIP_CHECK(hipGetLastError());
-      if (traced) {
-        std::vector<uint64_t> h(tbytes / sizeof(uint64_t));
-        HIP_CHECK(hipMemcpyAsync(h.data(), tr, tbytes, hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-        HIP_CHECK(hipFree(tr));
-        std::FILE* f = std::fopen(res_trace_path_.c_str(), "w");
-        GOL_REQUIRE(f != nullptr, "GOL_RES_TRACE: cannot open " + res_trace_path_);
-        std::fprintf(f, "region,strip,band,refresh,t_start,t_stored,t_flags,t_loaded,clk_start,clk_loaded,k,rw,T\n");
-        for (int r = 0; r < pl.ns * pl.nb; ++r)
-          for (int m = 0; m < hipk::kResTraceRefreshes; ++m) {  // m = 0: kernel start / loaded / loop end / end
-            const uint64_t* q = &h[size_t((int64_t(r) * hipk::kResTraceRefreshes + m) * 6)];
-            if (!q[0]) continue;
-            std::fprintf(f, "%d,%d,%d,%d,%llu,%llu,%llu,%llu,%llu,%llu,%d,%d,%d\n", r, r / pl.nb, r % pl.nb, m,
-                         (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[2],
-                         (unsigned long long)q[3], (unsigned long long)q[4], (unsigned long long)q[5], pl.k, pl.rw,
-                         a.T);
-          }
-        std::fclose(f);
-      }
-      return drift;
-#endif  // GOL_EXPERIMENTAL
-    }
     if (trace_at_ >= 0 && trace_pair_ && (launches_ == trace_at_ || launches_ == trace_at_ + 1))
       return run_block_traced_pair(a, linkable);
     if (trace_at_ >= 0 && launches_ == trace_at_) {
@@ -826,10 +666,8 @@ class HipBackend final : public Backend {
     return e;
   }
   bool drifts(Layout l) const override {
-    if (l == Layout::U8 && tune_.u8_lds)  // the packed LDS tile (adder window), not the byte kernels
-      return lds_add_ && tune_.lds_pack && tune_.lds_T >= 8 &&
-             (tune_.xlane == hipk::kXlaneAuto || tune_.xlane == hipk::kXlaneAdd);
-    return tune_.xlane == hipk::kXlaneAdd && (l == Layout::Bits ? tune_.wpl_bits < 2 : true);
+    if (l == Layout::U8 && tune_.u8_lds) return false;  // the LDS-tiled byte kernels run the DPP window
+    return tune_.xlane == hipk::kXlaneAdd;
   }
   // The adder window (kXlaneAdd) beats the DPP window only at four resident
   // waves per SIMD; its grouped kernel fits that at T = 12 (120 VGPRs) with
@@ -870,17 +708,11 @@ class HipBackend final : public Backend {
             break;
           }
     }
-    const bool one_word = l == Layout::U8 || tune_.wpl_bits < 2;
-    // The packed LDS-tiled byte kernel runs the adder window (drifting frame)
-    // wherever the engine allows it (whole-width torus rows).
-    if (l == Layout::U8 && tune_.u8_lds && lds_add_ && tune_.lds_pack && k.tmax >= 8 &&
-        (tune_.xlane == hipk::kXlaneAuto || tune_.xlane == hipk::kXlaneAdd))
-      k.drift = true;
-    if (tune_.xlane == hipk::kXlaneAdd && one_word && !(l == Layout::U8 && tune_.u8_lds)) {
+    if (tune_.xlane == hipk::kXlaneAdd && !(l == Layout::U8 && tune_.u8_lds)) {
       k.drift = true;
       if (tmax_req <= 0) k.tmax = 12;
-    } else if (tune_.xlane == hipk::kXlaneAuto && l == Layout::Bits && one_word && !tune_.skew &&
-               tune_.split == 0 && tune_.group != 0 && (tmax_req <= 0 || tmax_req == 12)) {
+    } else if (tune_.xlane == hipk::kXlaneAuto && l == Layout::Bits && tune_.group != 0 &&
+               (tmax_req <= 0 || tmax_req == 12)) {
       constexpr int64_t kT = 12;
       const int64_t strips = ceil_div(ceil_div(cols, 32) + 16, 63);  // + a deep halo's words
       if (strips * (rows / (2 * kT)) >= int64_t(16) * cus_) k = {int(kT), true};
@@ -891,7 +723,7 @@ class HipBackend final : public Backend {
     // per SIMD; T = 12 2.48-2.50; T = 8 2.05-2.08, 2 waves; T = 4 2.97 (twice
     // the launches); the 8-GPU rank tile 32768 x 4096 keeps T = 16 at 2 waves;
     // profiles/r04/small_grid_T_sweep.jsonl).
-    if (!k.drift && tmax_req <= 0 && l == Layout::Bits && one_word && tune_.group != 0 && k.tmax == 16) {
+    if (!k.drift && tmax_req <= 0 && l == Layout::Bits && tune_.group != 0 && k.tmax == 16) {
       const int64_t strips = ceil_div(ceil_div(cols, 32) + 16, 63);
       for (int t : {16, 12, 8}) {
         k.tmax = t;
@@ -907,45 +739,6 @@ class HipBackend final : public Backend {
       k.link = strips * (rows / (2 * k.tmax)) >= int64_t(6) * cus_;
     }
     return k;
-  }
-  // Resident epochs: on when forced (GOL_RESIDENT=1) and the plan fits;
-  // auto (-1) also needs the tile to leave the grouped kernel short of four
-  // waves per SIMD (the adder window's occupancy), where the resident launch
-  // measured faster (docs/HISTORY.md, "Resident epochs").
-  int resident_epoch(Layout l, int64_t rows, int64_t cols, int D_req, bool multi) const override {
-#ifndef GOL_EXPERIMENTAL
-    (void)l, (void)rows, (void)cols, (void)D_req, (void)multi;
-    return 0;
-#else
-    if (resident_mode_ == 0 || l != Layout::Bits || !tune_.wrap || cols % 32 != 0 || tune_.wpl_bits >= 2) return 0;
-    {
-      std::lock_guard<std::mutex> lk(live_mu());
-      if (live_backends()[dev_] > 1) return 0;  // ranks share this GPU: a launch may not get every CU
-    }
-    if (tune_.xlane != hipk::kXlaneAuto && tune_.xlane != hipk::kXlaneAdd) return 0;
-    const int D = D_req > 0 ? D_req : resident_D_ > 0 ? resident_D_ : multi ? 256 : 128;
-    if (D <= 16) return 0;
-    BlockArgs a;
-    a.g = TileGeom::make(Layout::Bits, rows, cols, D, 0);
-    a.row_lo = D;
-    a.row_hi = D + rows;
-    a.T = D;
-    a.full_width = a.allow_drift = true;
-    hipk::ResidentPlan pl;
-    if (!hipk::plan_resident(a, cus_, resident_k_, &pl)) return 0;
-    if (resident_mode_ < 0) {
-      const int64_t strips = ceil_div(ceil_div(cols, int64_t(32)) + 16, int64_t(63));
-      if (strips * (rows / 24) >= int64_t(16) * cus_) return 0;  // the grouped adder kernel fills 4 waves/SIMD
-    }
-    return D;
-#endif
-  }
-  void reserve_resident(const TileGeom& /*g*/) override {
-    if (!hipk::kExperimentalBuild) return;
-    const size_t mb = size_t(cus_) * hipk::kResidentRecBytes;  // one exchange record per workgroup
-    tune_.chain_mem(5, mb);
-    tune_.chain_mem(6, mb);
-    tune_.chain_mem(7, size_t(cus_) * 4);
   }
   int64_t min_block_rows(Layout l, int T) const override {
     return l == Layout::U8 && T > 32 ? int64_t(4) * (2 * T + 2) + T - 1 : 1;
@@ -1055,13 +848,9 @@ class HipBackend final : public Backend {
                                             std::to_string(err_host_[2]) + "]"
                                       : "";
       fail(std::string(e == 2   ? "life_group kernel (chained groups): a wave gave up waiting for the group below" + diag
-                       : e == 4 ? "life_resident kernel: a workgroup gave up waiting for its neighbours' halo rows "
-                                  "(not every workgroup was resident: another kernel on this GPU?)"
-                       : e == 5 ? "life_resident kernel: a wave gave up waiting for its neighbours' edge rows"
                        : e == 3 ? "life_group kernel (linked launches): a group gave up waiting for the previous "
                                   "launch's rows"
-                       : e == 6 ? "life_flow kernel: an item gave up waiting for the items of the block before it"
-                                : "life_short kernel: a wave gave up waiting for its neighbour's LDS rows") +
+                                : "life_block kernel: unknown device error") +
            " (device error word " + std::to_string(e) + "); the rows of that launch are invalid");
     }
   }
@@ -1203,25 +992,14 @@ class HipBackend final : public Backend {
   std::string cu_part_;    // GOL_CU_PARTITION, for name()
   hipk::LifeTuning tune_;
   hipStream_t comm_ = nullptr;
-  void* scratch_ = nullptr;  // split-schedule boundary states
-  size_t scratch_bytes_ = 0;
-  // chain_mem: chained groups' flags, slots; linked launches' 3 x completion
-  // words; resident epochs' two mirrors and per-workgroup flags (5..7).
-  void* chain_[10] = {};
-  size_t chain_bytes_[10] = {};
-  int resident_mode_ = 0, resident_k_ = 8, resident_D_ = 0, resident_probe_ = 0;
-  bool lds_add_ = false;  // GOL_LDS_ADD
-  int64_t resident_launches_ = 0, res_trace_at_ = -1;
-  std::string res_trace_path_;
+  // chain_mem: chained groups' flags, slots; linked launches' 3 x completion words.
+  void* chain_[5] = {};
+  size_t chain_bytes_[5] = {};
   hipk::LinkState link_;  // linked launches (GOL_LINK)
-  hipk::FlowState flow_;  // flow launches: ticket counter, completion words (chain_mem 8, 9)
-  bool flow_on_ = true;   // GOL_FLOW
-  int64_t flow_trace_at_ = -1;  // GOL_FLOW_TRACE
-  std::string flow_trace_path_;
   bool link_on_ = false;  // every eligible launch (GOL_LINK=1)
   int link_mode_ = -1;
   uint32_t chain_seq_ = 0;
-  bool u8_pipe_ = true;  // GOL_U8_PIPE: T = 48 / 64 byte passes
+  bool u8_pipe_ = true;  // GOL_U8_PIPE: T = 48 byte passes
   int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, 2 timing probe, -1 autotuned per launch shape
   bool tune_log_ = false;
   std::map<TuneKey, TuneStats> tuned_;
@@ -1247,8 +1025,6 @@ class HipBackend final : public Backend {
 };
 
 }  // namespace
-
-bool experimental_build() { return hipk::kExperimentalBuild; }
 
 bool hip_available() {
   int n = 0;

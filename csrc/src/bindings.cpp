@@ -134,7 +134,6 @@ PYBIND11_MODULE(_gol, m) {
       .def("values", &Tuning::values)
       .def("changed", &Tuning::changed)
       .def("summary", &Tuning::summary)
-      .def("require_build", &Tuning::require_build)
       .def("copy", [](const Tuning& t) { return Tuning(t); });
   m.def("tuning_keys", []() {
     py::list out;
@@ -154,7 +153,6 @@ PYBIND11_MODULE(_gol, m) {
   py::class_<Backend, std::shared_ptr<Backend>>(m, "Backend")
       .def("name", &Backend::name)
       .def("tuning", &Backend::tuning, py::return_value_policy::copy)
-      .def("flow_desc", &Backend::flow_desc)
       .def("is_device", &Backend::is_device)
       .def("device", &Backend::device)
       .def("stream", [](const Backend& b) { return reinterpret_cast<std::uintptr_t>(b.stream()); })
@@ -174,7 +172,6 @@ PYBIND11_MODULE(_gol, m) {
   m.def("hip_pci_bus_id", &hip_pci_bus_id);
   m.def("hip_release_errors", &hip_release_errors);
   m.def("hip_uuid", &hip_uuid);
-  m.def("experimental_build", &experimental_build);
 
   py::class_<Transport, std::shared_ptr<Transport>>(m, "Transport")
       .def("rank", &Transport::rank)
@@ -249,7 +246,6 @@ PYBIND11_MODULE(_gol, m) {
       .def_readwrite("timing_barriers", &EngineConfig::timing_barriers)
       .def_readwrite("self_exchange", &EngineConfig::self_exchange)
       .def_readwrite("u8_compute", &EngineConfig::u8_compute)
-      .def_readwrite("flow", &EngineConfig::flow)
       .def_readwrite("graphs", &EngineConfig::graphs)
       .def_readwrite("watchdog_s", &EngineConfig::watchdog_s)
       .def_readwrite("tune", &EngineConfig::tune);
@@ -268,8 +264,6 @@ PYBIND11_MODULE(_gol, m) {
       .def_readonly("graph_launches", &RunResult::graph_launches)
       .def_readonly("halo_bytes", &RunResult::halo_bytes)
       .def_readonly("linked_launches", &RunResult::linked_launches)
-      .def_readonly("flow_launches", &RunResult::flow_launches)
-      .def_readonly("flow_blocks", &RunResult::flow_blocks)
       .def_readonly("phase_timed", &RunResult::phase_timed)
       .def_readonly("compute_ms", &RunResult::compute_ms)
       .def_readonly("halo_ms", &RunResult::halo_ms)
@@ -290,8 +284,6 @@ PYBIND11_MODULE(_gol, m) {
         d["graph_launches"] = r.graph_launches;
         d["halo_bytes"] = r.halo_bytes;
         d["linked_launches"] = r.linked_launches;
-        d["flow_launches"] = r.flow_launches;
-        d["flow_blocks"] = r.flow_blocks;
         d["phase_timed"] = r.phase_timed;
         d["compute_ms"] = r.compute_ms;
         d["halo_ms"] = r.halo_ms;
@@ -324,9 +316,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("drift", &Engine::drift)
       .def_property_readonly("drifting", &Engine::drifting)
       .def_property_readonly("row_ring", &Engine::row_ring)
-      .def_property_readonly("flow", &Engine::flow)
       .def_property_readonly("via_bits", &Engine::via_bits)
-      .def_property_readonly("resident", &Engine::resident)
       .def("normalize", &Engine::normalize, py::call_guard<py::gil_scoped_release>())
       .def("current_buffer", [](Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })
       .def("load_cells",

@@ -30,27 +30,6 @@ int64_t min_tile_rows(const Decomposition& d) { return d.H / d.Py; }
 int64_t min_tile_cols(const Decomposition& d) { return (d.W / d.col_unit / d.Px) * d.col_unit; }
 }  // namespace
 
-// Default flow: the blocks one by one (Backend::run_flow).
-int Backend::run_flow(const FlowArgs& f) {
-  int64_t drift = 0;
-  for (int j = 0; j < f.nblk; ++j) {
-    BlockArgs a;
-    a.in = f.buf[j & 1];
-    a.out = f.buf[(j & 1) ^ 1];
-    a.g = f.g;
-    a.row_lo = f.row_lo + int64_t(j) * f.shrink;
-    a.row_hi = f.row_hi - int64_t(j) * f.shrink;
-    a.T = f.T;
-    a.gen_base = f.gen_base + int64_t(j) * f.T;
-    a.changed = f.changed;
-    a.flags_base = f.flags_base;
-    a.allow_drift = f.allow_drift;
-    a.full_width = f.full_width;
-    drift += run_block(a);
-  }
-  return int(drift % std::max<int64_t>(1, f.g.W));
-}
-
 Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     : cfg_(cfg), be_(backend), tr_(transport) {
   GOL_REQUIRE(be_ && tr_, "engine needs a backend and a transport");
@@ -106,29 +85,16 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     if (row_exchange && h >= 2 * int64_t(D_) + 1) min_rows = std::min({h, int64_t(D_), h - 2 * int64_t(D_)});
     while (tmax_ > 1 && be_->min_block_rows(cl, tmax_) > min_rows) tmax_ = pick_T(tmax_ - 1);
   }
-  // Resident epochs (Backend::resident_epoch): a whole-width bit tile small
-  // enough for the register file runs each epoch as one launch (no T <= 16
-  // blocks, no segment triangles); the same decision on every rank (smallest
-  // tile).  Not with the overlapped schedules, which split epochs into blocks.
-  if (cl == Layout::Bits && dec_.Px == 1 && cfg_.W % 32 == 0 && cfg_.overlap != 1 && cfg_.overlap != 2) {
-    const int Dr = be_->resident_epoch(cl, ceil_div(dec_.H, int64_t(dec_.Py)), cfg_.W, cfg_.epoch, row_exchange);
-    if (Dr > 16 && (dec_.Py == 1 || Dr <= min_tile_rows(dec_))) {
-      resident_ = true;
-      D_ = Dr;
-      tmax_ = Dr;
-    }
-  }
   // A drifting kernel (one-sided window, Backend::drifts) consumes 2 cells of
   // left halo per generation and none on the right; it needs the tile to be
   // the whole torus width so that the drift is a relabeling of columns.
-  drift_ok_ = (kc.drift || resident_) && dec_.Px == 1 && cfg_.W % 32 == 0;  // resident: adder window
+  drift_ok_ = kc.drift && dec_.Px == 1 && cfg_.W % 32 == 0;
   // Whole-width tiles on a backend that wraps column reads (lane_cols in the
   // HIP kernels) never read their halo columns: no column fills.
   cols_filled_ = !(dec_.Px == 1 && cfg_.W % 32 == 0 && be_->wraps_columns(cl));
   // A single-rank torus on a backend that also wraps row reads (the LDS-tiled
   // byte kernels): one block per epoch over the owned rows, no fills at all.
-  rows_wrapped_ = !cols_filled_ && dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !resident_ &&
-                  be_->wraps_rows(cl);
+  rows_wrapped_ = !cols_filled_ && dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && be_->wraps_rows(cl);
   if (rows_wrapped_) D_ = tmax_;  // one block per epoch; nothing to fill or exchange
   // Halo columns: none when the kernels wrap (smaller rows to exchange and
   // fill); else D cells per side, 2D on the left for the drifting window.
@@ -143,8 +109,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // falls back to plain buffers with periodic fills.
   int ring_dv = 0;
   void* ring_bufs[2] = {nullptr, nullptr};
-  if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !rows_wrapped_ && !resident_ &&
-      cfg_.tune.i("pitch_pad") == 0) {
+  if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !rows_wrapped_ && cfg_.tune.i("pitch_pad") == 0) {
     const TileGeom probe = TileGeom::make(cl, r.size(), c.size(), 0, hw);
     ring_dv = be_->row_ring_halo(probe.H, probe.pitch, tmax_);
     // The byte layout on bit words keeps its byte tiles too: the rings must
@@ -194,19 +159,6 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // (latency-bound), so poll half as often; a stop is still exact and at most
   // two windows late.
   poll_gens_ = cfg_.poll_gens > 0 ? cfg_.poll_gens : (tr_->size() > 1 || cfg_.self_exchange) ? 512 : 256;
-  // Flow launches (EngineConfig::flow): runs of equal blocks as one
-  // persistent launch, where the backend has the kernel for the layout and T.
-  // Not for the resident and LDS-tiled schedules (their own launches).  A
-  // ring's epoch then only paces the polls (one flow launch per poll window)
-  // and the column fills, if any: the column halos hold 32 hw cells of light
-  // cone (half with a drifting frame).
-  flow_ = cfg_.flow != 0 && be_->has_flow(cl, tmax_) && !resident_ && !rows_wrapped_;
-  if (flow_ && rows_ring_ && cfg_.epoch <= 0) {
-    int64_t cap = poll_gens_;
-    if (cols_filled_) cap = std::min<int64_t>(cap, 32 * int64_t(hw) / (drift_ok_ ? 2 : 1));
-    D_ = tmax_ * int(std::max<int64_t>(1, cap / tmax_));
-  }
-
   if (rows_ring_ && !via_bits_) {
     for (int i = 0; i < 2; ++i) buf_[i] = ring_bufs[i];
   } else {
@@ -233,8 +185,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // epoch), which on the 32768 x 4096 per-rank tile cost 4x more than the
   // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
   const bool interior = min_tile_rows(dec_) >= 2 * int64_t(D_) + 1;  // on every rank
-  overlap_ = row_exchange && cfg_.overlap == 2 && interior && !via_bits_ && !resident_;
-  const bool early_ok = row_exchange && dec_.Px == 1 && interior && !via_bits_ && !resident_;
+  overlap_ = row_exchange && cfg_.overlap == 2 && interior && !via_bits_;
+  const bool early_ok = row_exchange && dec_.Px == 1 && interior && !via_bits_;
   early_ = early_ok && cfg_.overlap == 1;
   // With the early-boundary schedule every transport operation runs on the
   // comm stream (one stream per communicator, in issue order), so the flag
@@ -249,15 +201,11 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     for (auto& e : edge_)
       for (auto& b : e) b = be_->alloc(size_t(gs_.bytes()));
   }
-  watchdog_s_ = cfg_.watchdog_s > 0 ? cfg_.watchdog_s
-                : cfg_.tune.i("watchdog_s") > 0 ? std::max(1.0, double(cfg_.tune.i("watchdog_s")))
-                                                : 900.0;
+  watchdog_s_ = cfg_.watchdog_s > 0 ? cfg_.watchdog_s : cfg_.tune.f("watchdog_s") > 0 ? cfg_.tune.f("watchdog_s") : 900.0;
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
-  if (resident_) be_->reserve_resident(via_bits_ ? gb_ : g_);  // before any capture
   if (use_graphs_) early_ = comm_route_ = false;  // captured epochs stay on one stream
-  if (use_graphs_) flow_ = false;  // a flow launch takes tickets and sequence numbers: never replayed
   // Overlap auto: measure both schedules on the real ranks (see auto_choose).
   // The one-GPU RCCL rehearsal measured the early-boundary schedule slower
   // (profiles/r02/rehearsal_overlap.jsonl), but it has no xGMI latency in it;
@@ -376,7 +324,6 @@ int64_t Engine::alive_count() {
 }
 
 int Engine::pick_T(int64_t remaining) const {
-  if (resident_) return int(std::min<int64_t>(remaining, tmax_));  // any T: one launch per epoch
   if (rows_wrapped_) {  // the LDS-tiled byte kernels: T = 1, 2, 4, ... (powers of two)
     int t = 1;
     while (2 * t <= tmax_ && 2 * t <= remaining) t *= 2;
@@ -574,14 +521,6 @@ void Engine::epoch_via_bits(int64_t d) {
   while (d > 0) {
     const int T = pick_T(d);
     if (rows_ring_) a = gb_.Dv - T;
-    if (const int n = flow_count(T, d, false)) {
-      add_drift(flow_blocks(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, n, a + T, gb_.R() - a - T, gen_));
-      bpar_ ^= n & 1;
-      gen_ += int64_t(n) * T;
-      a += int64_t(n) * T;
-      d -= int64_t(n) * T;
-      continue;
-    }
     add_drift(launch(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
     bpar_ ^= 1;
     gen_ += T;
@@ -644,16 +583,6 @@ void Engine::run_epoch(int64_t d) {
   while (d > 0) {
     const int T = pick_T(d);
     if (rows_ring_) a = g_.Dv - T;  // every block covers exactly the owned rows
-    // Runs of equal blocks as one flow launch; the early-boundary schedule
-    // keeps its split last block.
-    if (const int n = flow_count(T, d, early_ && send_next_ && full)) {
-      add_drift(flow_blocks(buf_[cur_], buf_[cur_ ^ 1], g_, T, n, a + T, g_.R() - a - T, gen_));
-      cur_ ^= n & 1;
-      gen_ += int64_t(n) * T;
-      a += int64_t(n) * T;
-      d -= int64_t(n) * T;
-      continue;
-    }
     if (d == T && early_ && send_next_ && full)
       last_block_early(T);
     else
@@ -764,7 +693,6 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   a.full_width = dec_.Px == 1 && cfg_.W % 32 == 0;
   a.wrap_rows = rows_wrapped_;
   a.stream = stream;
-  a.resident = resident_;
   // Linked launches assume the device to themselves: not while transport
   // work may run beside them on the comm stream (early-boundary schedule,
   // side polls).
@@ -776,40 +704,6 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   const int drift = be_->run_block(a);
   phase_end(kCompute, t, stream);
   ++launches_;
-  return drift;
-}
-
-int Engine::flow_count(int T, int64_t d, bool keep_last) const {
-  if (!flow_ || capturing_ || !be_->has_flow(via_bits_ ? Layout::Bits : cfg_.layout, T)) return 0;
-  int64_t n = d / T;
-  if (keep_last && n * T == d) --n;  // the last block runs on its own
-  return n >= 2 ? int(n) : 0;
-}
-
-int Engine::flow_blocks(void* in, void* out, const TileGeom& g, int T, int n, int64_t row_lo, int64_t row_hi,
-                        int64_t gen_base) {
-  FlowArgs f;
-  f.buf[0] = in;
-  f.buf[1] = out;
-  f.g = g;
-  f.T = T;
-  f.nblk = n;
-  f.row_lo = row_lo;
-  f.row_hi = row_hi;
-  f.shrink = rows_ring_ ? 0 : T;  // a ring's blocks all cover the owned rows; an epoch's shrink by T
-  f.ring = rows_ring_;
-  f.gen_base = gen_base;
-  const int64_t span = int64_t(n) * T;
-  f.changed = (flags_ && gen_base + span < flags_base_ + flags_len_ && gen_base >= flags_base_) ? flags_ : nullptr;
-  f.flags_base = flags_base_;
-  f.allow_drift = drift_ok_;
-  f.full_width = dec_.Px == 1 && cfg_.W % 32 == 0;
-  void* t = phase_begin(nullptr);
-  const int drift = be_->run_flow(f);
-  phase_end(kCompute, t, nullptr);
-  ++launches_;
-  ++flow_launches_;
-  flow_blocks_ += n;
   return drift;
 }
 
@@ -968,7 +862,6 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   const int64_t g0 = graph_runs_;
   const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_, es0 = early_sends_;
   const int64_t lk0 = be_->linked_launches();
-  const int64_t fl0 = flow_launches_, fb0 = flow_blocks_;
   trace::Range trace_run("gol.run");
   if (cfg_.timing_barriers) {
     settle_pending(false);  // one stream at a time on the communicator
@@ -1068,8 +961,6 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.graph_launches = graph_runs_ - g0;
   res.halo_bytes = halo_bytes_ - hb0;
   res.linked_launches = be_->linked_launches() - lk0;
-  res.flow_launches = flow_launches_ - fl0;
-  res.flow_blocks = flow_blocks_ - fb0;
   res.generations = limit;
   collect_phases(res);
   if (found >= 0) {

@@ -2,6 +2,7 @@
 
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -54,6 +55,36 @@ void pwrite_all(int fd, const void* buf, size_t n, int64_t off, const std::strin
     n -= size_t(r);
     off += r;
   }
+}
+
+// A file may not grow past the process's RLIMIT_FSIZE: the kernel would
+// answer ftruncate / pwrite / fallocate with SIGXFSZ, which kills the process
+// (a Python caller with it) before any error can be reported.
+void check_fsize_limit(int64_t end, const std::string& path) {
+  struct rlimit rl;
+  if (::getrlimit(RLIMIT_FSIZE, &rl) == 0 && rl.rlim_cur != RLIM_INFINITY && uint64_t(end) > uint64_t(rl.rlim_cur))
+    fail("output '" + path + "' needs " + std::to_string(end) + " bytes, beyond the file size limit (RLIMIT_FSIZE " +
+         std::to_string(uint64_t(rl.rlim_cur)) + " bytes)");
+}
+
+// Backs the byte range [off, off + n) of a file with disk blocks before it is
+// written through a shared mapping: a store into a sparse page that the file
+// system cannot back (disk or quota full, EIO) raises SIGBUS instead of an
+// error.  Returns false when the file system cannot reserve ranges (the
+// caller then writes with pwrite, which reports such errors); a reservation
+// the file system refuses for lack of space fails here, with its reason.
+bool reserve_range(int fd, int64_t off, int64_t n, const std::string& path) {
+  if (n <= 0) return true;
+  check_fsize_limit(off + n, path);
+  // fallocate(2), not posix_fallocate: glibc emulates the latter where the
+  // file system lacks the call by writing a zero byte per block, which would
+  // race with the other ranks writing their rows of the same file.
+  int r;
+  do r = ::fallocate(fd, 0, off, n);
+  while (r != 0 && errno == EINTR);
+  if (r == 0) return true;
+  if (errno == EOPNOTSUPP || errno == EINVAL || errno == ENOSYS) return false;
+  sys_fail("cannot reserve space for output", path);
 }
 
 // A read-only or writable shared mapping of a file range, page-aligned
@@ -178,6 +209,7 @@ void create_text_file(const std::string& path, int64_t W, int64_t H) {
   Fd f;
   f.fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
   if (f.fd < 0) sys_fail("cannot create output", path);
+  check_fsize_limit(H * (W + 1), path);
   if (::ftruncate(f.fd, H * (W + 1)) != 0) sys_fail("cannot size output", path);
 }
 
@@ -193,11 +225,13 @@ void write_text_tile(const std::string& path, int64_t W, int64_t H, Extent rows,
   // The tile's rows through a writable shared mapping of their byte range
   // (the MPI-IO writers' subarray view, src/game_mpi_async.c:382-455), rows
   // converted straight into the page cache in parallel; pwrite per row where
-  // the file cannot be mapped.
+  // the file cannot be mapped or its range not reserved (reserve_range).
   const int64_t first = rows.begin * (W + 1) + cols.begin;
   const int64_t last = (rows.end - 1) * (W + 1) + cols.begin + nc + (nl ? 1 : 0);
   struct stat st;
-  Map m(f.fd, first, (::fstat(f.fd, &st) == 0 && st.st_size >= last) ? last - first : 0, true);
+  const bool sized = ::fstat(f.fd, &st) == 0 && st.st_size >= last;
+  check_fsize_limit(last, path);
+  Map m(f.fd, first, (sized && reserve_range(f.fd, first, last - first, path)) ? last - first : 0, true);
   global_pool().parallel_for(nr, [&](int64_t b, int64_t e) {
     std::vector<uint8_t> buf(m.base ? 0 : size_t(nc + 1));
     for (int64_t i = b; i < e; ++i) {
@@ -217,7 +251,7 @@ void generate_text_file(const std::string& path, int64_t W, int64_t H, uint64_t 
   f.fd = ::open(path.c_str(), O_RDWR);
   if (f.fd < 0) sys_fail("cannot open output", path);
   const uint32_t th = density_thresh(density);
-  Map m(f.fd, 0, H * (W + 1), true);
+  Map m(f.fd, 0, reserve_range(f.fd, 0, H * (W + 1), path) ? H * (W + 1) : 0, true);
   global_pool().parallel_for(H, [&](int64_t b, int64_t e) {
     std::vector<uint8_t> buf(m.base ? 0 : size_t(W + 1));
     for (int64_t r = b; r < e; ++r) {

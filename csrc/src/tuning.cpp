@@ -11,8 +11,7 @@ const std::vector<TuningKey>& tuning_keys() {
   static const std::vector<TuningKey> keys = {
       // --- tune: the default build's performance knobs -------------------
       {"xlane", "GOL_XLANE", "-1", 'i', "tune",
-       "cross-lane window of the bit kernels: -1 auto (adder where the frame may drift, else DPP), 0 DPP, "
-       "3 adder (1 ds_bpermute, 2 carry chain: experimental)"},
+       "cross-lane window of the bit kernels: -1 auto (adder where the frame may drift, else DPP), 0 DPP, 3 adder"},
       {"group", "GOL_GROUP", "8", 'i', "tune",
        "waves per workgroup of the grouped schedule: 8 or 4; 0 the classic (ungrouped) schedule; -1 the model's "
        "choice"},
@@ -23,7 +22,7 @@ const std::vector<TuningKey>& tuning_keys() {
       {"min_seg_rows", "GOL_MIN_SEG_ROWS", "16", 'i', "tune",
        "shortest row segment a wave of the classic schedule is given"},
       {"chain", "GOL_CHAIN", "-1", 'i', "tune",
-       "chained groups: -1 timed per launch shape, 0 off, 1 on (2 timing probe: experimental)"},
+       "chained groups: -1 timed per launch shape, 0 off, 1 on, 2 timing probe (no waits: wrong cells)"},
       {"chain_spin", "GOL_CHAIN_SPIN", "16", 'i', "tune", "log2 of a chained wave's spin budget"},
       {"chain_acquire", "GOL_CHAIN_ACQUIRE", "1", 'i', "tune", "chained waits end with an acquire (L1 invalidate)"},
       {"link", "GOL_LINK", "-1", 'i', "tune",
@@ -38,44 +37,28 @@ const std::vector<TuningKey>& tuning_keys() {
       {"lds_pack", "GOL_LDS_PACK", "1", 'i', "tune", "LDS kernel packs its tile to bits"},
       {"lds_xcd", "GOL_LDS_XCD", "0", 'i', "tune", "XCD-aware tile order of the LDS kernel"},
       {"lds_waves", "GOL_LDS_WAVES", "0", 'i', "tune", "LDS kernel waves per block: 0 auto, 8 or 16"},
-      {"u8_pipe", "GOL_U8_PIPE", "1", 'i', "tune", "byte passes of T = 48 / 64 as level-pipelined wave pairs"},
+      {"u8_pipe", "GOL_U8_PIPE", "1", 'i', "tune", "byte passes of T = 48 as level-pipelined wave pairs"},
       {"u8_via_bits", "GOL_U8_VIA_BITS", "-1", 'i', "tune",
        "byte layout computes on bit words: -1 auto, 0 bytes, 1 bits (EngineConfig::u8_compute wins when set)"},
       {"side_poll", "GOL_SIDE_POLL", "0", 'i', "tune", "multi-rank polls reduce on the comm stream"},
       {"poll_copy_side", "GOL_POLL_COPY_SIDE", "-1", 'i', "tune",
        "single-rank polls copy their flags on a side stream, linked chains continuing across them: -1 where "
        "blocks are deeper than 8 generations, 1 always, 0 never (join the compute streams, copy there)"},
-      {"watchdog_s", "GOL_WATCHDOG_S", "0", 'i', "tune", "poll watchdog in seconds (0: 900; EngineConfig wins)"},
+      {"watchdog_s", "GOL_WATCHDOG_S", "0", 'f', "tune", "poll watchdog in seconds (0: 900; EngineConfig wins)"},
       {"host_threads", "GOL_HOST_THREADS", "0", 'i', "tune", "host thread pool size (0: min(cores, 16))"},
       {"cu_partition", "GOL_CU_PARTITION", "", 's', "tune",
        "k/n: this process's streams run on the k-th of n CU slices (ranks sharing a GPU)"},
-      // --- experimental: measured slower, or timing probes ---------------
-      {"wpl", "GOL_WPL", "1", 'i', "experimental", "words per lane of the bit kernels"},
-      {"skew", "GOL_SKEW", "0", 'i', "experimental", "skewed (ILP) schedule"},
-      {"split", "GOL_SPLIT", "0", 'i', "experimental", "split schedule (boundary states in scratch)"},
-      {"short", "GOL_SHORT", "0", 'i', "experimental", "short-segment groups"},
-      {"pipe", "GOL_PIPE", "0", 'i', "experimental", "level-pipelined wave pairs on bit words"},
-      {"resident", "GOL_RESIDENT", "0", 'i', "experimental", "resident epochs: -1 auto, 0 off, 1 on"},
-      {"res_k", "GOL_RES_K", "0", 'i', "experimental", "resident refresh period / halo rows (0: deepest)"},
-      {"res_d", "GOL_RES_D", "0", 'i', "experimental", "resident epoch depth"},
-      {"res_probe", "GOL_RES_PROBE", "0", 'i', "experimental", "resident timing probe without refreshes"},
-      {"lds_add", "GOL_LDS_ADD", "0", 'i', "experimental", "packed LDS tile with the adder window"},
-      {"flow", "GOL_FLOW", "0", 'i', "experimental", "persistent dataflow launches"},
-      {"flow_m", "GOL_FLOW_M", "0", 'i', "experimental", "waves per flow item (0: planner)"},
-      {"flow_nseg", "GOL_FLOW_NSEG", "0", 'i', "experimental", "flow groups per strip (0: planner)"},
-      {"flow_spin", "GOL_FLOW_SPIN", "20", 'i', "experimental", "log2 of a flow item's spin budget"},
-      {"link_force", "GOL_LINK_FORCE", "0", 'i', "experimental", "run the linked kernel unlinked (its cost probe)"},
-      {"pitch_pad", "GOL_PITCH_PAD", "0", 'i', "experimental", "extra bytes per padded row (multiple of 256)"},
+      // --- probe: timing probes (exact but measured slower, or wrong cells) -
+      {"link_force", "GOL_LINK_FORCE", "0", 'i', "probe", "run the linked kernel unlinked (its cost probe)"},
+      {"pitch_pad", "GOL_PITCH_PAD", "0", 'i', "probe", "extra bytes per padded row (multiple of 256)"},
       // --- diag ------------------------------------------------------------
       {"check_device", "GOL_CHECK_DEVICE", "0", 'i', "diag", "assert device affinity of every call and buffer"},
       {"tune_log", "GOL_TUNE_LOG", "0", 'i', "diag", "log per-launch-shape autotuning decisions"},
       {"host_profile", "GOL_HOST_PROFILE", "0", 'i', "diag", "host time per block (printed at exit)"},
       {"wg_trace", "GOL_WG_TRACE", "", 's', "diag", "N:path[:pair]: per-workgroup timestamps of launch N"},
-      {"res_trace", "GOL_RES_TRACE", "", 's', "diag", "N:path: resident launch N's trace"},
-      {"flow_trace", "GOL_FLOW_TRACE", "", 's', "diag", "N:path: flow launch N's per-item trace"},
       // --- fault injection ---------------------------------------------------
       {"fault_delay_spins", "GOL_FAULT_DELAY_SPINS", "0", 'i', "fault",
-       "seam groups / items publish late (x 127 s_sleep, <= 4096)"},
+       "seam groups of linked launches publish late (x 127 s_sleep, <= 4096)"},
       {"fault_delay_us", "GOL_FAULT_DELAY_US", "0", 'i', "fault", "thread transport delays messages randomly"},
       {"fault_garble", "GOL_FAULT_GARBLE", "0", 'i', "fault", "thread transport corrupts the N-th message"},
       {"fault_checkpoint_crash", "GOL_FAULT_CHECKPOINT_CRASH", "0", 'i', "fault",
@@ -83,8 +66,6 @@ const std::vector<TuningKey>& tuning_keys() {
       {"overlap_auto", "GOL_OVERLAP_AUTO", "", 's', "fault", "plain | early: force the overlap trial's outcome"},
       // --- CPU emulation of device features ----------------------------------
       {"cpu_ring", "GOL_CPU_RING", "0", 's', "emul", "CPU backend row rings: 0, 1, or fail (mapping fails)"},
-      {"cpu_resident", "GOL_CPU_RESIDENT", "0", 'i', "emul", "CPU backend accepts resident epochs"},
-      {"cpu_flow", "GOL_CPU_FLOW", "0", 'i', "emul", "CPU backend accepts flow runs"},
       {"cpu_drift", "GOL_CPU_DRIFT", "0", 'i', "emul", "CPU backend's drifting frame (as the adder window)"},
   };
   return keys;
@@ -104,6 +85,15 @@ bool parse_int(const std::string& s, long* out) {
   if (s.empty()) return false;
   char* end = nullptr;
   const long v = std::strtol(s.c_str(), &end, 10);
+  if (*end != '\0') return false;
+  *out = v;
+  return true;
+}
+
+bool parse_float(const std::string& s, double* out) {
+  if (s.empty()) return false;
+  char* end = nullptr;
+  const double v = std::strtod(s.c_str(), &end);
   if (*end != '\0') return false;
   *out = v;
   return true;
@@ -132,8 +122,11 @@ Tuning Tuning::from_env() {
 Tuning& Tuning::set(const std::string& key, const std::string& value) {
   const TuningKey& k = key_of(key);
   long v = 0;
+  double f = 0;
   if (k.type == 'i' && !parse_int(value, &v))
     fail(std::string("tuning ") + k.key + "=" + value + " (" + k.env + "): expected an integer");
+  if (k.type == 'f' && !parse_float(value, &f))
+    fail(std::string("tuning ") + k.key + "=" + value + " (" + k.env + "): expected a number");
   v_[k.key] = value;
   src_[k.key] = "set";
   return *this;
@@ -152,6 +145,13 @@ int Tuning::i(const std::string& key) const {
   return int(v);
 }
 
+double Tuning::f(const std::string& key) const {
+  const TuningKey& k = key_of(key);
+  double v = 0;
+  GOL_REQUIRE(k.type == 'f' && parse_float(v_.at(k.key), &v), std::string("tuning key ") + key + " is not a number");
+  return v;
+}
+
 const std::string& Tuning::s(const std::string& key) const { return v_.at(key_of(key).key); }
 
 bool Tuning::is_default(const std::string& key) const {
@@ -160,6 +160,12 @@ bool Tuning::is_default(const std::string& key) const {
     long a = 0, b = 0;
     parse_int(v_.at(k.key), &a);
     parse_int(k.dflt, &b);
+    return a == b;
+  }
+  if (k.type == 'f') {
+    double a = 0, b = 0;
+    parse_float(v_.at(k.key), &a);
+    parse_float(k.dflt, &b);
     return a == b;
   }
   return v_.at(k.key) == k.dflt;
@@ -179,20 +185,6 @@ std::string Tuning::summary() const {
   for (const auto& kv : changed())
     s += (s.empty() ? "" : " ") + kv.first + "=" + kv.second + "[" + src_.at(kv.first) + "]";
   return s.empty() ? "defaults" : s;
-}
-
-void Tuning::require_build(bool experimental_build) const {
-  if (experimental_build) return;
-  for (const TuningKey& k : tuning_keys())
-    if (std::string(k.cls) == "experimental" && !is_default(k.key))
-      fail(std::string("tuning ") + k.key + "=" + v_.at(k.key) + " (" + k.env + ", " + k.doc +
-           ") selects a measured-slower variant or probe that this build does not carry; rebuild with "
-           "GOL_EXPERIMENTAL=1 python -m gol_amd.native_build");
-  const int x = i("xlane");
-  if (x == 1 || x == 2)
-    fail("tuning xlane=" + std::to_string(x) + " (ds_bpermute / carry-chain window) needs an experimental build "
-         "(GOL_EXPERIMENTAL=1 python -m gol_amd.native_build)");
-  if (i("chain") == 2) fail("tuning chain=2 (chained-group timing probe) needs an experimental build");
 }
 
 }  // namespace gol

@@ -33,6 +33,25 @@ using namespace gol;
 
 namespace {
 
+// A JSON string literal of s (quotes, backslashes and control bytes escaped):
+// tuning values such as trace paths are arbitrary text.
+std::string jstr(const std::string& s) {
+  std::string o = "\"";
+  for (const unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += char(c);
+    } else if (c < 0x20) {
+      char b[8];
+      std::snprintf(b, sizeof b, "\\u%04x", c);
+      o += b;
+    } else {
+      o += char(c);
+    }
+  }
+  return o + "\"";
+}
+
 struct Options {
   int64_t W = 0, H = 0;
   std::string input;
@@ -456,13 +475,17 @@ int run(const Options& o) {
     if (!o.metrics.empty()) {
       std::ofstream f(o.metrics);
       double cups = res.loop_ms > 0 ? double(o.W) * double(o.H) * double(res.executed) / (res.loop_ms * 1e-3) : 0;
-      f << "{\"engine\": \"" << engine << "\", \"backend\": \"" << backends[0]->name()
-        << "\", \"layout\": \"" << layout_name(layout) << "\", \"ranks\": " << P
-        << ", \"decomp\": \"" << engines[0]->decomp().describe() << "\", \"tuning\": \"" << o.tune.summary()
-        << "\", \"W\": " << o.W
+      std::string tuning_changed = "{";
+      for (const auto& kv : o.tune.changed())
+        tuning_changed += (tuning_changed.size() > 1 ? ", " : "") + jstr(kv.first) + ": " + jstr(kv.second);
+      tuning_changed += "}";
+      f << "{\"engine\": " << jstr(engine) << ", \"backend\": " << jstr(backends[0]->name())
+        << ", \"layout\": " << jstr(layout_name(layout)) << ", \"ranks\": " << P
+        << ", \"decomp\": " << jstr(engines[0]->decomp().describe()) << ", \"tuning\": " << jstr(o.tune.summary())
+        << ", \"tuning_changed\": " << tuning_changed << ", \"W\": " << o.W
         << ", \"H\": " << o.H << ", \"generations\": " << res.generations
-        << ", \"executed\": " << res.executed << ", \"stop_reason\": \"" << res.stop_reason
-        << "\", \"loop_ms\": " << res.loop_ms << ", \"read_ms\": " << read_ms
+        << ", \"executed\": " << res.executed << ", \"stop_reason\": " << jstr(res.stop_reason)
+        << ", \"loop_ms\": " << res.loop_ms << ", \"read_ms\": " << read_ms
         << ", \"read_parse_ms\": " << read_parse_ms << ", \"read_load_ms\": " << read_load_ms
         << ", \"write_ms\": " << write_ms
         << ", \"write_store_ms\": " << *std::max_element(store_ms.begin(), store_ms.end())
@@ -470,9 +493,9 @@ int run(const Options& o) {
         << ", \"file_bytes\": " << o.H * (o.W + 1) << ", \"cell_updates_per_s\": " << cups
         << ", \"epoch\": " << engines[0]->epoch_depth() << ", \"tmax\": " << engines[0]->tmax()
         << ", \"exchanges\": " << res.exchanges << ", \"polls\": " << res.polls
-        << ", \"kernel_launches\": " << res.kernel_launches << ", \"comm\": \"" << (P > 1 ? comm : "self")
-        << "\", \"overlap_mode\": \"" << engines[0]->overlap_mode()
-        << "\", \"overlap_trial_ms_plain\": " << engines[0]->trial_ms_plain()
+        << ", \"kernel_launches\": " << res.kernel_launches << ", \"comm\": " << jstr(P > 1 ? comm : "self")
+        << ", \"overlap_mode\": " << jstr(engines[0]->overlap_mode())
+        << ", \"overlap_trial_ms_plain\": " << engines[0]->trial_ms_plain()
         << ", \"overlap_trial_ms_early\": " << engines[0]->trial_ms_early()
         << ", \"phase_timed\": " << (res.phase_timed ? "true" : "false") << ", \"compute_ms\": " << res.compute_ms
         << ", \"halo_ms\": " << res.halo_ms << ", \"fill_ms\": " << res.fill_ms

@@ -70,35 +70,6 @@ __global__ __launch_bounds__(256) void k_row(uint32_t* out, int steps) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = sink;
 }
 
-// Production row-word bodies with two words per lane.
-template <int T, int XL>
-__global__ __launch_bounds__(256) void k_row2(uint32_t* out, int steps) {
-  using IO = BitsIO<2, XL>;
-  Levels<T, 2> st;
-#pragma unroll
-  for (int L = 0; L < T; ++L)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int s = 0; s < 3; ++s) st.h0[L][s].w[i] = st.h1[L][s].w[i] = st.cc[L][s].w[i] = 0u;
-      st.acc[L].w[i] = 0u;
-    }
-  uint32_t seed = threadIdx.x * 2654435761u + blockIdx.x;
-  uint32_t sink = 0;
-  for (int k = 0; k + 3 <= steps; k += 3) {
-    Vec<2> a{{seed = xs(seed), seed = xs(seed)}};
-    Vec<2> ra = levels_full<T, IO, 0, 0, T>(st, a);
-    Vec<2> b{{seed = xs(seed), seed = xs(seed)}};
-    Vec<2> rb = levels_full<T, IO, 1, 0, T>(st, b);
-    Vec<2> c{{seed = xs(seed), seed = xs(seed)}};
-    Vec<2> rc = levels_full<T, IO, 2, 0, T>(st, c);
-    sink ^= ra.w[0] ^ ra.w[1] ^ rb.w[0] ^ rb.w[1] ^ rc.w[0] ^ rc.w[1];
-  }
-#pragma unroll
-  for (int L = 0; L < T; ++L) sink ^= st.acc[L].w[0] ^ st.acc[L].w[1];
-  out[blockIdx.x * blockDim.x + threadIdx.x] = sink;
-}
-
 // (w << 1) | carry_in; returns the carry out (w's msb) through *co.
 __device__ __forceinline__ uint32_t shl_cin(uint32_t w, uint64_t cin, uint64_t* co) {
   uint32_t r;
@@ -226,13 +197,6 @@ int main(int argc, char** argv) {
     for (int n : {1, 2, 4}) std::printf(" %8.2f", run(k_col<T, C, SC>, n, steps, cus, out, T * C)); \
     std::printf("\n");                                                                                \
   } while (0)
-#define ROW2(T, XL, name)                                                                          \
-  do {                                                                                             \
-    attr(reinterpret_cast<const void*>(&k_row2<T, XL>));                                           \
-    std::printf("%-34s", name);                                                                    \
-    for (int n : {1, 2, 4}) std::printf(" %8.2f", run(k_row2<T, XL>, n, steps, cus, out, 2 * T)); \
-    std::printf("\n");                                                                             \
-  } while (0)
   if (argc > 2 && std::atoi(argv[2]) == 1) {  // occupancy sweep of the row-word bodies: 1-8 waves per SIMD
     std::printf("%-34s %8s %8s %8s %8s %8s\n", "variant", "1 w", "2 w", "4 w", "6 w", "8 w");
 #define ROWN(T, XL, name)                                                                                \
@@ -249,10 +213,6 @@ int main(int argc, char** argv) {
     CHK(hipFree(out));
     return 0;
   }
-  ROW2(8, kXlaneAdd, "row words x2/lane, adder, T=8");
-  ROW2(12, kXlaneAdd, "row words x2/lane, adder, T=12");
-  ROW2(16, kXlaneAdd, "row words x2/lane, adder, T=16");
-  ROW2(8, kXlaneDpp, "row words x2/lane, DPP, T=8");
   ROW(8, kXlaneAdd, "row words, adder window, T=8");
   ROW(8, kXlaneDpp, "row words, DPP window, T=8");
   ROW(12, kXlaneAdd, "row words, adder window, T=12");

@@ -52,7 +52,6 @@ class LifeConfig:
     watchdog_s: float = 0.0       # fail when a termination poll waits longer (0 = GOL_WATCHDOG_S or 900 s)
     u8_compute: str = "auto"      # auto | bits | bytes: byte-layout epochs on bit words (packed once per epoch)
                                   # or on the bytes themselves; auto = bits on the GPU with the plain schedule
-    flow: str = "auto"            # auto | on | off: runs of equal temporal blocks as one persistent dataflow launch
     # Runtime tuning, key -> value (``native().tuning_keys()``; csrc/include/gol/tuning.hpp): kernel and
     # schedule knobs over the GOL_* environment overrides.  Used by the engine and by the backend this
     # Simulation creates (an explicitly passed backend keeps the tuning it was created with).
@@ -87,7 +86,6 @@ class LifeConfig:
         c.self_exchange = bool(self.self_exchange)
         c.watchdog_s = float(self.watchdog_s)
         c.u8_compute = {"auto": -1, "bytes": 0, "bits": 1}[self.u8_compute]
-        c.flow = {"auto": -1, "off": 0, "on": 1}[self.flow]
         c.tune = make_tuning(self.tune)
         return c
 
@@ -153,8 +151,6 @@ class RunReport:
     graph_launches: int = 0
     halo_bytes: int = 0
     linked_launches: int = 0  # launches that overlapped the previous one (GOL_LINK)
-    flow_launches: int = 0    # persistent dataflow launches (LifeConfig.flow)
-    flow_blocks: int = 0      # temporal blocks they ran
     # Per-phase device time (Simulation.phase_timing).
     phase_timed: bool = False
     compute_ms: float = 0.0
@@ -241,8 +237,7 @@ class Simulation:
                 "overlap_trial_ms_plain": self._eng.trial_ms_plain,
                 "overlap_trial_ms_early": self._eng.trial_ms_early,
                 "u8_compute": ("bits" if self._eng.via_bits else "bytes") if self.config.resolved_layout() == "u8" else None,
-                "row_ring": bool(self._eng.row_ring), "flow": bool(self._eng.flow),
-                "flow_plan": self.backend.flow_desc(),
+                "row_ring": bool(self._eng.row_ring),
                 "kernel": self._kernel_name(),
                 "tuning": self.tuning(), "tuning_changed": self.tuning_changed()}
 
@@ -270,15 +265,12 @@ class Simulation:
         be = self.backend.name()
         if lay == "u8" and not e.via_bits and "lds-tiled" in be:
             return "LDS-tiled byte kernel (" + be.split("; u8 ")[-1].rstrip("]").strip() + ")"
-        window = ("adder window (drifting frame)" if e.drifting else "symmetric window") if not e.resident \
-            else "resident epochs, adder window (drifting frame)"
+        window = "adder window (drifting frame)" if e.drifting else "symmetric window"
         parts = [f"bit-sliced temporal blocks, T={e.tmax}", window]
         if lay == "u8":
             parts.append("byte grid packed to bit words once per run" if e.via_bits else "byte-layout kernels")
         if e.row_ring:
             parts.append("row ring (no halo fills)")
-        if e.flow:
-            parts.append("persistent dataflow launches")
         return ", ".join(parts)
 
     # -- state -----------------------------------------------------------
@@ -315,8 +307,7 @@ class Simulation:
                         exchanges=r.exchanges, polls=r.polls, kernel_launches=r.kernel_launches,
                         cells=self.config.width * self.config.height, overlapped=r.overlapped,
                         graph_launches=r.graph_launches, halo_bytes=r.halo_bytes,
-                        linked_launches=r.linked_launches, flow_launches=r.flow_launches,
-                        flow_blocks=r.flow_blocks, phase_timed=r.phase_timed,
+                        linked_launches=r.linked_launches, phase_timed=r.phase_timed,
                         compute_ms=r.compute_ms, halo_ms=r.halo_ms, fill_ms=r.fill_ms,
                         allreduce_ms=r.allreduce_ms)
         self.last_report = rep

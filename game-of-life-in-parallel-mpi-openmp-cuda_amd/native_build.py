@@ -27,37 +27,22 @@ CSRC = REPO / "csrc"
 BIN = REPO / "bin"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("GOL_OFFLOAD_ARCH", "gfx950")
-# GOL_EXPERIMENTAL=1: also compile the variants and schedules that were
-# measured slower than the defaults (docs/HISTORY.md "What was tried"):
-# resident epochs, split / skewed / short-segment / linked / bit-layout
-# pipelined schedules, the ds_bpermute and carry-chain windows, two words per
-# lane, the packed LDS tile's adder window.  The default build leaves them out
-# (a smaller module and GPU tier); the backend refuses their knobs loudly.
-EXPERIMENTAL = os.environ.get("GOL_EXPERIMENTAL", "0") not in ("", "0")
-BUILD = REPO / "build" / ("obj_exp" if EXPERIMENTAL else "obj")
-MODE_STAMP = PKG_DIR / "_gol.mode"  # which mode _gol.so / bin/* were linked in (travels with the .so)
+BUILD = REPO / "build" / "obj"
 
 HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/transport.cpp",
              "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp", "src/tuning.cpp"]
+# One translation unit per compiled kernel variant (layout x cross-lane
+# window), so the build compiles them in parallel.  The variants measured
+# slower than these (resident epochs, persistent dataflow launches, short
+# segments, split / skewed schedules, ds_bpermute and carry-chain windows, two
+# words per lane) were removed in round 6; their code is in git history
+# (docs/HISTORY.md) and their numbers in docs/HISTORY.md / PERFORMANCE.md.
 LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_add", "u8_w1_dpp", "u8_w1_add",
                  *[f"u8_w1_dpp_t{t}" for t in (24, 32)],  # deep byte passes
                  "u8_w1_dpp_t48"]  # pipelined wave pairs (life_pipe_impl.hpp)
-EXPERIMENTAL_VARIANTS = ["bits_w1_bperm", "bits_w1_carry", "bits_w2_dpp", "bits_w2_carry", "u8_w1_carry",
-                         "u8_w1_carry_t24", "u8_w1_carry_t32"]
-RESIDENT_TUS = 9  # life_resident_rw0..8.hip: the resident kernel's rows-per-wave instantiations
-# Persistent dataflow launches (life_flow_impl.hpp): exact, measured slower
-# than the grouped launches on every tile (docs/PERFORMANCE.md "Persistent
-# dataflow launches"), so experimental builds only.
-FLOW_VARIANTS = ["bits_add", "bits_dpp"]
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
             *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
             "kernels/tile_ops.hip"]
-EXPERIMENTAL_TUS = [*[f"kernels/life_block_{v}.hip" for v in EXPERIMENTAL_VARIANTS], "kernels/life_resident.hip",
-                    *[f"kernels/life_resident_rw{i}.hip" for i in range(RESIDENT_TUS)],
-                    *[f"kernels/life_flow_{v}.hip" for v in FLOW_VARIANTS]]
-if EXPERIMENTAL:
-    HIP_SRCS += EXPERIMENTAL_TUS
-MODE = "experimental" if EXPERIMENTAL else "default"
 BIND_SRCS = ["src/bindings.cpp"]
 CLI_MAIN = "tools/gol_main.cpp"
 GEN_MAIN = "tools/gol_gen.cpp"
@@ -72,25 +57,18 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the native build needs ROCm (hipcc --offload-arch=gfx950)")
 
 
-# Headers only the experimental translation units include: editing them does
-# not make a default module stale.
-EXPERIMENTAL_HEADERS = {"kernels/life_resident_impl.hpp", "kernels/life_short_impl.hpp", "kernels/life_flow_impl.hpp"}
-
-
 def _headers_mtime() -> float:
     m = 0.0
     for p in list(CSRC.rglob("*.hpp")) + list(CSRC.rglob("*.h")):
-        if not EXPERIMENTAL and p.relative_to(CSRC).as_posix() in EXPERIMENTAL_HEADERS:
-            continue
         m = max(m, p.stat().st_mtime)
     return m
 
 
 def _compile_cmd(src: Path, obj: Path) -> list[str]:
-    inc = [f"-I{CSRC / 'include'}", f"-I{CSRC}", *(["-DGOL_EXPERIMENTAL=1"] if EXPERIMENTAL else [])]
+    inc = [f"-I{CSRC / 'include'}", f"-I{CSRC}"]
     if src.suffix == ".hip":
         extra = []
-        if src.name.startswith(("life_block_", "life_flow_")):
+        if src.name.startswith("life_block_"):
             # Scheduler for the temporal-blocking kernels: max-ILP interleaves the
             # independent generation levels.  Measured on MI355X it is on par
             # with the default strategy (the kernel is VALU-throughput bound);
@@ -149,7 +127,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     # Longest compiles first (deep byte passes, then the kernel variants), so
     # the pool does not end on one long translation unit.
     todo.sort(key=lambda s: 0 if any(f"_t{t}" in s for t in (24, 32, 48, 64)) else
-              1 if ("life_block_" in s or "life_flow_" in s or "life_resident_rw" in s) else 2)
+              1 if "life_block_" in s else 2)
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]
@@ -163,16 +141,14 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         "gol": BIN / "gol",
         "gol_gen": BIN / "gol_gen",
     }
-    stamp = MODE_STAMP.read_text().strip() if MODE_STAMP.exists() else ""
-    relink = bool(todo) or force or any(not p.exists() for p in outs.values()) or stamp != MODE
+    relink = bool(todo) or force or any(not p.exists() for p in outs.values())
     if relink:
         _run([_hipcc(), "-shared", "-fPIC", *core, str(objs[BIND_SRCS[0]]), "-o", str(MODULE), *rocm_libs],
              verbose)
         _run([_hipcc(), *core, str(objs[CLI_MAIN]), "-o", str(outs["gol"]), *rocm_libs], verbose)
         _run([_hipcc(), *core, str(objs[GEN_MAIN]), "-o", str(outs["gol_gen"]), *rocm_libs], verbose)
-        MODE_STAMP.write_text(MODE + "\n")
     LAST_BUILD.clear()
-    LAST_BUILD.update(compiled=len(todo), up_to_date=len(srcs) - len(todo), relinked=relink, mode=MODE)
+    LAST_BUILD.update(compiled=len(todo), up_to_date=len(srcs) - len(todo), relinked=relink)
     return outs
 
 
@@ -184,57 +160,6 @@ def gfx950_code_objects(path: Path = MODULE) -> int:
     """Number of gfx950 device code objects bundled in a built library (the
     offload bundle entries name their target)."""
     return path.read_bytes().count(b"amdgcn-amd-amdhsa--" + ARCH.encode())
-
-
-def compile_experimental(verbose: bool = False, jobs: int | None = None) -> int:
-    """Compile-check the experimental-only translation units (the measured-
-    slower variants and the resident kernel) with -DGOL_EXPERIMENTAL into
-    build/obj_exp, without linking or touching the default module; returns
-    how many were compiled.  __graft_entry__.build() runs it so every HIP
-    source in the tree is compiled for gfx950 each round."""
-    global EXPERIMENTAL, BUILD
-    saved = EXPERIMENTAL, BUILD
-    EXPERIMENTAL, BUILD = True, REPO / "build" / "obj_exp"
-    try:
-        BUILD.mkdir(parents=True, exist_ok=True)
-        srcs = [*EXPERIMENTAL_TUS, "kernels/life_block.hip", "src/backend_hip.hip",
-                "kernels/life_block_bits_w1_dpp.hip"]
-        objs = {s: BUILD / (s.replace("/", "_") + ".o") for s in srcs}
-        hdr = _headers_mtime()
-        todo = [s for s in srcs if _needs(objs[s], CSRC / s, hdr)]
-        with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
-            for f in [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]:
-                f.result()
-        return len(todo)
-    finally:
-        EXPERIMENTAL, BUILD = saved
-
-
-def build_experimental_module(out: Path, verbose: bool = False, jobs: int | None = None) -> Path:
-    """The whole module in experimental mode, linked to `out` (not the default
-    module's path); load it with GOL_NATIVE_SO=<out> to run the experimental
-    GPU tests (pytest -m "gpu and experimental")."""
-    global EXPERIMENTAL, BUILD, HIP_SRCS
-    saved = EXPERIMENTAL, BUILD, HIP_SRCS
-    EXPERIMENTAL, BUILD = True, REPO / "build" / "obj_exp"
-    HIP_SRCS = HIP_SRCS + EXPERIMENTAL_TUS
-    try:
-        BUILD.mkdir(parents=True, exist_ok=True)
-        srcs = HOST_SRCS + HIP_SRCS + BIND_SRCS
-        objs = {s: BUILD / (s.replace("/", "_") + ".o") for s in srcs}
-        hdr = _headers_mtime()
-        todo = [s for s in srcs if _needs(objs[s], CSRC / s, hdr)]
-        with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
-            for f in [ex.submit(_run, _compile_cmd(CSRC / s, objs[s]), verbose) for s in todo]:
-                f.result()
-        out = Path(out)
-        out.parent.mkdir(parents=True, exist_ok=True)
-        rocm_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx",
-                     f"-Wl,-rpath,{ROCM / 'lib'}", "-pthread"]
-        _run([_hipcc(), "-shared", "-fPIC", *[str(objs[s]) for s in srcs], "-o", str(out), *rocm_libs], verbose)
-        return out
-    finally:
-        EXPERIMENTAL, BUILD, HIP_SRCS = saved
 
 
 SELFTEST_MAIN = "tools/gol_selftest.cpp"
@@ -270,8 +195,6 @@ def build_selftest(kind: str = "address", verbose: bool = False, jobs: int | Non
 
 def is_built() -> bool:
     if not MODULE.exists():
-        return False
-    if not MODE_STAMP.exists() or MODE_STAMP.read_text().strip() != MODE:
         return False
     hdr = _headers_mtime()
     newest = max([(CSRC / s).stat().st_mtime for s in HOST_SRCS + HIP_SRCS + BIND_SRCS] + [hdr])

@@ -42,8 +42,16 @@ def main() -> int:
     ap.add_argument("out")
     ap.add_argument("--repeat", type=int, default=1)
     ap.add_argument("--timeout", type=int, default=180)
+    ap.add_argument("--only", default="", help="comma-separated configuration names to run (default: all)")
     a = ap.parse_args()
     rows = parse(a.matrix)
+    if a.only:
+        keep = a.only.split(",")
+        unknown = sorted(set(keep) - {r[0] for r in rows})
+        if unknown:
+            print(f"bench_matrix: no configuration named {unknown} in {a.matrix}", file=sys.stderr)
+            return 2
+        rows = [r for r in rows if r[0] in keep]
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     log = open(os.path.splitext(a.out)[0] + ".log", "a")
     for run in range(a.repeat):
@@ -69,7 +77,7 @@ def main() -> int:
                     f.write(json.dumps(rec) + "\n")
                 c = rec.get("config", {})
                 print(f"  {name}: {rec['ms_per_step']:.3f} ms/step  {rec['value']:.4g}  verified={rec.get('verified')}"
-                      f"  flow={c.get('flow_plan', '')}", flush=True)
+                      f"  sha={((c.get('verify') or {}).get('final_sha256') or '')[:12]}", flush=True)
             if r.returncode != 0 or not recs:
                 print(f"{name}: exit {r.returncode}; stopping (see {log.name})", flush=True)
                 print(r.stderr[-3000:], flush=True)

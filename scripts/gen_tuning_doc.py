@@ -12,7 +12,7 @@ sys.path.insert(0, REPO)
 from gol_amd._native import native  # noqa: E402
 
 CLASSES = {"tune": "Performance knobs of the default build",
-           "experimental": "Measured-slower kernels, schedules and timing probes",
+           "probe": "Timing probes of the default kernels (exact but slower, or wrong cells by design)",
            "diag": "Traces, logs and consistency checks",
            "fault": "Fault injection (tests)",
            "emul": "CPU backend emulating device features (tests)"}
@@ -25,9 +25,8 @@ def main() -> None:
            "regenerate with `python scripts/gen_tuning_doc.py`). Set a key with `--tune key=value` (bin/gol,",
            "`python -m gol_amd.cli`, bench.py) or `LifeConfig(tune={key: value})`; its `GOL_*` variable",
            "overrides the default (precedence: default < environment < explicit). Backends, the engine and",
-           "the transports read the table once, at construction. Keys of class `experimental` are refused",
-           "by default builds (`GOL_EXPERIMENTAL=1 python -m gol_amd.native_build` builds the module that",
-           "carries them).", ""]
+           "the transports read the table once, at construction. The kernel variants and schedules measured",
+           "slower than the defaults were removed in round 6 (their numbers: docs/HISTORY.md).", ""]
     for c, title in CLASSES.items():
         out += [f"## {c}: {title}", "", "| key | environment | default | meaning |", "|---|---|---|---|"]
         for k in keys:

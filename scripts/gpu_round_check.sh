@@ -18,7 +18,7 @@ if has multirank; then
   bash scripts/gpu_multirank.sh "${O#gpurun_out/}/multirank" || exit 1
 fi
 if has large; then
-  timeout -k 10 420 python -u scripts/bench_matrix.py scripts/matrices/r05_large_1M.txt "$O/large_1M.jsonl" \
+  timeout -k 10 420 python -u scripts/bench_matrix.py scripts/matrices/main.txt "$O/large_1M.jsonl" --only bits_1M,u8_1M_share8 \
     --timeout 400 || exit 1
 fi
 if has prof; then

@@ -2,8 +2,7 @@
 
 Markers: ``gpu`` - needs a real MI355X (run on the GPU box with ``-m gpu``);
 everything else runs on the CPU (``-m "not gpu"``), including the
-multi-process ``gloo`` tests.  ``experimental`` - a measured-slower kernel
-variant or schedule that only experimental builds carry (skipped otherwise).
+multi-process ``gloo`` tests.
 """
 from __future__ import annotations
 
@@ -23,16 +22,6 @@ if str(REPO) not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD Instinct GPU (MI355X, gfx950)")
     config.addinivalue_line("markers", "slow: long-running test")
-    config.addinivalue_line("markers", "experimental: needs an experimental native build (GOL_EXPERIMENTAL=1: "
-                                       "the measured-slower kernel variants and schedules)")
-
-
-def pytest_runtest_setup(item):
-    if item.get_closest_marker("experimental") is not None:
-        import gol_amd  # noqa: PLC0415
-
-        if not gol_amd.native().experimental_build():
-            pytest.skip("not an experimental build (GOL_EXPERIMENTAL=1 python -m gol_amd.native_build)")
 
 
 def pytest_terminal_summary(terminalreporter):

@@ -13,10 +13,6 @@ from gol_amd.parallel import InProcessGroup
 from golden import CASES, CONVERGING, GLIDER
 
 pytestmark = pytest.mark.gpu
-# Measured-slower variants and schedules: compiled only into experimental
-# builds (GOL_EXPERIMENTAL=1 native_build); skipped when the module lacks them.
-experimental = pytest.mark.experimental
-X = experimental
 
 
 @pytest.fixture
@@ -63,20 +59,15 @@ def test_every_temporal_block_size(gpu, tmax, layout):
     assert (got == want).all()
 
 
-@pytest.mark.parametrize("wpl,xlane,skew", [(1, 0, 0), (1, 3, 0)] + [
-    pytest.param(*v, marks=X) for v in [(1, 1, 0), (1, 2, 0), (2, 0, 0), (2, 2, 0), (1, 0, 1), (1, 2, 1), (2, 0, 1),
-                                        (1, 3, 1)]])
+@pytest.mark.parametrize("xlane", [0, 3])
 @pytest.mark.parametrize("tmax", [1, 4, 8, 12, 16])
-def test_kernel_variants_vs_torch(gpu, tune, wpl, xlane, skew, tmax):
-    """Every compiled life_block variant (words/lane x DPP|bpermute|carry x
-    schedule) against the fp32 conv oracle, including the changed-flag
-    termination."""
-    tune["wpl"] = str(wpl)
+def test_kernel_variants_vs_torch(gpu, tune, xlane, tmax):
+    """Every compiled life_block variant (DPP | adder window) against the fp32
+    conv oracle, including the changed-flag termination."""
     tune["xlane"] = str(xlane)
-    tune["skew"] = str(skew)
     # 4000 cells wide: 125 words -> tail handling in the last column wave.
     W, H = 4000 - 4000 % 32, 333
-    g = random_grid(W, H, 11 * wpl + tmax)
+    g = random_grid(W, H, 11 + tmax)
     gens = 3 * tmax + 1
     want = life_step_torch(g, gens, device="cuda")
     assert (life_step(g, gens, engine="hip", layout="bits", tmax=tmax) == want).all()
@@ -88,7 +79,7 @@ def test_kernel_variants_vs_torch(gpu, tune, wpl, xlane, skew, tmax):
         assert (out == ref).all(), seed
 
 
-@pytest.mark.parametrize("xlane", [0, pytest.param(2, marks=X), 3])
+@pytest.mark.parametrize("xlane", [0, 3])
 @pytest.mark.parametrize("tmax", [1, 8, 16])
 def test_u8_kernel_variants_vs_torch(gpu, tune, xlane, tmax):
     tune["xlane"] = str(xlane)
@@ -100,7 +91,7 @@ def test_u8_kernel_variants_vs_torch(gpu, tune, xlane, tmax):
 
 
 @pytest.mark.parametrize("tmax", [24, 32])
-@pytest.mark.parametrize("xlane", [0, pytest.param(2, marks=X), 3])
+@pytest.mark.parametrize("xlane", [0, 3])
 def test_deep_byte_passes_vs_torch(gpu, tune, tmax, xlane):
     """T = 24 / 32 byte-layout passes (life_block_u8_w1_*_t24/_t32.hip, the
     HBM-bound layout's deep passes) in every byte variant and schedule,
@@ -202,78 +193,6 @@ def test_grouped_schedule_many_groups_and_termination(gpu, tune, group):
         out, rep = simulate(grid, 1000, engine="hip", layout=layout, tmax=16)
         assert rep.generations == rgens, layout
         assert (out == ref).all(), layout
-
-
-@experimental
-@pytest.mark.parametrize("layout", ["bits", "u8"])  # u8: falls back to the grouped kernel
-@pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
-@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
-def test_short_segment_schedule_vs_torch(gpu, tune, layout, W, H, xlane, tmax):
-    """Short-segment groups (csrc/kernels/life_short_impl.hpp: segments of
-    Q < 2T rows, the whole sweep unrolled, level rows of the lower wave handed
-    over through LDS with per-level flags) forced on, against the fp32 conv
-    oracle; several segment lengths Q via the wave-count target."""
-    tune["short"] = "2"
-    tune["xlane"] = str(xlane)
-    g = random_grid(W, H, W * 3 + H)
-    want = life_step_torch(g, 35, device="cuda")
-    for target in ("0", "100000", "3000"):
-        tune["target_waves"] = target
-        assert (life_step(g, 35, engine="hip", layout=layout, tmax=tmax) == want).all(), target
-
-
-@experimental
-@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
-def test_short_segment_schedule_termination(gpu, tune, xlane, tmax):
-    tune["short"] = "2"
-    tune["xlane"] = str(xlane)
-    tune["target_waves"] = "100000"
-    grid = np.zeros((1024, 512), dtype=np.uint8)
-    W, H, seed, density = CONVERGING[5]
-    grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
-    ref, rgens, _ = reference_run(grid)
-    for layout in ("bits", "u8"):
-        out, rep = simulate(grid, 1000, engine="hip", layout=layout, tmax=tmax)
-        assert rep.generations == rgens, layout
-        assert (out == ref).all(), layout
-
-
-@experimental
-@pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100)])
-@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12), (3, 16), (0, 12)])
-def test_pipe_schedule_vs_torch(gpu, tune, W, H, xlane, tmax):
-    """Level-pipelined wave pairs (csrc/kernels/life_pipe_impl.hpp: stage A
-    runs levels 0..T/2-1 and hands its rows to stage B through an LDS ring)
-    forced on, against the fp32 conv oracle; several group shapes via the
-    wave-count target."""
-    tune["pipe"] = "2"
-    tune["xlane"] = str(xlane)
-    g = random_grid(W, H, W * 5 + H)
-    want = life_step_torch(g, 2 * tmax + 11, device="cuda")
-    for target in ("0", "100000", "3000"):
-        tune["target_waves"] = target
-        sim = Simulation(LifeConfig(W, H, gen_limit=2 * tmax + 11, tmax=tmax, tune=tune), engine="hip")
-        assert "pipe=forced" in sim.describe()["backend"]
-        sim.load(g)
-        sim.advance(2 * tmax + 11)
-        assert (sim.tile() == want).all(), target
-
-
-@experimental
-@pytest.mark.parametrize("xlane,tmax", [(0, 16), (3, 12)])
-def test_pipe_schedule_termination(gpu, tune, xlane, tmax):
-    """Exact Generations with the pipelined pairs: both stages raise their
-    levels' change flags."""
-    tune["pipe"] = "2"
-    tune["xlane"] = str(xlane)
-    tune["target_waves"] = "100000"
-    grid = np.zeros((1024, 512), dtype=np.uint8)
-    W, H, seed, density = CONVERGING[5]
-    grid[500:500 + H, 200:200 + W] = random_grid(W, H, seed, density)
-    ref, rgens, _ = reference_run(grid)
-    out, rep = simulate(grid, 1000, engine="hip", tmax=tmax)
-    assert rep.generations == rgens
-    assert (out == ref).all()
 
 
 @pytest.mark.parametrize("W,H", [(32 * 200, 700), (4000 - 4000 % 32, 1111), (2048, 333), (4096, 2100),
@@ -473,50 +392,6 @@ def test_u8_lds_termination(gpu, tune, W, H, seed, density):
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
     out, rep = simulate(g, 1000, engine="hip", layout="u8")
-    assert rep.generations == rgens
-    assert (out == ref).all()
-
-
-@experimental
-@pytest.mark.parametrize("layout", ["bits", "u8"])
-@pytest.mark.parametrize("tmax", [4, 8, 16])
-@pytest.mark.parametrize("W,H", [(4000 - 4000 % 32, 1500), (2048, 333), (96, 100)])
-def test_split_schedule_vs_torch(gpu, tune, layout, tmax, W, H):
-    """Split schedule (trapezoid per segment + inverted triangle per boundary,
-    boundary states through memory) forced on, many short segments."""
-    tune["split"] = "1"
-    tune["min_seg_rows"] = "1"
-    g = random_grid(W, H, 3 * tmax + W)
-    gens = 3 * tmax + 2
-    want = life_step_torch(g, gens, device="cuda")
-    got = life_step(g, gens, engine="hip", layout=layout, tmax=tmax)
-    assert (got == want).all()
-
-
-@experimental
-@pytest.mark.parametrize("W,H,seed,density", CONVERGING)
-def test_split_schedule_termination(gpu, tune, W, H, seed, density):
-    tune["split"] = "1"
-    tune["min_seg_rows"] = "1"
-    g = random_grid(W, H, seed, density)
-    ref, rgens, _ = reference_run(g)
-    for tmax in (4, 8):
-        out, rep = simulate(g, 1000, engine="hip", tmax=tmax)
-        assert rep.generations == rgens
-        assert (out == ref).all()
-
-
-@experimental
-def test_split_schedule_tall_grid_flags(gpu, tune):
-    """Many boundaries per launch; the changed flags of both phases must OR
-    to the exact per-generation result (compare a run that stops early)."""
-    tune["split"] = "1"
-    g = np.zeros((4096, 512), dtype=np.uint8)
-    g[2000:2002, 100:102] = 1  # a block (still life)
-    W, H, seed, density = CONVERGING[5]
-    g[1990:1990 + H, 300:300 + W] = random_grid(W, H, seed, density)  # settles after a while
-    out, rep = simulate(g, 1000, engine="hip", tmax=16)
-    ref, rgens, _ = reference_run(g)
     assert rep.generations == rgens
     assert (out == ref).all()
 
@@ -914,118 +789,6 @@ def test_u8_via_bits_graphs_survive_drift_rotation(gpu, tune):
         want = life_step_torch(want, 2 * eng.epoch_depth, device="cuda")
         assert (sim.tile() == want).all()
     assert graphs > 0 and drifted > 0
-
-
-# ---- resident epochs (life_resident_impl.hpp) -------------------------------
-
-def _resident_sim(tune, W, H, k=8, D=0, rccl_self=False, **kw):
-    import gc
-
-    from gol_amd import make_backend, native
-    gc.collect()  # a stale backend on the device would turn resident epochs off
-    tune["resident"] = "1"
-    tune["res_k"] = str(k)
-    if D:
-        tune["res_d"] = str(D)
-    cfg = LifeConfig(W, H, self_exchange=rccl_self, **kw, tune=tune)
-    if rccl_self:  # the multi-rank epoch schedule against a 1-rank RCCL communicator
-        C = native()
-        sim = Simulation(cfg, transport=C.rccl_transport(C.rccl_unique_id(), 0, 1, 0, tune=make_tuning(tune)),
-                         backend=make_backend("hip", 0, tune=tune))
-    else:
-        sim = Simulation(cfg, engine="hip")
-    assert sim.native_engine.resident, "resident epochs did not engage"
-    return sim
-
-
-@experimental
-@pytest.mark.parametrize("W,H,k,D", [(4096, 1024, 8, 0), (32 * 200, 700, 16, 48), (2048, 333, 4, 64),
-                                     (32768, 512, 8, 128), (96, 70, 8, 40)])
-def test_resident_epochs_vs_torch(gpu, tune, W, H, k, D):
-    """Whole epochs in one launch with the tile in registers: bands, strips,
-    halo refreshes every k generations and the drifting frame, exact against
-    the fp32 oracle over several epochs (and a partial one)."""
-    g = random_grid(W, H, W + H + k)
-    sim = _resident_sim(tune, W, H, k=k, D=D, gen_limit=400, check_similarity=False)
-    sim.load(g)
-    sim.advance(301)
-    assert (sim.tile() == life_step_torch(g, 301, device="cuda")).all()
-
-
-@experimental
-def test_resident_chunked_runs_and_rehearsal(gpu, tune):
-    """Chunked runs (partial epochs at every chunk end) and the multi-rank
-    epoch schedule against a self-exchanging transport (deep halo rows)."""
-    W, H = 8192, 1536
-    g = random_grid(W, H, 5)
-    for self_exchange in (False, True):
-        sim = _resident_sim(tune, W, H, gen_limit=2000, check_similarity=False, rccl_self=self_exchange)
-        sim.load(g)
-        want = g
-        for n in (300, 517, 96):
-            sim.advance(n)
-            want = life_step_torch(want, n, device="cuda")
-            assert (sim.tile() == want).all(), (self_exchange, n)
-        del sim
-
-
-@experimental
-@pytest.mark.parametrize("case", [c for c in CONVERGING if c[0] % 32 == 0] + [(256, 512, 77, 0.5)])
-def test_resident_termination_matches_reference(gpu, tune, case):
-    """The per-generation change flags of resident launches (one LDS slot per
-    generation, flushed every 64) give the reference's Generations count."""
-    W, H, seed, density = case
-    g = random_grid(W, H, seed, density)
-    ref, gens, _ = reference_run(g)
-    sim = _resident_sim(tune, W, H, D=40, poll_gens=80)
-    sim.load(g)
-    rep = sim.run()
-    assert rep.generations == gens
-    assert (sim.tile() == ref).all()
-
-
-@experimental
-def test_resident_termination_large_still_life(gpu, tune):
-    """A soup that dies out inside a long epoch: the first unchanged
-    generation lies deep inside one resident launch."""
-    W, H = 4096, 2048
-    g = np.zeros((H, W), np.uint8)
-    g[100:102, 200:202] = 1          # block (still life)
-    g[1000, 3000:3003] = 1           # blinker: similarity every 2 generations
-    sim = _resident_sim(tune, W, H, D=200)
-    sim.load(g)
-    rep = sim.run()
-    ref, gens, _ = reference_run(g)
-    assert rep.generations == gens
-    assert (sim.tile() == ref).all()
-
-
-@experimental
-def test_resident_u8_via_bits_and_graphs(gpu, tune):
-    tune["u8_via_bits"] = "1"
-    W, H = 4096, 1024
-    g = random_grid(W, H, 9)
-    for graphs in ("off", "on"):
-        sim = _resident_sim(tune, W, H, layout="u8", graphs=graphs, gen_limit=1000, check_similarity=False)
-        sim.load(g)
-        sim.advance(700)
-        assert (sim.tile() == life_step_torch(g, 700, device="cuda")).all(), graphs
-        del sim
-
-
-@experimental
-def test_resident_off_when_ranks_share_the_gpu(gpu, tune):
-    """Four in-process ranks on one device: a resident launch could not get
-    every CU, so the engines fall back to the grouped kernels (still exact)."""
-    tune["resident"] = "1"
-    W, H = 4096, 1024
-    g = random_grid(W, H, 3)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=300, decomp="1x4", check_similarity=False, tune=tune), 4,
-                         engine="hip")
-    assert not any(s.native_engine.resident for s in grp.sims)
-    grp.load(g)
-    grp.parallel(lambda s: s.advance(300))
-    assert (grp.gather() == life_step_torch(g, 300, device="cuda")).all()
 
 
 # ---- row ring (Backend::row_ring_halo, hipMemMap'd halos) -------------------

@@ -111,3 +111,46 @@ def test_ascii_and_binary_inputs_equivalent(native):
     a = reference_run(g, 50)[0]
     b = reference_run(ascii_grid, 50)[0]
     assert (a == b).all()
+
+
+_FSIZE_CHILD = r"""
+import resource, sys
+sys.path.insert(0, {repo!r})
+from gol_amd.utils import io
+resource.setrlimit(resource.RLIMIT_FSIZE, (1 << 20, 1 << 20))
+for what, call in [("create", lambda: io.create_text_file({p1!r}, 2048, 2048)),
+                   ("generate", lambda: io.generate({p2!r}, 2048, 2048, seed=1))]:
+    try:
+        call()
+    except Exception as e:
+        print(what, "raised", "RLIMIT_FSIZE" in str(e))
+    else:
+        print(what, "returned")
+"""
+
+
+def test_output_beyond_file_size_limit_raises_not_signals(tmp_path, native, repo):
+    """outputs are written through shared mappings; a file the
+    process may not grow must fail with an error (SIGXFSZ / SIGBUS would kill
+    a Python caller without a message)."""
+    import subprocess
+    import sys
+
+    code = _FSIZE_CHILD.format(repo=str(repo), p1=str(tmp_path / "a.txt"), p2=str(tmp_path / "b.txt"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    assert r.stdout.split("\n")[:2] == ["create raised True", "generate raised True"], r.stdout
+
+
+def test_mapped_writes_reserve_their_blocks(tmp_path, native):
+    """A tile written through a mapping is backed by disk blocks first
+    (fallocate), so a full file system reports an error instead of SIGBUS."""
+    W, H = 4096, 64
+    p = tmp_path / "s.txt"
+    io.create_text_file(str(p), W, H)  # sized by ftruncate: sparse
+    g = random_grid(W, H, 5)
+    io.write_tile(str(p), W, H, 0, 0, g)
+    st = os.stat(p)
+    if st.st_blocks * 512 < st.st_size:
+        pytest.skip("this file system does not reserve ranges (fallocate unsupported): the pwrite path ran")
+    assert (io.read_grid(str(p), W, H) == g).all()

@@ -26,13 +26,15 @@ def test_table_defaults_and_classes(native):
     t = native.Tuning()
     assert t.changed() == {} and t.summary() == "defaults"
     assert len({k["key"] for k in keys}) == len(keys) and len({k["env"] for k in keys}) == len(keys)
-    assert {k["class"] for k in keys} == {"tune", "experimental", "diag", "fault", "emul"}
+    assert {k["class"] for k in keys} == {"tune", "probe", "diag", "fault", "emul"}
     for k in keys:
         assert k["env"].startswith("GOL_") and t.get(k["key"]) == k["default"] and t.source(k["key"]) == "default"
-    # the probe-only and measured-slower switches are experimental-class
+    # the timing probes are probe-class; the measured-slower variants are gone
     cls = {k["key"]: k["class"] for k in keys}
-    for key in ("link_force", "flow", "resident", "split", "short", "pipe", "skew", "wpl", "pitch_pad"):
-        assert cls[key] == "experimental", key
+    for key in ("link_force", "pitch_pad"):
+        assert cls[key] == "probe", key
+    for gone in ("flow", "resident", "split", "short", "pipe", "skew", "wpl", "lds_add"):
+        assert gone not in cls, gone
 
 
 def test_precedence_default_env_set(native, monkeypatch):
@@ -70,15 +72,15 @@ def test_bad_settings_fail_loudly(native, monkeypatch):
         native.Tuning.from_env()
 
 
-def test_require_build_refuses_experimental_knobs(native):
-    t = native.Tuning()
-    t.require_build(False)  # defaults: fine
-    for k, v in (("flow", "1"), ("link_force", "1"), ("xlane", "1"), ("chain", "2"), ("pitch_pad", "256")):
-        bad = native.Tuning()
-        bad.set(k, v)
-        with pytest.raises(Exception, match="(?i)experimental"):
-            bad.require_build(False)
-        bad.require_build(True)
+def test_watchdog_accepts_fractional_seconds(native, monkeypatch):
+    """GOL_WATCHDOG_S is a number of seconds (0.5 was accepted
+    before the table was typed); a malformed value names its variable."""
+    monkeypatch.setenv("GOL_WATCHDOG_S", "0.5")
+    assert native.Tuning.from_env().get("watchdog_s") == "0.5"
+    Simulation(LifeConfig(64, 32), engine="cpu")  # a default EngineConfig reads it
+    monkeypatch.setenv("GOL_WATCHDOG_S", "soon")
+    with pytest.raises(Exception, match="GOL_WATCHDOG_S.*expected a number"):
+        native.Tuning.from_env()
 
 
 def test_config_tuning_reaches_engine_and_backend(native):
@@ -112,7 +114,7 @@ def test_an_explicit_backend_keeps_its_own_tuning(native):
 
 def test_knobs_are_read_in_one_place():
     """The framework reads its GOL_* knobs through Tuning::from_env only; the
-    remaining environment reads are the build (arch, experimental switch),
+    remaining environment reads are the build (arch, scheduler strategy),
     the module loader and the Python checkpoint writer's fault hook."""
     sites = []
     for p in list((REPO / "csrc").rglob("*.[ch]pp")) + list((REPO / "csrc").rglob("*.hip")):
@@ -142,6 +144,16 @@ def test_gol_cli_tune(gol_bin, tmp_path):
         assert r.returncode == 0, r.stderr
         outs.append((o.read_bytes(), r.stdout.split("Generations:")[-1].split()[0]))
     assert outs[0] == outs[1]
+    # --metrics-json stays valid JSON whatever text a string-valued key holds
+    # (trace paths with quotes or backslashes).
+    m = tmp_path / "m.json"
+    odd = 'x:/tmp/a"b\\c'
+    r = subprocess.run([str(gol_bin), "64", "64", "--random", "1", "--engine", "cpu", "--gens", "5",
+                        "--tune", f"wg_trace={odd}", "--metrics-json", str(m)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    rec = json.loads(m.read_text())
+    assert rec["tuning_changed"]["wg_trace"] == odd and odd in rec["tuning"]
 
 
 def test_python_cli_tune_help():
