@@ -252,7 +252,7 @@ def parse_args(argv=None):
     ap.add_argument("--tmax", type=int, default=0)
     ap.add_argument("--epoch", type=int, default=0)
     ap.add_argument("--poll", type=int, default=0)
-    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "edges"])
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "edges", "trigger"])
     ap.add_argument("--graphs", default="off", choices=["auto", "on", "off"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--repeats", type=int, default=1, help="timed repetitions (best is reported)")
@@ -563,7 +563,8 @@ def main() -> int:
                 "overlapped_halo_exchange": bool(rs and rs[-1].overlapped),
                 "overlap_mode": desc["overlap_mode"],
                 "overlap_trial_ms_per_epoch": {"plain": desc["overlap_trial_ms_plain"],
-                                               "early_boundary": desc["overlap_trial_ms_early"]},
+                                               desc["overlap_alternative"]: desc["overlap_trial_ms_early"]},
+                "triggered_sends": desc["triggered_sends"],
                 "graph_epochs": sum(r.graph_launches for r in rs),
                 "phase_ms_one_step": phases,
                 "verify": verify,

@@ -75,6 +75,14 @@ class Backend {
   }
   virtual void* stream_mark(void* /*from*/) { return nullptr; }
   virtual void stream_wait(void* /*on*/, void* /*mark*/) {}
+  // Boundary trigger (BlockArgs::trigger): makes `stream` wait until the
+  // groups of the last run_block that met the trigger rows have written
+  // them, without waiting for the rest of that launch.  Returns false when
+  // it did not arm (the backend could not count them): the caller then
+  // orders `stream` after the whole launch.  Synchronous backends never arm.
+  virtual bool supports_trigger() const { return false; }
+  virtual bool comm_wait_trigger(void* /*stream*/) { return false; }
+  virtual int64_t triggered() const { return 0; }  // waits armed so far (diagnostics)
   // A side stream for a termination poll that does not join the compute
   // streams: returned after it has been made to wait for everything enqueued
   // so far on every compute stream (a linked chain's second stream

@@ -47,13 +47,21 @@ struct EngineConfig {
   //      the flag all-reduce included, runs on the comm stream;
   //    2 edges: the edge strips are recomputed in scratch tiles while the
   //      interior runs (round 1; eight small launches per epoch);
+  //    3 trigger: the last temporal block of a full epoch runs as usual, but
+  //      its boundary groups count themselves done on a device counter
+  //      (Backend::comm_wait_trigger) and the comm stream, waiting on that
+  //      counter in the command processor, sends the new boundary rows while
+  //      the block's interior groups still run; the next epoch's first block
+  //      waits for their arrival.  No dual launch, no spinning consumer;
+  //      byte tiles on bit words included;
   //    0 off: everything on the compute stream;
-  //   -1 auto: where the early-boundary schedule applies (row strips with
-  //      an interior), the first epochs alternate the plain and the
-  //      early-boundary schedule, every rank times them with events, the
-  //      per-epoch medians are MAX-reduced over ranks, and all ranks keep the
-  //      faster one (GOL_OVERLAP_AUTO=plain|early forces the outcome after
-  //      the trial, for tests); elsewhere as off.
+  //   -1 auto: where an overlapped schedule applies (row strips), the first
+  //      epochs alternate the plain schedule and the alternative (trigger
+  //      where the backend supports it, else early boundary), every rank
+  //      times them with events, the per-epoch medians are MAX-reduced over
+  //      ranks, and all ranks keep the faster one (GOL_OVERLAP_AUTO=plain|
+  //      early|trigger forces the outcome after the trial, for tests);
+  //      elsewhere as off.
   int overlap = -1;
   // Check each termination poll one poll window later, so the host never
   // drains the device queue (stops are absorbing, so running past is exact).
@@ -145,13 +153,17 @@ class Engine {
   Extent cols() const { return dec_.cols(rank_); }
   int epoch_depth() const { return D_; }
   int tmax() const { return tmax_; }
-  bool overlap() const { return overlap_ || early_; }
+  bool overlap() const { return overlap_ || early_ || trigger_; }
   // "off" | "on" | "edges" | "auto:trial" | "auto:plain" | "auto:early".
   std::string overlap_mode() const;
-  // Median epoch time (ms, MAX over ranks) of the plain and the
-  // early-boundary schedule measured by the auto trial (-1: not measured).
+  // Median epoch time (ms, MAX over ranks) of the plain schedule and of the
+  // alternative the auto trial measured (-1: not measured), and the
+  // alternative's name ("trigger" or "early").
   double trial_ms_plain() const { return auto_ms_[0]; }
   double trial_ms_early() const { return auto_ms_[1]; }
+  std::string trial_alternative() const { return auto_alt_ == 3 ? "trigger" : "early"; }
+  // Epoch exchanges started by the boundary trigger so far (diagnostics).
+  int64_t triggered_sends() const { return triggered_sends_; }
   // Sample per-phase device times into RunResult (event pairs around every
   // kernel, exchange, fill and reduction; adds a little launch overhead).
   void set_phase_timing(bool on) { phase_timing_ = on; }
@@ -217,13 +229,14 @@ class Engine {
   // One temporal block in <in> -> <out> for generations (gen_base, gen_base+T];
   // returns the frame drift of the launch (cells).
   int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base,
-             void* stream = nullptr, int64_t dual_offset = 0, bool prio_boost = false);
+             void* stream = nullptr, int64_t dual_offset = 0, bool prio_boost = false,
+             const int64_t* trigger_rows = nullptr);
   void add_drift(int64_t cells);
   void exchange_columns(void* buf, const TileGeom& g);
   void halo_exchange_on(void* buf, const TileGeom& g);
   // Byte layout on bit words (EngineConfig::u8_compute = 1): one epoch on
   // the bit tile, and the per-run pack / unpack of the byte tile.
-  void epoch_via_bits(int64_t d);
+  void epoch_via_bits(int64_t d, bool sent_early);
   void pack_bits();
   void unpack_bits();
   void sync_bytes();  // unpack a live bit image into the byte tile (pack_bits in engine.cpp)
@@ -235,6 +248,11 @@ class Engine {
   void compute_after_comm();
   // Last block of a full epoch in the early-boundary schedule (engine.cpp).
   void last_block_early(int T);
+  // Last block of a full epoch in the trigger schedule, in -> out on tile g
+  // (the byte tile or its bit image); the caller flips its buffer parity.
+  void last_block_trigger(void* in, void* out, const TileGeom& g, int T);
+  // Schedule of the next epochs: 0 plain, 1 early boundary, 3 trigger.
+  void set_schedule(int s);
   // Waits for an early exchange still in flight; `invalidate` when the
   // buffers are about to change outside the schedule.
   void settle_pending(bool invalidate);
@@ -271,7 +289,9 @@ class Engine {
   void* colbuf_[4] = {nullptr, nullptr, nullptr, nullptr};  // send W, send E, recv W, recv E
   bool overlap_ = false;             // edge-scratch schedule (overlap = 2)
   bool early_ = false;               // early-boundary schedule (overlap = 1)
+  bool trigger_ = false;             // boundary-triggered sends (overlap = 3)
   bool comm_route_ = false;          // transport operations on the comm stream (multi-rank, overlap != 0)
+  int64_t triggered_sends_ = 0;
   bool send_next_ = false;           // the current epoch is followed by another one in this run
   bool rows_pending_ = false;        // halo rows of buf_[cur_] were sent early
   void* rows_arrived_ = nullptr;     // comm-stream mark: they have arrived
@@ -312,7 +332,8 @@ class Engine {
   // Overlap auto trial.
   bool auto_overlap_ = false;       // trial still running
   bool auto_decided_ = false;
-  int auto_sched_ = 0;              // schedule of the current epoch: 0 plain, 1 early
+  int auto_sched_ = 0;              // trial slot of the current epoch: 0 plain, 1 the alternative
+  int auto_alt_ = 1;                // the alternative: 1 early boundary, 3 trigger
   int64_t auto_full_epochs_ = 0;    // full epochs seen so far
   void* auto_open_ = nullptr;       // start mark of the current epoch
   int auto_open_sched_ = -1;        // its schedule (-1: not a trial epoch)

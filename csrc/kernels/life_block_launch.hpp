@@ -70,6 +70,23 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
     if (link) return false;  // the buffers moved under the previous launch: start a new chain
   }
   if (++L.seq == 0) L.seq = 1;
+  // Boundary trigger: count the groups meeting the trigger rows (the kernel
+  // adds one per such group when it publishes).
+  L.bnd_n = 0;
+  q.bnd_count = nullptr;
+  if (L.bnd_req && L.bnd_count) {
+    int64_t n = 0;
+    for (int g = 0; g < q.nseg; ++g) {
+      const int64_t e = q.row_lo + int64_t(g) * q.seg_rows + std::min(g, q.seg_rem) + q.seg_rows +
+                        (g < q.seg_rem ? 1 : 0);
+      const int64_t b = e - q.seg_rows - (g < q.seg_rem ? 1 : 0);
+      n += group_meets(b, e, L.bnd_r) ? 1 : 0;
+    }
+    L.bnd_n = n * q.ncolw;
+    q.bnd_count = L.bnd_count;
+    for (int i = 0; i < 4; ++i) q.bnd_r[i] = L.bnd_r[i];
+  }
+  L.bnd_req = false;
   q.link_flag = L.flags[L.seq % 3];
   q.link_seq = L.seq;
   hipStream_t st = L.stream[0];

@@ -486,9 +486,19 @@ void life_group_kernel(const LifeBlockParams p) {
       for (int i = 0; i < p.fault_delay; ++i) __builtin_amdgcn_s_sleep(127);
     __syncthreads();
     // One word per group: a folded block publishes each of its groups.
-    if (p.link_flag && m == 0 && lane < nsub && grp + lane < p.nseg)
+    if (p.link_flag && m == 0 && lane < nsub && grp + lane < p.nseg) {
       __hip_atomic_store(p.link_flag + (int64_t(kcol) * p.nseg + grp + lane), p.link_seq, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
+      // Boundary trigger: the rows were written through (sc1) and drained
+      // above; the counter is read by the command processor of another
+      // stream (hipStreamWaitValue64), hence system scope.
+      if (p.bnd_count) {
+        const int g = grp + lane;
+        const int64_t e = group_end(g), b = e - p.seg_rows - (g < p.seg_rem ? 1 : 0);
+        if (group_meets(b, e, p.bnd_r))
+          __hip_atomic_fetch_add(p.bnd_count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
   if (p.wg_trace) wg_trace_record(p.wg_trace, M, m, lane, t_start);
 }

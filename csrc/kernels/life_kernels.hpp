@@ -82,6 +82,12 @@ struct LifeBlockParams {
   // > 0: both launches cover the owned rows of a row ring of this many rows;
   // the rows a group reads beyond them wrap around the torus (link_wait).
   int64_t link_ring_rows;
+  // Boundary trigger (BlockArgs::trigger; linked launches only): after its
+  // link_flag store, every group whose output rows meet [bnd_r[0], bnd_r[1])
+  // or [bnd_r[2], bnd_r[3]) adds 1 to *bnd_count (system scope: a stream
+  // waits on it with hipStreamWaitValue64).  Null: off.
+  unsigned long long* bnd_count;
+  int64_t bnd_r[4];
   // Fault injection (GOL_FAULT_DELAY_SPINS, tests): producers at the torus
   // seam - a linked launch's first and last groups - sleep this many s_sleep 127
   // rounds (~3.4 us each) before publishing, so a missing dependency wait
@@ -132,7 +138,21 @@ struct LinkState {
   // (profiles/r04/linked_events_ab.jsonl).
   bool events = true;
   int chain = 0;  // launches in the current chain
+  // Boundary trigger of the next launch (BlockArgs::trigger): requested
+  // rows, the counter, and how many increments the launch will make
+  // (launch_linked sets it; 0: the launch could not carry the trigger).
+  bool bnd_req = false;
+  int64_t bnd_r[4] = {0, 0, 0, 0};
+  unsigned long long* bnd_count = nullptr;
+  int64_t bnd_n = 0;
 };
+
+// Groups of a grouped plan whose output rows meet the two trigger ranges,
+// counted per column strip (a folded strip publishes each of its groups
+// once, so the launch makes ncolw times this many increments).
+inline __host__ __device__ bool group_meets(int64_t g0, int64_t g1, const int64_t* r) {
+  return (g0 < r[1] && g1 > r[0]) || (g0 < r[3] && g1 > r[2]);
+}
 
 // Everything enqueued on stream[1] precedes what comes next on stream[0];
 // the next launch starts a new chain.

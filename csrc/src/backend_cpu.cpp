@@ -99,7 +99,21 @@ class CpuBackend final : public Backend {
     const std::string& ring = t.s("cpu_ring");
     ring_ = !ring.empty() && ring != "0";
     ring_fail_ = ring == "fail";  // tests: the mapping fails after the size check
+    trigger_ = t.on("cpu_trigger");
   }
+  // GOL_CPU_TRIGGER=1: the engine's boundary-trigger schedule (overlap =
+  // trigger) on the host.  Every operation completes in program order, so the
+  // boundary rows of a trigger launch are written when run_block returns and
+  // the wait is armed at once; the engine's bookkeeping (early sends, the
+  // arrival before the next epoch, the auto trial) is what this tests.
+  bool supports_trigger() const override { return trigger_; }
+  bool comm_wait_trigger(void*) override {
+    const bool armed = armed_;
+    armed_ = false;
+    triggered_ += armed;
+    return armed;
+  }
+  int64_t triggered() const override { return triggered_; }
   ~CpuBackend() override {
     for (auto& kv : rings_) ::munmap(kv.first, kv.second);
   }
@@ -224,11 +238,15 @@ class CpuBackend final : public Backend {
   bool drift_ = false;
   bool ring_ = false;      // GOL_CPU_RING
   bool ring_fail_ = false;  // GOL_CPU_RING=fail
+  bool trigger_ = false;    // GOL_CPU_TRIGGER
+  bool armed_ = false;      // the last run_block carried BlockArgs::trigger
+  int64_t triggered_ = 0;
   std::mutex ring_mu_;
   std::map<void*, size_t> rings_;  // row rings: base -> mapped bytes
 };
 
 int CpuBackend::run_block(const BlockArgs& a) {
+  armed_ = a.trigger && trigger_;
   if (a.dual_offset) {  // two row ranges: one block each, flags OR together
     BlockArgs b = a;
     b.dual_offset = 0;

@@ -106,6 +106,11 @@ class HipBackend final : public Backend {
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
     tune_.fault_delay = std::max(0, std::min(4096, t.i("fault_delay_spins")));
     tune_log_ = t.on("tune_log");
+    {
+      int wv = 0;
+      trigger_ok_ = hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, dev_) == hipSuccess && wv;
+      (void)hipGetLastError();
+    }
     tune_.chain_seq = &chain_seq_;
     // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words
     // (zeroed when allocated: flags and words are compared with sequence
@@ -154,6 +159,7 @@ class HipBackend final : public Backend {
     if (comm_) hipStreamSynchronize(comm_);
     for (auto& kv : rings_) release_ring(kv.second);
     if (stage_) hipFree(stage_);
+    if (trigger_mem_) hipFree(trigger_mem_);
     for (void* c : chain_)
       if (c) hipFree(c);
     for (auto& p : pending_) {
@@ -523,6 +529,22 @@ class HipBackend final : public Backend {
     }
     return side;
   }
+  // Boundary trigger (BlockArgs::trigger): `stream` waits, in the command
+  // processor, until the boundary groups of the last run_block have counted
+  // themselves done (hipStreamWaitValue64 on the cumulative counter).  False
+  // when that launch could not carry the trigger: the caller orders `stream`
+  // after the whole launch instead.
+  bool comm_wait_trigger(void* stream) override {
+    if (!trigger_target_ || !stream) return false;
+    GOL_ON_DEVICE();
+    HIP_CHECK(hipStreamWaitValue64(static_cast<hipStream_t>(stream), trigger_counter(), trigger_target_,
+                                   hipStreamWaitValueGte, ~0ull));
+    trigger_target_ = 0;
+    ++triggered_;
+    return true;
+  }
+  bool supports_trigger() const override { return trigger_ok_; }
+  int64_t triggered() const override { return triggered_; }
   // Marks come from a small ring of reusable timing-free events: a mark is
   // only waited on by the next few operations of an epoch.
   void* stream_mark(void* from) override {
@@ -576,6 +598,15 @@ class HipBackend final : public Backend {
     }
     ++launches_;
     hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
+    // Boundary trigger: armed only if the launch runs linked (the grouped
+    // kernel's publish path counts the boundary groups).
+    trigger_target_ = 0;
+    link_.bnd_n = 0;
+    link_.bnd_req = a.trigger && linkable && trigger_counter();
+    if (link_.bnd_req) {
+      for (int i = 0; i < 4; ++i) link_.bnd_r[i] = a.trigger_rows[i];
+      link_.bnd_count = trigger_counter();
+    }
     Pending* timed = nullptr;
     if (chain_mode_ < 0 && !linkable) timed = autotune_chain(a);
     if (linkable) tune_.chain = 0;
@@ -585,6 +616,11 @@ class HipBackend final : public Backend {
     if (prof_on_) prof_launch_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - l0).count();
     HIP_CHECK(hipGetLastError());
     if (timed) HIP_CHECK(hipEventRecord(timed->e1, s));
+    if (a.trigger && link_.bnd_n > 0) {  // the linked kernel carries the counter
+      trigger_total_ += uint64_t(link_.bnd_n);
+      trigger_target_ = trigger_total_;
+    }
+    link_.bnd_req = false;
     return drift;
   }
 
@@ -1000,6 +1036,25 @@ class HipBackend final : public Backend {
   int link_mode_ = -1;
   uint32_t chain_seq_ = 0;
   bool u8_pipe_ = true;  // GOL_U8_PIPE: T = 48 byte passes
+  // Boundary trigger: cumulative counter in signal memory (the command
+  // processor polls it), increments expected so far, and the target of the
+  // last armed launch (0: none pending).
+  unsigned long long* trigger_counter() {
+    if (!trigger_ok_) return nullptr;
+    if (!trigger_mem_) {
+      GOL_ON_DEVICE();
+      HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&trigger_mem_), sizeof(uint64_t),
+                                      hipMallocSignalMemory));
+      HIP_CHECK(hipMemsetAsync(trigger_mem_, 0, sizeof(uint64_t), stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      trigger_total_ = 0;
+    }
+    return trigger_mem_;
+  }
+  unsigned long long* trigger_mem_ = nullptr;
+  uint64_t trigger_total_ = 0, trigger_target_ = 0;
+  int64_t triggered_ = 0;
+  bool trigger_ok_ = false;
   int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, 2 timing probe, -1 autotuned per launch shape
   bool tune_log_ = false;
   std::map<TuneKey, TuneStats> tuned_;

@@ -310,6 +310,8 @@ PYBIND11_MODULE(_gol, m) {
       .def("overlap_mode", &Engine::overlap_mode)
       .def_property_readonly("trial_ms_plain", &Engine::trial_ms_plain)
       .def_property_readonly("trial_ms_early", &Engine::trial_ms_early)
+      .def("trial_alternative", &Engine::trial_alternative)
+      .def("triggered_sends", &Engine::triggered_sends)
       .def_property("phase_timing", &Engine::phase_timing, &Engine::set_phase_timing)
       .def("graphs", &Engine::graphs)
       .def_property("generation", &Engine::generation, &Engine::set_generation)

@@ -188,13 +188,18 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   overlap_ = row_exchange && cfg_.overlap == 2 && interior && !via_bits_;
   const bool early_ok = row_exchange && dec_.Px == 1 && interior && !via_bits_;
   early_ = early_ok && cfg_.overlap == 1;
+  // Boundary-triggered sends (overlap = 3; last_block_trigger): row strips
+  // on a backend that can count boundary groups done.  Byte tiles on bit
+  // words too: the trigger runs on the bit image.
+  const bool trigger_ok = row_exchange && dec_.Px == 1 && be_->supports_trigger();
+  trigger_ = trigger_ok && cfg_.overlap == 3;
   // With the early-boundary schedule every transport operation runs on the
   // comm stream (one stream per communicator, in issue order), so the flag
   // all-reduce of a poll runs beside the compute stream.  Not by default: in
   // the one-GPU RCCL rehearsal each cross-stream event hop around an exchange
   // cost more than the all-reduce it takes off the compute stream
   // (profiles/r02/rehearsal_overlap.jsonl).
-  comm_route_ = early_;
+  comm_route_ = early_ || trigger_;
   if (overlap_) {
     gs_ = TileGeom::make(cfg_.layout, D_, g_.W, D_, g_.hw);
     GOL_REQUIRE(gs_.pitch == g_.pitch, "edge scratch pitch mismatch");
@@ -205,12 +210,16 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
-  if (use_graphs_) early_ = comm_route_ = false;  // captured epochs stay on one stream
+  if (use_graphs_) early_ = trigger_ = comm_route_ = false;  // captured epochs stay on one stream
   // Overlap auto: measure both schedules on the real ranks (see auto_choose).
   // The one-GPU RCCL rehearsal measured the early-boundary schedule slower
   // (profiles/r02/rehearsal_overlap.jsonl), but it has no xGMI latency in it;
   // on a multi-GPU node the decision is taken from the node itself.
-  auto_overlap_ = cfg_.overlap == -1 && early_ok && !use_graphs_;
+  // The alternative measured against the plain schedule: the trigger where
+  // it applies (no dual launch, no cross-stream hop before the send), else
+  // the early-boundary schedule.
+  auto_overlap_ = cfg_.overlap == -1 && (early_ok || trigger_ok) && !use_graphs_;
+  auto_alt_ = trigger_ok ? 3 : 1;
   // Side polls: with a transport whose flag reduction has its own
   // communicator (RCCL), a poll's all-reduce and D2H copy run on the comm
   // stream after a mark on the compute stream, which never waits for them:
@@ -512,16 +521,20 @@ void* Engine::bit_scratch(int i) const {
 // bit_scratch(bpar_) when a run starts and unpacks it when the run ends): the
 // halo exchange or fill and every temporal block run on the bit tile, whose
 // per-generation flags are those of the same cells.
-void Engine::epoch_via_bits(int64_t d) {
+void Engine::epoch_via_bits(int64_t d, bool sent_early) {
   trace::Range tr("gol.epoch_via_bits");
-  halo_exchange_on(bit_scratch(bpar_), gb_);
+  if (!sent_early) halo_exchange_on(bit_scratch(bpar_), gb_);
   // A partial epoch's trapezoid starts d rows outside the owned rows; a row
   // ring's blocks all cover exactly the owned rows (a = Dv - T).
+  const bool full = d == D_;
   int64_t a = D_ - d;
   while (d > 0) {
     const int T = pick_T(d);
     if (rows_ring_) a = gb_.Dv - T;
-    add_drift(launch(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
+    if (d == T && trigger_ && send_next_ && full)
+      last_block_trigger(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T);
+    else
+      add_drift(launch(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
     bpar_ ^= 1;
     gen_ += T;
     a += T;
@@ -558,10 +571,6 @@ void Engine::unpack_bits() {
 }
 
 void Engine::run_epoch(int64_t d) {
-  if (via_bits_) {
-    epoch_via_bits(d);
-    return;
-  }
   if (overlap_) {
     epoch_overlapped(d);
     return;
@@ -575,6 +584,10 @@ void Engine::run_epoch(int64_t d) {
   }
   // The previous epoch ends here (its early rows have arrived).
   if (auto_overlap_) auto_mark();
+  if (via_bits_) {
+    epoch_via_bits(d, sent_early);
+    return;
+  }
   if (!sent_early) halo_exchange();
   // A partial epoch (d < D) needs only d halo rows: its trapezoid starts d
   // rows outside the owned rows, not D.
@@ -583,10 +596,15 @@ void Engine::run_epoch(int64_t d) {
   while (d > 0) {
     const int T = pick_T(d);
     if (rows_ring_) a = g_.Dv - T;  // every block covers exactly the owned rows
-    if (d == T && early_ && send_next_ && full)
+    if (d == T && early_ && send_next_ && full) {
       last_block_early(T);
-    else
+    } else if (d == T && trigger_ && send_next_ && full) {
+      last_block_trigger(buf_[cur_], buf_[cur_ ^ 1], g_, T);
+      cur_ ^= 1;
+      gen_ += T;
+    } else {
       step_block(T, a + T, g_.R() - a - T);
+    }
     a += T;
     d -= T;
   }
@@ -669,8 +687,61 @@ void Engine::last_block_early(int T) {
   gen_ += T;
 }
 
+// Trigger schedule (overlap = 3; Py > 1 or the one-rank RCCL rehearsal, Px
+// == 1, columns wrapped).  The reference exchanges halos and then waits
+// (MPI_Startall + MPI_Waitall before evolve, src/game_mpi.c:392-403).  Here
+// the last temporal block of a full epoch writes exactly the owned rows, and
+// the next epoch's halos are the first and last Dv of them.  That block runs
+// as one ordinary (linked) launch whose groups meeting those rows count
+// themselves done on a device counter once their rows are written through;
+// the comm stream waits on the counter in the command processor
+// (Backend::comm_wait_trigger) and sends the rows while the block's interior
+// groups still run.  The next epoch's first block waits for the arrival mark
+// (run_epoch).  Nothing spins: no kernel waits on the exchange, and the send
+// waits only on work already running.
+void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
+  trace::Range tr("gol.last_block_trigger");
+  const int64_t Dv = g.Dv, H = g.H, pitch = g.pitch;
+  const int64_t rows[4] = {Dv, 2 * Dv, H, H + Dv};
+  add_drift(launch(in, out, g, T, Dv, Dv + H, gen_, nullptr, 0, false, rows));
+  if (cols_filled_ && H > 2 * Dv) {  // column halos of the rows that are not sent, on the compute stream
+    void* t = phase_begin(nullptr);
+    be_->fill_cols_rows(out, g, 2 * Dv, H - 2 * Dv);
+    phase_end(kFill, t, nullptr);
+  }
+  void* comm = be_->comm_stream();
+  if (be_->comm_wait_trigger(comm))
+    ++triggered_sends_;
+  else
+    be_->stream_wait(comm, be_->stream_mark(nullptr));  // not armed: after the whole block
+  if (cols_filled_) {  // the sent rows carry their column halos
+    void* t = phase_begin(comm);
+    be_->fill_cols_rows(out, g, Dv, std::min(Dv, H), comm);
+    if (H > Dv) be_->fill_cols_rows(out, g, std::max(H, 2 * Dv), Dv + H - std::max(H, 2 * Dv), comm);
+    phase_end(kFill, t, comm);
+  }
+  auto* base = static_cast<uint8_t*>(out);
+  auto nb = dec_.neighbors(rank_);
+  const size_t bytes = size_t(Dv * pitch);
+  std::vector<P2POp> ops = {
+      {true, nb[kNorth], base + Dv * pitch, bytes},        // my top rows -> north's bottom halo
+      {false, nb[kSouth], base + (Dv + H) * pitch, bytes},  // south's top rows -> my bottom halo
+      {true, nb[kSouth], base + H * pitch, bytes},          // my bottom rows -> south's top halo
+      {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
+  };
+  void* tx = phase_begin(comm);
+  tr_->exchange(ops, comm ? comm : be_->stream());
+  phase_end(kHalo, tx, comm);
+  rows_arrived_ = comm ? be_->stream_mark(comm) : nullptr;
+  rows_pending_ = true;
+  halo_bytes_ += 2 * int64_t(bytes);
+  ++exchanges_;
+  ++early_sends_;
+}
+
 int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
-                   int64_t gen_base, void* stream, int64_t dual_offset, bool prio_boost) {
+                   int64_t gen_base, void* stream, int64_t dual_offset, bool prio_boost,
+                   const int64_t* trigger_rows) {
   BlockArgs a;
   a.in = in;
   a.out = out;
@@ -695,8 +766,14 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   a.stream = stream;
   // Linked launches assume the device to themselves: not while transport
   // work may run beside them on the comm stream (early-boundary schedule,
-  // side polls).
-  a.link = link_ && !early_ && !comm_route_ && !poll_side_;
+  // side polls).  The trigger schedule links: its sends start only once the
+  // boundary groups are done, and the launch after them (the next epoch's
+  // first block) waits for their arrival and starts a new chain.
+  a.link = link_ && !early_ && !poll_side_ && (!comm_route_ || trigger_);
+  if (trigger_rows) {
+    a.trigger = true;
+    for (int i = 0; i < 4; ++i) a.trigger_rows[i] = trigger_rows[i];
+  }
   a.ring = rows_ring_;
   a.dual_offset = dual_offset;
   a.prio_boost = prio_boost;
@@ -996,8 +1073,14 @@ void Engine::auto_choose(bool full_epoch) {
       trial = sched;
     }
   }
-  early_ = comm_route_ = sched == 1;
+  set_schedule(sched == 1 ? auto_alt_ : 0);
   auto_sched_ = trial;
+}
+
+void Engine::set_schedule(int s) {
+  early_ = s == 1;
+  trigger_ = s == 3;
+  comm_route_ = early_ || trigger_;
 }
 
 void Engine::auto_mark() {
@@ -1041,11 +1124,14 @@ void Engine::auto_decide() {
   be_->copy_d2h(v, dev, sizeof(v));
   auto_ms_[0] = v[0] * 1e-4;
   auto_ms_[1] = v[1] * 1e-4;
-  bool early = double(v[1]) < 0.98 * double(v[0]);
+  bool alt = double(v[1]) < 0.98 * double(v[0]);
   const std::string& forced = cfg_.tune.s("overlap_auto");  // fault injection (tests)
-  if (forced == "early") early = true;
-  if (forced == "plain") early = false;
-  early_ = comm_route_ = early;
+  if (forced == "early" || forced == "trigger") alt = true;
+  if (forced == "plain") alt = false;
+  GOL_REQUIRE(forced.empty() || forced == "plain" || forced == (auto_alt_ == 3 ? "trigger" : "early"),
+              "tuning overlap_auto=" + forced + ": this tile's alternative schedule is " +
+                  (auto_alt_ == 3 ? "trigger" : "early"));
+  set_schedule(alt ? auto_alt_ : 0);
   auto_overlap_ = false;
   auto_decided_ = true;
 }
@@ -1053,9 +1139,10 @@ void Engine::auto_decide() {
 std::string Engine::overlap_mode() const {
   if (overlap_) return "edges";
   if (cfg_.overlap == 1) return early_ ? "on" : "off";
+  if (cfg_.overlap == 3) return trigger_ ? "trigger" : "off";
   if (cfg_.overlap == -1) {
     if (auto_overlap_) return "auto:trial";
-    if (auto_decided_) return early_ ? "auto:early" : "auto:plain";
+    if (auto_decided_) return early_ ? "auto:early" : trigger_ ? "auto:trigger" : "auto:plain";
   }
   return "off";
 }

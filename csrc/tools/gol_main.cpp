@@ -100,10 +100,12 @@ struct Options {
                "                              has a GPU of its own, else thread)\n"
                "  --decomp auto|PxQ           process grid (Px columns x Py rows)\n"
                "  --tmax T --epoch D --poll N temporal block, halo depth, poll interval\n"
-               "  --overlap auto|on|off|edges on = early boundary rows sent while the interior\n"
-               "                              computes; edges = recomputed edge strips; off = no\n"
-               "                              overlap; auto = time plain and early epochs on the\n"
-               "                              ranks and keep the faster (row strips only)\n"
+               "  --overlap auto|on|off|edges|trigger\n"
+               "                              trigger = an epoch's new boundary rows are sent as soon\n"
+               "                              as the groups writing them finish; on = early boundary\n"
+               "                              strips in a launch of their own; edges = recomputed edge\n"
+               "                              strips; off = no overlap; auto = time plain against\n"
+               "                              trigger (or early) epochs on the ranks, keep the faster\n"
                "  --graphs auto|on|off        replay full epochs as captured HIP graphs\n"
                "  --threads N                 host threads for the cpu engine\n"
                "  --tune KEY=VALUE            runtime tuning (repeatable; --tune help lists the keys,\n"
@@ -166,7 +168,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--poll" || a == "--poll-every") o.poll = std::atoi(next().c_str());
     else if (a == "--overlap") {
       std::string v = next();
-      o.overlap = v == "on" ? 1 : v == "off" ? 0 : v == "edges" ? 2 : -1;
+      o.overlap = v == "on" ? 1 : v == "off" ? 0 : v == "edges" ? 2 : v == "trigger" ? 3 : -1;
     } else if (a == "--graphs") {
       std::string v = next();
       o.graphs = v == "on" ? 1 : v == "off" ? 0 : -1;

@@ -41,7 +41,7 @@ def parse_args(argv=None):
                    help="generations per halo exchange (deep halo depth)")
     p.add_argument("--poll", "--poll-every", dest="poll", type=int, default=0,
                    help="generations between termination polls")
-    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "edges"],
+    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "edges", "trigger"],
                    help="on = early boundary rows sent while the interior computes; edges = recomputed "
                         "edge strips; off = no overlap; auto = time plain and early epochs on the ranks "
                         "and keep the faster one (row strips only)")

@@ -197,13 +197,17 @@ def test_phase_times_with_ranks(native):
     assert (grp.gather() == want).all()
 
 
-@pytest.mark.parametrize("pick", ["plain", "early", ""])
+@pytest.mark.parametrize("pick,alt", [("plain", "early"), ("early", "early"), ("", "early"), ("plain", "trigger"),
+                                      ("trigger", "trigger"), ("", "trigger")])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_overlap_auto_trial_is_exact(native, monkeypatch, pick, layout):
-    """Trial epochs alternate the schedules (early-boundary sends included),
-    then every rank keeps the decided one; forced either way (and measured)
-    the final grid and Generations equal the serial loop's."""
+def test_overlap_auto_trial_is_exact(native, monkeypatch, pick, alt, layout):
+    """Trial epochs alternate the plain schedule and the alternative (the
+    boundary trigger where the backend supports it - the CPU backend with
+    cpu_trigger - else early boundary), then every rank keeps the decided
+    one; forced either way (and measured) the final grid and Generations
+    equal the serial loop's."""
     monkeypatch.setenv("GOL_OVERLAP_AUTO", pick)
+    monkeypatch.setenv("GOL_CPU_TRIGGER", "1" if alt == "trigger" else "0")
     W, H, gens = 256, 3 * 200, 700
     g = random_grid(W, H, 7)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x3", layout=layout, tmax=8, epoch=32,
@@ -216,10 +220,13 @@ def test_overlap_auto_trial_is_exact(native, monkeypatch, pick, layout):
     if pick:
         assert mode == f"auto:{pick}"
     else:
-        assert mode in ("auto:plain", "auto:early")
+        assert mode in ("auto:plain", f"auto:{alt}")
     d = grp.sims[0].describe()
+    assert d["overlap_alternative"] == alt
     assert d["overlap_trial_ms_plain"] > 0 and d["overlap_trial_ms_early"] > 0
-    assert all(r.overlapped for r in reps)  # the trial ran early-boundary epochs
+    assert all(r.overlapped for r in reps)  # the trial ran epochs of the alternative
+    if alt == "trigger":
+        assert d["triggered_sends"] > 0
     want, _, _ = reference_run(g, gens, check_similarity=False)
     assert (grp.gather() == want).all()
 

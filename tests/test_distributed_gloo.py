@@ -82,3 +82,23 @@ def test_bench_cpu_dry_run_two_ranks(native, tmp_path):
     assert cfg["step_stop_reasons"] == ["limit"]
     assert cfg["exchanges_per_step"] >= 1 and cfg["polls_per_step"] >= 1
     assert abs(rec["value"] - 256 * 256 * 300 / (rec["ms_per_step"] * 3e-3)) < 1e-6 * rec["value"]
+
+
+@pytest.mark.parametrize("nproc,layout", [(2, "bits"), (4, "u8")])
+def test_torchrun_trigger_schedule_matches_serial(native, tmp_path, nproc, layout):
+    """The boundary-trigger schedule (overlap trigger: each epoch's new
+    boundary rows sent as soon as the groups writing them are done) across
+    real rank processes over gloo, the CPU backend emulating the device
+    counter (tuning cpu_trigger): byte-identical output and Generations."""
+    W, H = 128, 160
+    g = random_grid(W, H, 47)
+    inp = tmp_path / "in.txt"
+    io.write_grid(str(inp), g)
+    r = _torchrun(nproc, ["-m", "gol_amd", str(W), str(H), str(inp), "--engine", "cpu", "--gens", "300",
+                          "--decomp", f"1x{nproc}", "--layout", layout, "--comm", "torch", "--epoch", "8",
+                          "--tmax", "4", "--overlap", "trigger", "--tune", "cpu_trigger=1",
+                          "--output", str(tmp_path / "out.txt"), "--style", "mpi"], tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ref, gens, _ = reference_run(g, 300)
+    assert f"Generations:\t{gens}" in r.stdout
+    assert (tmp_path / "out.txt").read_text() == io.format_text(ref)

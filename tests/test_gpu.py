@@ -455,7 +455,7 @@ def test_termination_gpu(gpu, W, H, seed, density):
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("2x2", 4), ("2x4", 8), ("3x3", 9)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-@pytest.mark.parametrize("overlap", ["off", "on", "edges"])
+@pytest.mark.parametrize("overlap", ["off", "on", "edges", "trigger"])
 def test_multi_subdomain_one_gpu(gpu, tune, spec, P, layout, overlap):
     W, H = 32 * 12, 300
     g = random_grid(W, H, 42)
@@ -465,7 +465,8 @@ def test_multi_subdomain_one_gpu(gpu, tune, spec, P, layout, overlap):
     grp.load(g)
     reps = grp.run()
     assert all(r.generations == 150 for r in reps)
-    assert all(r.overlapped == (overlap == "edges" or (overlap == "on" and spec.startswith("1x"))) for r in reps)
+    assert all(r.overlapped == (overlap == "edges" or (overlap in ("on", "trigger") and spec.startswith("1x")))
+               for r in reps)
     assert (grp.gather() == want).all()
 
 
@@ -516,7 +517,7 @@ def test_rccl_single_rank_self_exchange(gpu, tune):
     assert flags.tolist() == [3, 0, 7]
 
 
-@pytest.mark.parametrize("overlap,side", [("off", "1"), ("off", "0"), ("on", "1"), ("edges", "1")])
+@pytest.mark.parametrize("overlap,side", [("off", "1"), ("off", "0"), ("on", "1"), ("edges", "1"), ("trigger", "0")])
 @pytest.mark.parametrize("xlane", [0, -1])
 def test_rccl_self_exchange_rehearsal(gpu, tune, overlap, side, xlane):
     """The multi-rank row-strip schedule on one GPU (bench.py --rehearse-rccl):
@@ -986,3 +987,34 @@ def test_rank_tile_links_only_without_comm_stream_work(gpu, tune, overlap):
     else:
         assert rep.linked_launches == 0 and rep.overlapped
     assert (sim.tile() == life_step_torch(g, 600, device="cuda")).all()
+
+
+@pytest.mark.parametrize("layout,delay", [("bits", "0"), ("bits", "300"), ("u8", "0")])
+def test_rank_tile_trigger_schedule(gpu, tune, layout, delay):
+    """The boundary-trigger schedule on the 8-GPU rank tile (32768 x 4096,
+    multi-rank epochs against a 1-rank RCCL communicator): the last block of
+    every full epoch is a linked launch whose boundary groups count
+    themselves done on a device counter, the comm stream waits on it
+    (hipStreamWaitValue64) and sends the rows while the interior groups run.
+    With GOL_FAULT_DELAY_SPINS the first and last groups - exactly the
+    boundary groups - publish ~1 ms late, so a send that did not wait for
+    them would ship the previous generation.  Byte tiles run it on their bit
+    image.  Exact against the fp32 oracle."""
+    tune.pop("u8_via_bits", None)
+    tune["fault_delay_spins"] = delay
+    C = gpu
+    W, H = 32768, 4096
+    g = random_grid(W, H, 23)
+    gens = 600  # two full epochs followed by another: two triggered sends
+    want = life_step_torch(g, gens, device="cuda")
+    tr = C.rccl_transport(C.rccl_unique_id(), 0, 1, 0, tune=make_tuning(tune))
+    sim = Simulation(LifeConfig(W, H, layout=layout, gen_limit=gens, self_exchange=True, overlap="trigger",
+                                tune=tune),
+                     transport=tr, backend=C.hip_backend(0, tune=make_tuning(tune)))
+    d = sim.describe()
+    assert d["overlap_mode"] == "trigger" and d["epoch"] == 256
+    sim.load(g)
+    rep = sim.advance(gens)
+    assert rep.overlapped and rep.linked_launches > 0
+    assert sim.native_engine.triggered_sends() == 2
+    assert (sim.tile() == want).all()

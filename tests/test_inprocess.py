@@ -60,14 +60,19 @@ def test_random_init_decomposition_independent(native, tune):
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x3", 3), ("2x2", 4), ("2x3", 6)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("tmax,epoch", [(4, 8), (8, 8), (4, 12), (2, 5)])
-@pytest.mark.parametrize("mode", ["on", "edges"])
+@pytest.mark.parametrize("mode", ["on", "edges", "trigger"])
 def test_overlapped_exchange_matches_serial(native, tune, spec, P, layout, tmax, epoch, mode):
     """Overlapped epochs are bit-identical to the serial reference, including
     a short final epoch (gens not a multiple of the epoch depth):
-      on     early boundary rows: the last block of an epoch computes the 2D
-             boundary rows, sends them, then computes the interior (row
-             strips only, Px == 1);
-      edges  interior during the row exchange, edge strips in scratch tiles."""
+      on       early boundary rows: the last block of an epoch computes the 2D
+               boundary rows, sends them, then computes the interior (row
+               strips only, Px == 1);
+      edges    interior during the row exchange, edge strips in scratch tiles;
+      trigger  the last block's boundary rows are sent once the groups
+               writing them are done (row strips; the CPU backend emulates
+               the counter, tuning cpu_trigger)."""
+    if mode == "trigger":
+        tune["cpu_trigger"] = "1"
     W, H = 192, 150
     g = random_grid(W, H, 77 + tmax)
     gens = 3 * epoch + epoch // 2 + 1
@@ -78,13 +83,16 @@ def test_overlapped_exchange_matches_serial(native, tune, spec, P, layout, tmax,
     reps = grp.run()
     want = mode == "edges" or spec.startswith("1x")
     assert all(r.overlapped == want for r in reps)
+    if mode == "trigger":
+        assert all(s.native_engine.triggered_sends() == (3 if want else 0) for s in grp.sims)
     assert (grp.gather() == ref).all()
 
 
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
 @pytest.mark.parametrize("lagged", [True, False])
-@pytest.mark.parametrize("mode", ["on", "edges"])
+@pytest.mark.parametrize("mode", ["on", "edges", "trigger"])
 def test_overlapped_termination(native, tune, W, H, seed, density, lagged, mode):
+    tune["cpu_trigger"] = "1"
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
     cfg = LifeConfig(W, H, decomp="1x2", layout="u8", tmax=2, epoch=3, poll_gens=4, overlap=mode,
@@ -93,7 +101,8 @@ def test_overlapped_termination(native, tune, W, H, seed, density, lagged, mode)
     grp.load(g)
     reps = grp.run()
     assert {r.generations for r in reps} == {rgens}
-    assert all(r.overlapped == (H // 2 >= 7 and r.executed > 3) for r in reps)
+    # The trigger needs no interior (H > 2D): only a second epoch in the run.
+    assert all(r.overlapped == ((H // 2 >= 7 or mode == "trigger") and r.executed > 3) for r in reps)
     assert (grp.gather() == ref).all()
 
 
@@ -110,6 +119,11 @@ def test_overlap_modes(native, tune):
     assert not ov() and not ov(overlap="off")
     assert not ov(H=40, overlap="on")  # tile rows 20 <= 2D
     assert not ov(decomp="2x1", overlap="on")
+    # trigger: row strips on a backend that counts boundary groups done
+    assert not ov(overlap="trigger")
+    tune["cpu_trigger"] = "1"
+    assert ov(overlap="trigger") and ov(H=40, overlap="trigger")
+    assert not ov(decomp="2x1", overlap="trigger")
 
 
 @pytest.mark.parametrize("lagged", [True, False])
