@@ -266,7 +266,8 @@ def parse_args(argv=None):
                     help="after the timed steps, run G more generations and check them against the fp32 "
                          "PyTorch oracle and the u8 layout (0: skip)")
     ap.add_argument("--verify-bands", action="store_true",
-                    help="check on row bands read from the device even below 2^30 cells (one rank; tests)")
+                    help="check on row bands read from the device even below the whole-grid limits "
+                         "(one rank: torus bands; several: each rank's own bands, cones from its neighbours)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="runtime tuning (repeatable; python -m gol_amd.cli --tune help lists the keys)")
     ap.add_argument("--no-phase-step", action="store_true",
@@ -458,10 +459,25 @@ def main() -> int:
                   "final_sha256": digest, "digest_of": "the checked row bands",
                   "vs_torch_fp32_oracle": ok_torch, "vs_u8_layout": None,
                   "seconds": round(time.perf_counter() - t_v, 2)}
+    elif a.verify > 0 and (S * Hg > VERIFY_MAX_CELLS or a.verify_bands) and eng.decomp.Px == 1:
+        # Several ranks, a grid no host holds whole (BASELINE config 5): every
+        # rank checks row bands of its own tile, the light-cone rows beyond it
+        # sent by its neighbours - no gather (parallel/dist.py verify_row_bands).
+        from gol_amd.parallel.dist import verify_row_bands  # noqa: PLC0415
+
+        t_v = time.perf_counter()
+        g_snap = sim.generation
+        vb = verify_row_bands(sim, a.verify, ORACLE_BAND_ROWS, device="cuda" if on_gpu else "cpu")
+        verified = vb["ok"]
+        verify = {"generations": vb["generations"], "from_generation": int(g_snap), "stop_reason": vb["stop_reason"],
+                  "oracle": f"{vb['bands_per_rank']} row bands of {vb['band_rows']} per rank (top, middle, bottom "
+                            f"of each tile), light cones of {vb['cone_rows']} rows from the neighbours; no gather",
+                  "vs_torch_fp32_oracle": vb["ok"], "vs_u8_layout": None,
+                  "seconds": round(time.perf_counter() - t_v, 2)}
     elif a.verify > 0 and S * Hg > VERIFY_MAX_CELLS:
-        # Several ranks: gathering the grid for the check would not fit.
-        log(f"bench.py: --verify skipped: {S}x{Hg} on {world} ranks exceeds {VERIFY_MAX_CELLS} cells")
-        verify = {"skipped": f"grid beyond {VERIFY_MAX_CELLS} cells on several ranks"}
+        # Several ranks in a 2-D decomposition: gathering the grid would not fit.
+        log(f"bench.py: --verify skipped: {S}x{Hg} on {world} ranks exceeds {VERIFY_MAX_CELLS} cells (2-D tiles)")
+        verify = {"skipped": f"grid beyond {VERIFY_MAX_CELLS} cells on a 2-D decomposition"}
     elif a.verify > 0:
         from gol_amd.ops.life_ops import life_step_torch_roll  # noqa: PLC0415
         from gol_amd.parallel.dist import gather_grid  # noqa: PLC0415

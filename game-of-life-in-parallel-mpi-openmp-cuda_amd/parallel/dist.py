@@ -215,3 +215,106 @@ def gather_grid(sim, group=None):
     for (a, b, c, d), t in zip(exts, parts):
         out[a:b, c:d] = t[: b - a, : d - c].cpu().numpy()
     return out
+
+
+def band_starts_local(rows: int, band_rows: int) -> list[int]:
+    """First local rows of a rank's check bands: its top, middle and bottom
+    rows (the top and bottom bands sit on the rows the halo exchange feeds)."""
+    b = min(band_rows, rows)
+    return sorted({0, max(0, rows // 2 - b // 2), rows - b})
+
+
+def verify_row_bands(sim, gens: int, band_rows: int = 128, device: str = "cpu", group=None,
+                     after_snapshot=None) -> dict:
+    """Check the next `gens` generations of a multi-rank run on row bands of
+    every rank's own tile, with no gather: the multi-rank counterpart of
+    bench.py's single-rank band check, for grids no host can hold whole
+    (BASELINE config 5: 2^40 cells over 8 ranks).
+
+    Row strips (Px == 1, the default decomposition): each rank snapshots, for
+    each of its bands (top, middle, bottom rows of its tile), the band plus
+    `gens` rows of light cone on each side.  Cone rows beyond its tile come
+    from its neighbours: before the run every rank sends its top `gens` rows
+    north and its bottom `gens` rows south (one batched send/recv pair each
+    way over the process group, RCCL on GPU, gloo on CPU).  After the
+    collective run of `gens` generations each rank compares its bands, read
+    straight from the device (Engine.store_rows), with the fp32 oracle on the
+    cone (ops.life_ops.life_step_torch_roll; columns wrap, the cone's own row
+    wrap only corrupts rows that are dropped), and the verdict is the AND
+    over ranks.  Nothing larger than (band + 2 gens) rows of one rank's
+    width is ever copied to a host.  The reference checks nothing of the
+    kind; its collective variants gather the whole grid to write it
+    (src/game_mpi_collective.c:331-361).  `after_snapshot(sim)` (tests) runs
+    between the snapshots and the run: a corrupted cell there must fail."""
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+
+    from ..ops.life_ops import life_step_torch_roll  # noqa: PLC0415
+
+    eng = sim.native_engine
+    dec = eng.decomp
+    rank = sim.rank
+    if dec.Px != 1:
+        raise ValueError("verify_row_bands: row strips only (Px == 1)")
+    r0, r1 = sim.rows
+    ht = r1 - r0
+    G = int(gens)
+    comm_dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    # The shortest tile bounds the cone: a neighbour must hold G rows.
+    hmin = torch.tensor([ht], dtype=torch.int64, device=comm_dev)
+    dist.all_reduce(hmin, op=dist.ReduceOp.MIN, group=group)
+    if G > int(hmin.item()):
+        raise ValueError(f"verify_row_bands: {G} generations of light cone exceed a {int(hmin.item())}-row tile")
+    b = min(band_rows, ht)
+    starts = band_starts_local(ht, band_rows)
+    nb = dec.neighbors(rank)
+    north, south = int(nb[0]), int(nb[1])
+    W = sim.config.width
+
+    def rows(lo: int, n: int) -> np.ndarray:
+        return eng.store_rows(lo, n) if n > 0 else np.zeros((0, W), np.uint8)
+
+    # Cone rows of the neighbours, in issue order on every rank: sends top ->
+    # north, bottom -> south; receives from south (its top rows, below mine),
+    # then from north (its bottom rows) - so two ranks that are each other's
+    # north and south (Py == 2) still pair the right messages.
+    send_top = torch.from_numpy(np.ascontiguousarray(rows(0, G))).to(comm_dev)
+    send_bot = torch.from_numpy(np.ascontiguousarray(rows(ht - G, G))).to(comm_dev)
+    from_south = torch.empty((G, W), dtype=torch.uint8, device=comm_dev)
+    from_north = torch.empty((G, W), dtype=torch.uint8, device=comm_dev)
+    ops = [dist.P2POp(dist.isend, send_top, north, group), dist.P2POp(dist.isend, send_bot, south, group),
+           dist.P2POp(dist.irecv, from_south, south, group), dist.P2POp(dist.irecv, from_north, north, group)]
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    above, below = from_north.cpu().numpy(), from_south.cpu().numpy()
+    del send_top, send_bot, from_south, from_north
+
+    def cone(s: int) -> np.ndarray:
+        """Snapshot of local rows [s - G, s + b + G), neighbours' rows where
+        they fall outside the tile."""
+        lo, hi = s - G, s + b + G
+        parts = []
+        if lo < 0:
+            parts.append(above[G + lo:])
+        parts.append(rows(max(lo, 0), min(hi, ht) - max(lo, 0)))
+        if hi > ht:
+            parts.append(below[:hi - ht])
+        return np.concatenate(parts, axis=0)
+
+    snaps = [cone(s) for s in starts]
+    if after_snapshot is not None:
+        after_snapshot(sim)
+    g0 = sim.generation
+    rv = eng.run_until(g0 + G)
+    done = sim.generation - g0
+    ok = True
+    for s, snap in zip(starts, snaps):
+        c = snap[G - done:G + b + done]  # a run that stopped early ran `done` generations
+        want = life_step_torch_roll(c, done, device=device)[done:done + b]
+        ok = ok and bool(np.array_equal(rows(s, b), want))
+        del want, c
+    del snaps
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=comm_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return {"ok": bool(flag.item()), "generations": int(done), "stop_reason": rv.stop_reason,
+            "bands_per_rank": len(starts), "band_rows": b, "cone_rows": G}

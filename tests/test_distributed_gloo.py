@@ -102,3 +102,57 @@ def test_torchrun_trigger_schedule_matches_serial(native, tmp_path, nproc, layou
     ref, gens, _ = reference_run(g, 300)
     assert f"Generations:\t{gens}" in r.stdout
     assert (tmp_path / "out.txt").read_text() == io.format_text(ref)
+
+
+@pytest.mark.parametrize("nproc,layout,overlap", [(2, "bits", "off"), (3, "u8", "trigger"), (4, "bits", "auto")])
+def test_bench_multirank_band_verifier(native, tmp_path, nproc, layout, overlap):
+    """bench.py --verify-bands on several ranks: every rank checks the top,
+    middle and bottom row bands of its own tile against the fp32 oracle, the
+    light-cone rows beyond its tile sent by its north and south neighbours
+    (parallel/dist.py verify_row_bands) - the path config 5's 2^40-cell grid
+    takes, where no host can gather the grid."""
+    args = [str(REPO / "bench.py"), "--gpus", str(nproc), "--engine", "cpu", "--comm", "torch",
+            "--size", "256", "--height", str(96 * nproc), "--layout", layout, "--steps", "1", "--warmup", "0",
+            "--gens-per-step", "64", "--prewarm", "0", "--verify", "40", "--verify-bands", "--overlap", overlap,
+            "--tune", "cpu_trigger=1"]
+    r = _torchrun(nproc, args, tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    v = rec["config"]["verify"]
+    assert rec["verified"] is True and v["vs_torch_fp32_oracle"] is True, v
+    assert "no gather" in v["oracle"] and v["generations"] == 40
+
+
+def test_multirank_band_verifier_catches_a_wrong_cell(native, tmp_path):
+    """The verifier is not vacuous: a few wrong cells on one rank, introduced
+    between the snapshot and the run, fails every rank (AND over ranks)."""
+    script = tmp_path / "flip.py"
+    script.write_text(f'''
+import sys
+sys.path.insert(0, {str(REPO)!r})
+import numpy as np
+import gol_amd
+from gol_amd.parallel.dist import init_process_group, make_transport, verify_row_bands, env_rank
+rank, world, local = env_rank()
+dist = init_process_group("gloo")
+be = gol_amd.make_backend("cpu", 0)
+sim = gol_amd.Simulation(gol_amd.LifeConfig(128, 64 * world, gen_limit=200, check_similarity=False),
+                         transport=make_transport("torch", be, 0), backend=be)
+sim.init_random(5, 0.5)
+sim.advance(10)
+ok = verify_row_bands(sim, 16, 32)["ok"]
+def flip(s):  # wrong cells in the middle band of rank 1 tile, after the snapshot
+    if rank == 1:
+        t = s.tile()
+        t[28:32, 58:62] ^= 1
+        s.load_tile(t)
+bad = verify_row_bands(sim, 16, 32, after_snapshot=flip)["ok"]
+sys.stdout.write(f"RESULT {{ok}} {{bad}}" + chr(10))
+sys.stdout.flush()
+dist.destroy_process_group()
+''')
+    r = _torchrun(2, [str(script)], tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("RESULT True False") == 2, r.stdout
