@@ -81,18 +81,16 @@ def _claim_stdout() -> int:
     return real
 
 
-def _free_port() -> int:
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        return sk.getsockname()[1]
-
 
 def _launch_ranks(ngpus: int, argv: list[str], out_fd: int) -> int:
     """`mpiexec -n N` for bench.py: N rank processes on this node, one per
     GPU, through torch.distributed.run.  Nothing here touches torch or the
     GPU; rank 0's JSON line is relayed to stdout, everything else to stderr."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ngpus}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    # --standalone: the launcher's rendezvous store binds 127.0.0.1:0 itself
+    # (a port probed free and then bound by the launcher could be taken in
+    # between: EADDRINUSE seen once on a busy box).
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
+           f"--nproc-per-node={ngpus}", os.path.abspath(__file__), *argv]
     log(f"bench.py: launching {ngpus} rank processes: {' '.join(cmd)}")
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE)
     assert proc.stdout is not None

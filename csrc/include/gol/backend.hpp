@@ -75,14 +75,22 @@ class Backend {
   }
   virtual void* stream_mark(void* /*from*/) { return nullptr; }
   virtual void stream_wait(void* /*on*/, void* /*mark*/) {}
-  // Boundary trigger (BlockArgs::trigger): makes `stream` wait until the
-  // groups of the last run_block that met the trigger rows have written
-  // them, without waiting for the rest of that launch.  Returns false when
-  // it did not arm (the backend could not count them): the caller then
-  // orders `stream` after the whole launch.  Synchronous backends never arm.
+  // Boundary trigger (BlockArgs::trigger).  trigger_stream() returns the
+  // compute stream, ordered so that work enqueued on it next starts once the
+  // groups of the last run_block that met the trigger rows have written them
+  // - not after the whole launch: with linked launches that block runs on
+  // the second compute stream, and the first one waits on the device counter
+  // instead - and *armed says whether that happened.  Not armed, it orders
+  // the stream after the whole launch (a join).  Either way the next
+  // run_block on the stream is ordered after what was enqueued in between,
+  // and, armed, may still link to the trigger launch.  Synchronous backends:
+  // nullptr (program order).
   virtual bool supports_trigger() const { return false; }
-  virtual bool comm_wait_trigger(void* /*stream*/) { return false; }
-  virtual int64_t triggered() const { return 0; }  // waits armed so far (diagnostics)
+  virtual void* trigger_stream(bool* armed) {
+    *armed = false;
+    join_streams();
+    return stream();
+  }
   // A side stream for a termination poll that does not join the compute
   // streams: returned after it has been made to wait for everything enqueued
   // so far on every compute stream (a linked chain's second stream

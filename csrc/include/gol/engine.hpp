@@ -48,12 +48,15 @@ struct EngineConfig {
   //    2 edges: the edge strips are recomputed in scratch tiles while the
   //      interior runs (round 1; eight small launches per epoch);
   //    3 trigger: the last temporal block of a full epoch runs as usual, but
-  //      its boundary groups count themselves done on a device counter
-  //      (Backend::comm_wait_trigger) and the comm stream, waiting on that
-  //      counter in the command processor, sends the new boundary rows while
-  //      the block's interior groups still run; the next epoch's first block
-  //      waits for their arrival.  No dual launch, no spinning consumer;
-  //      byte tiles on bit words included;
+  //      its boundary groups count themselves done on a device counter; with
+  //      linked launches that block runs on the second compute stream, and
+  //      the first one - idle once the block before it is done - waits on the
+  //      counter (Backend::trigger_stream) and sends the new boundary rows
+  //      while the block's interior groups still run; the next epoch's first
+  //      block follows the exchange on that stream and still links to the
+  //      last block, so the chain runs through the epoch boundary.  No dual
+  //      launch, no spinning consumer, no comm-stream hop; byte tiles on bit
+  //      words included;
   //    0 off: everything on the compute stream;
   //   -1 auto: where an overlapped schedule applies (row strips), the first
   //      epochs alternate the plain schedule and the alternative (trigger

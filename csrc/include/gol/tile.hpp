@@ -102,7 +102,7 @@ struct BlockArgs {
   // owned rows: rows outside them are the torus wrapped around, which a
   // linked launch's dependency waits must follow (life_group_impl.hpp).
   bool ring = false;
-  // Boundary trigger (Backend::comm_wait_trigger): the groups of this launch
+  // Boundary trigger (Backend::trigger_stream): the groups of this launch
   // whose output rows meet [trigger_rows[0], trigger_rows[1]) or
   // [trigger_rows[2], trigger_rows[3]) count themselves done on a device
   // counter once their rows are written, so a stream can start sending those

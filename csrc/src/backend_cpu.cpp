@@ -107,13 +107,11 @@ class CpuBackend final : public Backend {
   // the wait is armed at once; the engine's bookkeeping (early sends, the
   // arrival before the next epoch, the auto trial) is what this tests.
   bool supports_trigger() const override { return trigger_; }
-  bool comm_wait_trigger(void*) override {
-    const bool armed = armed_;
+  void* trigger_stream(bool* armed) override {
+    *armed = armed_;
     armed_ = false;
-    triggered_ += armed;
-    return armed;
+    return nullptr;
   }
-  int64_t triggered() const override { return triggered_; }
   ~CpuBackend() override {
     for (auto& kv : rings_) ::munmap(kv.first, kv.second);
   }
@@ -240,7 +238,6 @@ class CpuBackend final : public Backend {
   bool ring_fail_ = false;  // GOL_CPU_RING=fail
   bool trigger_ = false;    // GOL_CPU_TRIGGER
   bool armed_ = false;      // the last run_block carried BlockArgs::trigger
-  int64_t triggered_ = 0;
   std::mutex ring_mu_;
   std::map<void*, size_t> rings_;  // row rings: base -> mapped bytes
 };

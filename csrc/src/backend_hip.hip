@@ -529,22 +529,26 @@ class HipBackend final : public Backend {
     }
     return side;
   }
-  // Boundary trigger (BlockArgs::trigger): `stream` waits, in the command
-  // processor, until the boundary groups of the last run_block have counted
-  // themselves done (hipStreamWaitValue64 on the cumulative counter).  False
-  // when that launch could not carry the trigger: the caller orders `stream`
-  // after the whole launch instead.
-  bool comm_wait_trigger(void* stream) override {
-    if (!trigger_target_ || !stream) return false;
-    GOL_ON_DEVICE();
-    HIP_CHECK(hipStreamWaitValue64(static_cast<hipStream_t>(stream), trigger_counter(), trigger_target_,
-                                   hipStreamWaitValueGte, ~0ull));
+  // Boundary trigger (Backend::trigger_stream).  Armed when the trigger
+  // launch ran linked on the second compute stream: the compute stream, whose
+  // last work is the launch before it, waits for the boundary groups' count
+  // (hipStreamWaitValue64; ROCm runs the wait as a small kernel) and the link
+  // chain is left intact, so the next launch on it - the next epoch's first
+  // block, after the exchange - still links to the trigger launch.  Else a
+  // join: the exchange follows the whole launch.
+  void* trigger_stream(bool* armed) override {
+    *armed = false;
+    if (trigger_target_ && link_.stream[1] && link_.cur == 1 && link_.prev_valid) {
+      GOL_ON_DEVICE();
+      HIP_CHECK(hipStreamWaitValue64(stream_, trigger_counter(), trigger_target_, hipStreamWaitValueGte, ~0ull));
+      *armed = true;
+    } else {
+      join_streams();
+    }
     trigger_target_ = 0;
-    ++triggered_;
-    return true;
+    return stream_;
   }
   bool supports_trigger() const override { return trigger_ok_; }
-  int64_t triggered() const override { return triggered_; }
   // Marks come from a small ring of reusable timing-free events: a mark is
   // only waited on by the next few operations of an epoch.
   void* stream_mark(void* from) override {
@@ -1053,7 +1057,6 @@ class HipBackend final : public Backend {
   }
   unsigned long long* trigger_mem_ = nullptr;
   uint64_t trigger_total_ = 0, trigger_target_ = 0;
-  int64_t triggered_ = 0;
   bool trigger_ok_ = false;
   int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, 2 timing probe, -1 autotuned per launch shape
   bool tune_log_ = false;

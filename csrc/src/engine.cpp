@@ -199,7 +199,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // the one-GPU RCCL rehearsal each cross-stream event hop around an exchange
   // cost more than the all-reduce it takes off the compute stream
   // (profiles/r02/rehearsal_overlap.jsonl).
-  comm_route_ = early_ || trigger_;
+  comm_route_ = early_;  // the trigger schedule keeps its exchanges on the compute stream
   if (overlap_) {
     gs_ = TileGeom::make(cfg_.layout, D_, g_.W, D_, g_.hw);
     GOL_REQUIRE(gs_.pitch == g_.pitch, "edge scratch pitch mismatch");
@@ -688,37 +688,32 @@ void Engine::last_block_early(int T) {
 }
 
 // Trigger schedule (overlap = 3; Py > 1 or the one-rank RCCL rehearsal, Px
-// == 1, columns wrapped).  The reference exchanges halos and then waits
-// (MPI_Startall + MPI_Waitall before evolve, src/game_mpi.c:392-403).  Here
-// the last temporal block of a full epoch writes exactly the owned rows, and
-// the next epoch's halos are the first and last Dv of them.  That block runs
-// as one ordinary (linked) launch whose groups meeting those rows count
-// themselves done on a device counter once their rows are written through;
-// the comm stream waits on the counter in the command processor
-// (Backend::comm_wait_trigger) and sends the rows while the block's interior
-// groups still run.  The next epoch's first block waits for the arrival mark
-// (run_epoch).  Nothing spins: no kernel waits on the exchange, and the send
-// waits only on work already running.
+// == 1).  The reference exchanges halos and then waits (MPI_Startall +
+// MPI_Waitall before evolve, src/game_mpi.c:392-403).  Here the last temporal
+// block of a full epoch writes exactly the owned rows, and the next epoch's
+// halos are the first and last Dv of them.  That block runs as one ordinary
+// launch whose groups meeting those rows count themselves done on a device
+// counter once their rows are written through.  With linked launches it runs
+// on the second compute stream, and the first one - whose last work, the
+// block before, is done - waits on the counter (Backend::trigger_stream) and
+// sends the rows while the block's interior groups still run.  The next
+// epoch's first block follows the exchange on that stream and links to the
+// last block, so the chain is not restarted at the epoch boundary.  Nothing
+// spins on the exchange: it is stream-ordered before the launch that reads
+// the halo rows, and it waits only on work already running.  Measured on the
+// one-GPU rehearsal: docs/PERFORMANCE.md.
 void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
   trace::Range tr("gol.last_block_trigger");
   const int64_t Dv = g.Dv, H = g.H, pitch = g.pitch;
   const int64_t rows[4] = {Dv, 2 * Dv, H, H + Dv};
   add_drift(launch(in, out, g, T, Dv, Dv + H, gen_, nullptr, 0, false, rows));
-  if (cols_filled_ && H > 2 * Dv) {  // column halos of the rows that are not sent, on the compute stream
+  bool armed = false;
+  void* s = be_->trigger_stream(&armed);  // not armed: after the whole block (a join)
+  if (armed) ++triggered_sends_;
+  if (cols_filled_) {  // column halos of the new rows (armed launches wrap their columns: never here)
     void* t = phase_begin(nullptr);
-    be_->fill_cols_rows(out, g, 2 * Dv, H - 2 * Dv);
+    be_->fill_cols_rows(out, g, Dv, H);
     phase_end(kFill, t, nullptr);
-  }
-  void* comm = be_->comm_stream();
-  if (be_->comm_wait_trigger(comm))
-    ++triggered_sends_;
-  else
-    be_->stream_wait(comm, be_->stream_mark(nullptr));  // not armed: after the whole block
-  if (cols_filled_) {  // the sent rows carry their column halos
-    void* t = phase_begin(comm);
-    be_->fill_cols_rows(out, g, Dv, std::min(Dv, H), comm);
-    if (H > Dv) be_->fill_cols_rows(out, g, std::max(H, 2 * Dv), Dv + H - std::max(H, 2 * Dv), comm);
-    phase_end(kFill, t, comm);
   }
   auto* base = static_cast<uint8_t*>(out);
   auto nb = dec_.neighbors(rank_);
@@ -729,10 +724,11 @@ void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
       {true, nb[kSouth], base + H * pitch, bytes},          // my bottom rows -> south's top halo
       {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
   };
-  void* tx = phase_begin(comm);
-  tr_->exchange(ops, comm ? comm : be_->stream());
-  phase_end(kHalo, tx, comm);
-  rows_arrived_ = comm ? be_->stream_mark(comm) : nullptr;
+  // Phase timing would join the streams (timing_mark): only when it is on.
+  void* tx = phase_begin(s);
+  tr_->exchange(ops, s ? s : be_->stream());
+  phase_end(kHalo, tx, s);
+  rows_arrived_ = nullptr;  // stream-ordered before the next block on the compute stream
   rows_pending_ = true;
   halo_bytes_ += 2 * int64_t(bytes);
   ++exchanges_;
@@ -769,7 +765,7 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   // side polls).  The trigger schedule links: its sends start only once the
   // boundary groups are done, and the launch after them (the next epoch's
   // first block) waits for their arrival and starts a new chain.
-  a.link = link_ && !early_ && !poll_side_ && (!comm_route_ || trigger_);
+  a.link = link_ && !early_ && !comm_route_ && !poll_side_;
   if (trigger_rows) {
     a.trigger = true;
     for (int i = 0; i < 4; ++i) a.trigger_rows[i] = trigger_rows[i];
@@ -1080,7 +1076,7 @@ void Engine::auto_choose(bool full_epoch) {
 void Engine::set_schedule(int s) {
   early_ = s == 1;
   trigger_ = s == 3;
-  comm_route_ = early_ || trigger_;
+  comm_route_ = early_;
 }
 
 void Engine::auto_mark() {

@@ -3,7 +3,6 @@
 transport - the same code path the GPU uses with nccl=RCCL.  Compared
 byte-for-byte with the exact serial loop."""
 import os
-import socket
 import subprocess
 import sys
 from pathlib import Path
@@ -17,19 +16,14 @@ from gol_amd.utils import io
 REPO = Path(__file__).resolve().parents[1]
 
 
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
 
 def _torchrun(nproc: int, args: list[str], cwd: Path, timeout: int = 300) -> subprocess.CompletedProcess:
     env = dict(os.environ)
     env["PYTHONPATH"] = str(REPO) + os.pathsep + env.get("PYTHONPATH", "")
     env["GOL_HOST_THREADS"] = "2"
     env["OMP_NUM_THREADS"] = "1"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", *args]
+    cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}",
+           "--standalone", "--local-addr=127.0.0.1", *args]
     return subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
 
 

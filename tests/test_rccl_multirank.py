@@ -11,7 +11,6 @@ exact serial loop (tests/mp_rccl_worker.py).
 """
 import json
 import os
-import socket
 import subprocess
 import sys
 from pathlib import Path
@@ -22,11 +21,6 @@ REPO = Path(__file__).resolve().parents[1]
 
 pytestmark = pytest.mark.gpu
 
-
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _env():
@@ -44,8 +38,8 @@ def _ndev() -> int:
 
 
 def _torchrun(nproc, args, timeout=240):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", *args]
+    cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}",
+           "--standalone", "--local-addr=127.0.0.1", *args]
     return subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=timeout)
 
 
