@@ -369,6 +369,17 @@ void life_group_kernel(const LifeBlockParams p) {
   const auto group_end = [&](int g) {
     return p.row_lo + roff + int64_t(g) * p.seg_rows + min(g, p.seg_rem) + p.seg_rows + (g < p.seg_rem ? 1 : 0);
   };
+  // Boundary trigger: the groups whose rows the exchange waits for run at
+  // top issue priority throughout, so their count completes ahead of the
+  // interior groups sharing their SIMDs (wave-uniform).
+  bool hot = p.prio_boost != 0;
+  if (p.bnd_count) {
+    for (int j = 0; j < nsub && grp + j < p.nseg; ++j) {
+      const int64_t e = group_end(grp + j);
+      hot = hot || group_meets(e - p.seg_rows - (grp + j < p.seg_rem ? 1 : 0), e, p.bnd_r);
+    }
+    if (hot) __builtin_amdgcn_s_setprio(3);
+  }
   // Chained strips: wave wi = grp M + m starts at row_lo + wi q + 3 min(wi, x),
   // the first x = seg_rem waves taking q + 3 rows; the strip's last wave ends
   // at chain_end.
@@ -447,14 +458,14 @@ void life_group_kernel(const LifeBlockParams p) {
   if (publish) {  // wave-uniform: the rows are written through, then the flag
     __builtin_amdgcn_s_waitcnt(0);
     if (lane == 0) __hip_atomic_store(p.chain_flag + chain_at, p.chain_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!p.prio_boost) __builtin_amdgcn_s_setprio(0);
+    if (!hot) __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();  // every wave's boundary rows are in LDS
 
   int k = kPro;
   constexpr int S0 = kPro % 3, S1 = (S0 + 1) % 3, S2 = (S0 + 2) % 3;
   // Post-barrier work in level bodies: main loop + epilogue triangle.
-  Prio prio((kmain - kPro) * T + epi_work<T>(nfull), p.prio_boost != 0);
+  Prio prio((kmain - kPro) * T + epi_work<T>(nfull), hot);
   for (; k + 3 <= kmain; k += 3) {
     prio.at((k - kPro) * T);
     wr.row(k - T, levels_full<T, IO, S0, 0, T>(st, rd.template take<S0>(k)));
@@ -490,13 +501,12 @@ void life_group_kernel(const LifeBlockParams p) {
       __hip_atomic_store(p.link_flag + (int64_t(kcol) * p.nseg + grp + lane), p.link_seq, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
       // Boundary trigger: the rows were written through (sc1) and drained
-      // above; the counter is read by the command processor of another
-      // stream (hipStreamWaitValue64), hence system scope.
+      // above; a wave of another stream polls the counter (launch_wait_counter).
       if (p.bnd_count) {
         const int g = grp + lane;
         const int64_t e = group_end(g), b = e - p.seg_rows - (g < p.seg_rem ? 1 : 0);
         if (group_meets(b, e, p.bnd_r))
-          __hip_atomic_fetch_add(p.bnd_count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_fetch_add(p.bnd_count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }

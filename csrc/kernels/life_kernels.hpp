@@ -239,6 +239,9 @@ void launch_load_rows(uint8_t* buf, const TileGeom& g, const uint8_t* stage, int
 void launch_store_rows(const uint8_t* buf, const TileGeom& g, uint8_t* stage, int64_t ld,
                        int64_t r0, int64_t n, bool ascii, hipStream_t s);
 void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s);
+// Holds stream s until *counter >= target (one sleeping wave; error word 7
+// after ~4 s): the boundary trigger's wait (Backend::trigger_stream).
+void launch_wait_counter(const unsigned long long* counter, unsigned long long target, uint32_t* err, hipStream_t s);
 void launch_init_random(uint8_t* buf, const TileGeom& g, uint64_t seed, uint32_t thresh24,
                         int64_t grow0, int64_t gcol0, hipStream_t s);
 // Owned rows of `src` rotated left by `shift` cells (0 < shift < W) into

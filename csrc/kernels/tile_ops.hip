@@ -189,6 +189,25 @@ __global__ void init_random_u8(uint8_t* buf, int64_t pitch, int64_t row0, int64_
 
 __global__ void i64_k(int64_t* p, int64_t v, int add) { *p = add ? *p + v : v; }
 
+// Stream wait on a device counter (the boundary trigger, Backend::
+// trigger_stream): one wave whose lane 0 polls *counter >= target, sleeping
+// s_sleep 127 (~3.4 us) between polls, so the wave that holds the stream
+// costs the launches beside it almost no issue slots (ROCm's
+// hipStreamWaitValue64 kernel polled hard enough to slow the linked launches
+// around it by ~36 us per epoch, profiles/r06/).  Bounded (~4 s): it gives up
+// with the error word's code 7 instead of holding the stream forever.
+__global__ void wait_counter_k(const unsigned long long* counter, unsigned long long target, uint32_t* err) {
+  if (threadIdx.x != 0) return;
+  for (int spin = 0; spin < (1 << 20); ++spin) {
+    if (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      return;
+    }
+    __builtin_amdgcn_s_sleep(127);
+  }
+  if (err) __hip_atomic_store(err, 7u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Undo the adder window's storage drift (life_kernels.hpp kXlaneAdd): owned
 // word k of the output row is cells [32k, 32k+32) of the true frame, which
 // the drifted input holds at cells [32k + s, 32k + s + 32) (mod W).
@@ -280,6 +299,10 @@ void launch_convert_rows(const uint8_t* src, const TileGeom& gs, uint8_t* dst, c
 
 void launch_i64(int64_t* p, int64_t v, bool add, hipStream_t s) {
   hipLaunchKernelGGL(i64_k, dim3(1), dim3(1), 0, s, p, v, add ? 1 : 0);
+}
+
+void launch_wait_counter(const unsigned long long* counter, unsigned long long target, uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(wait_counter_k, dim3(1), dim3(64), 0, s, counter, target, err);
 }
 
 void launch_fill_cols(uint8_t* buf, const TileGeom& g, hipStream_t s) {

@@ -106,11 +106,7 @@ class HipBackend final : public Backend {
     tune_.chain = chain_mode_ < 0 ? 0 : chain_mode_;
     tune_.fault_delay = std::max(0, std::min(4096, t.i("fault_delay_spins")));
     tune_log_ = t.on("tune_log");
-    {
-      int wv = 0;
-      trigger_ok_ = hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, dev_) == hipSuccess && wv;
-      (void)hipGetLastError();
-    }
+    trigger_ok_ = link_mode_ != 0;  // armed only on linked launches
     tune_.chain_seq = &chain_seq_;
     // which: 0 chain flags, 1 chain slots, 2..4 linked-launch completion words
     // (zeroed when allocated: flags and words are compared with sequence
@@ -532,15 +528,16 @@ class HipBackend final : public Backend {
   // Boundary trigger (Backend::trigger_stream).  Armed when the trigger
   // launch ran linked on the second compute stream: the compute stream, whose
   // last work is the launch before it, waits for the boundary groups' count
-  // (hipStreamWaitValue64; ROCm runs the wait as a small kernel) and the link
-  // chain is left intact, so the next launch on it - the next epoch's first
+  // (one sleeping wave, hipk::launch_wait_counter) and the link chain is left
+  // intact, so the next launch on it - the next epoch's first
   // block, after the exchange - still links to the trigger launch.  Else a
   // join: the exchange follows the whole launch.
   void* trigger_stream(bool* armed) override {
     *armed = false;
     if (trigger_target_ && link_.stream[1] && link_.cur == 1 && link_.prev_valid) {
       GOL_ON_DEVICE();
-      HIP_CHECK(hipStreamWaitValue64(stream_, trigger_counter(), trigger_target_, hipStreamWaitValueGte, ~0ull));
+      hipk::launch_wait_counter(trigger_counter(), trigger_target_, tune_.err, stream_);
+      HIP_CHECK(hipGetLastError());
       *armed = true;
     } else {
       join_streams();
@@ -890,6 +887,7 @@ class HipBackend final : public Backend {
       fail(std::string(e == 2   ? "life_group kernel (chained groups): a wave gave up waiting for the group below" + diag
                        : e == 3 ? "life_group kernel (linked launches): a group gave up waiting for the previous "
                                   "launch's rows"
+                       : e == 7 ? "boundary trigger: the exchange's wait gave up on the boundary groups' count"
                                 : "life_block kernel: unknown device error") +
            " (device error word " + std::to_string(e) + "); the rows of that launch are invalid");
     }
@@ -1040,16 +1038,14 @@ class HipBackend final : public Backend {
   int link_mode_ = -1;
   uint32_t chain_seq_ = 0;
   bool u8_pipe_ = true;  // GOL_U8_PIPE: T = 48 byte passes
-  // Boundary trigger: cumulative counter in signal memory (the command
-  // processor polls it), increments expected so far, and the target of the
-  // last armed launch (0: none pending).
+  // Boundary trigger: cumulative device counter, increments expected so
+  // far, and the target of the last armed launch (0: none pending).
   unsigned long long* trigger_counter() {
     if (!trigger_ok_) return nullptr;
     if (!trigger_mem_) {
       GOL_ON_DEVICE();
-      HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&trigger_mem_), sizeof(uint64_t),
-                                      hipMallocSignalMemory));
-      HIP_CHECK(hipMemsetAsync(trigger_mem_, 0, sizeof(uint64_t), stream_));
+      HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&trigger_mem_), 256));
+      HIP_CHECK(hipMemsetAsync(trigger_mem_, 0, 256, stream_));
       HIP_CHECK(hipStreamSynchronize(stream_));
       trigger_total_ = 0;
     }
