@@ -233,7 +233,10 @@ class Engine {
   // returns the frame drift of the launch (cells).
   int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base,
              void* stream = nullptr, int64_t dual_offset = 0, bool prio_boost = false,
-             const int64_t* trigger_rows = nullptr);
+             const int64_t* trigger_rows = nullptr, bool hot_only = false);
+  // A block of a trigger epoch before its last: the boundary rows' light
+  // cone at top issue priority (engine.cpp).
+  void hot_block(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t d);
   void add_drift(int64_t cells);
   void exchange_columns(void* buf, const TileGeom& g);
   void halo_exchange_on(void* buf, const TileGeom& g);

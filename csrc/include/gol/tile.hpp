@@ -109,6 +109,10 @@ struct BlockArgs {
   // rows before the rest of the launch has finished.
   bool trigger = false;
   int64_t trigger_rows[4] = {0, 0, 0, 0};
+  // Earlier blocks of a trigger epoch: the groups meeting trigger_rows (the
+  // light cone of the boundary rows the epoch will send) run at top issue
+  // priority, nothing counted - so the boundary region leads the interior.
+  bool hot = false;
 };
 
 }  // namespace gol

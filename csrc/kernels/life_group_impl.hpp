@@ -373,7 +373,7 @@ void life_group_kernel(const LifeBlockParams p) {
   // top issue priority throughout, so their count completes ahead of the
   // interior groups sharing their SIMDs (wave-uniform).
   bool hot = p.prio_boost != 0;
-  if (p.bnd_count) {
+  if (p.bnd_hot) {
     for (int j = 0; j < nsub && grp + j < p.nseg; ++j) {
       const int64_t e = group_end(grp + j);
       hot = hot || group_meets(e - p.seg_rows - (grp + j < p.seg_rem ? 1 : 0), e, p.bnd_r);

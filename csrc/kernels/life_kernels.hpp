@@ -88,6 +88,7 @@ struct LifeBlockParams {
   // waits on it with hipStreamWaitValue64).  Null: off.
   unsigned long long* bnd_count;
   int64_t bnd_r[4];
+  int bnd_hot;  // groups meeting bnd_r run at top issue priority (with or without bnd_count)
   // Fault injection (GOL_FAULT_DELAY_SPINS, tests): producers at the torus
   // seam - a linked launch's first and last groups - sleep this many s_sleep 127
   // rounds (~3.4 us each) before publishing, so a missing dependency wait
@@ -142,6 +143,7 @@ struct LinkState {
   // rows, the counter, and how many increments the launch will make
   // (launch_linked sets it; 0: the launch could not carry the trigger).
   bool bnd_req = false;
+  bool bnd_count_req = false;  // count (the trigger launch) or priority only (BlockArgs::hot)
   int64_t bnd_r[4] = {0, 0, 0, 0};
   unsigned long long* bnd_count = nullptr;
   int64_t bnd_n = 0;

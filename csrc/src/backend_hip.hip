@@ -603,7 +603,8 @@ class HipBackend final : public Backend {
     // kernel's publish path counts the boundary groups).
     trigger_target_ = 0;
     link_.bnd_n = 0;
-    link_.bnd_req = a.trigger && linkable && trigger_counter();
+    link_.bnd_req = (a.trigger || a.hot) && linkable && trigger_counter();
+    link_.bnd_count_req = a.trigger;
     if (link_.bnd_req) {
       for (int i = 0; i < 4; ++i) link_.bnd_r[i] = a.trigger_rows[i];
       link_.bnd_count = trigger_counter();

@@ -533,6 +533,8 @@ void Engine::epoch_via_bits(int64_t d, bool sent_early) {
     if (rows_ring_) a = gb_.Dv - T;
     if (d == T && trigger_ && send_next_ && full)
       last_block_trigger(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T);
+    else if (trigger_ && send_next_ && full)
+      hot_block(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, a + T, gb_.R() - a - T, d);
     else
       add_drift(launch(bit_scratch(bpar_), bit_scratch(bpar_ ^ 1), gb_, T, a + T, gb_.R() - a - T, gen_));
     bpar_ ^= 1;
@@ -600,6 +602,10 @@ void Engine::run_epoch(int64_t d) {
       last_block_early(T);
     } else if (d == T && trigger_ && send_next_ && full) {
       last_block_trigger(buf_[cur_], buf_[cur_ ^ 1], g_, T);
+      cur_ ^= 1;
+      gen_ += T;
+    } else if (trigger_ && send_next_ && full) {
+      hot_block(buf_[cur_], buf_[cur_ ^ 1], g_, T, a + T, g_.R() - a - T, d);
       cur_ ^= 1;
       gen_ += T;
     } else {
@@ -735,9 +741,20 @@ void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
   ++early_sends_;
 }
 
+// An earlier block of a trigger epoch (d generations left before it): the
+// groups in the light cone of the rows the epoch will send - the first and
+// last Dv owned rows widened by the d - T generations still to come - run at
+// top issue priority, so that region leads the interior and the last block's
+// boundary groups finish ahead of the rest (last_block_trigger).
+void Engine::hot_block(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t d) {
+  const int64_t Dv = g.Dv, H = g.H, w = d - T;
+  const int64_t rows[4] = {row_lo, 2 * Dv + w, H - w, row_hi};
+  add_drift(launch(in, out, g, T, row_lo, row_hi, gen_, nullptr, 0, false, rows, /*hot_only=*/true));
+}
+
 int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
                    int64_t gen_base, void* stream, int64_t dual_offset, bool prio_boost,
-                   const int64_t* trigger_rows) {
+                   const int64_t* trigger_rows, bool hot_only) {
   BlockArgs a;
   a.in = in;
   a.out = out;
@@ -767,7 +784,8 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   // first block) waits for their arrival and starts a new chain.
   a.link = link_ && !early_ && !comm_route_ && !poll_side_;
   if (trigger_rows) {
-    a.trigger = true;
+    a.trigger = !hot_only;
+    a.hot = hot_only;
     for (int i = 0; i < 4; ++i) a.trigger_rows[i] = trigger_rows[i];
   }
   a.ring = rows_ring_;
