@@ -182,6 +182,20 @@ def band_oracle(snap, r0: int, gens: int, device: str):
     return life_step_torch_roll(snap[rows], gens, device=device)[gens:gens + b]
 
 
+def dtype_label(layout: str, u8_compute, kernel: str) -> str:
+    """What the cells are stored as and what the timed loop computes on.  A
+    byte grid whose epochs run on its bit image (u8_compute "bits", the GPU
+    default) says so: the timed loop never touches the bytes, which are
+    unpacked only when read (VERDICT r05 "Weak 5")."""
+    if layout == "bits":
+        return "u1 bit-packed cells (exact boolean B3/S23; reference stores u8 chars)"
+    if u8_compute == "bits":
+        return "u8 storage, computed on a live bit image (packed once, unpacked on read; exact)"
+    if "LDS-tiled" in kernel:
+        return "u8 byte-per-cell, LDS-tiled byte kernel (exact)"
+    return "u8 byte-per-cell, computed on the bytes (exact)"
+
+
 def grid_digest(parts) -> str:
     """sha256 of the verified final cells (0/1 bytes, row-major): the same seed
     and step count must give the same digest on any schedule or build, so two
@@ -520,6 +534,9 @@ def main() -> int:
             dist.barrier()
 
     desc = sim.describe()
+    if desc["row_ring_fallback"]:
+        log(f"bench.py: WARNING: the row ring fell back to periodic fills ({desc['row_ring_fallback']}); "
+            "the number below is not the ring schedule's")
     rehearsal = rehearsal_label(world, shared, bool(a.rehearse_rccl and world == 1 and on_gpu), infos)
     metric, headline, config_id = metric_label(S, Hg, gps, rehearsal)
     if rank == 0:
@@ -535,8 +552,7 @@ def main() -> int:
             "scaling": "strong",
             "verified": verified,
             "vs_baseline": value / BASELINE_VALUE,
-            "dtype": "u1 bit-packed cells (exact boolean B3/S23; reference stores u8 chars)"
-                     if a.layout == "bits" else "u8 byte-per-cell (exact)",
+            "dtype": dtype_label(a.layout, desc["u8_compute"], desc["kernel"]),
             "data": "synthetic: on-device counter-based RNG random grid, density 0.5 (generate.sh distribution)",
             "headline": headline,
             "config_id": config_id,
@@ -565,6 +581,9 @@ def main() -> int:
                 "kernel_launches_per_step": rs[-1].kernel_launches if rs else 0,
                 "linked_launches_per_step": rs[-1].linked_launches if rs else 0,
                 "row_ring": desc["row_ring"],
+                # A ring the tile should have had but the backend could not
+                # map (its error): the run used periodic row fills instead.
+                "row_ring_fallback": desc["row_ring_fallback"],
                 # Knobs set by hand: GOL_* variables, and every tuning key off
                 # its default with its source (bench.py's own rehearsal
                 # partition aside); the effective values of the tune class.

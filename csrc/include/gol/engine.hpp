@@ -190,6 +190,9 @@ class Engine {
   // Whether the tile is a row ring (Backend::row_ring_halo): no row fills,
   // one temporal block per epoch over the owned rows.
   bool row_ring() const { return rows_ring_; }
+  // Why a row ring this tile should have had could not be built (the
+  // backend's error; the tile then runs with periodic row fills), or "".
+  const std::string& row_ring_fallback() const { return ring_fallback_; }
   // Rotates the drift out of the current buffer (owned rows); every
   // read-out (store_cells) does this first.
   void normalize();
@@ -324,6 +327,7 @@ class Engine {
   bool cols_filled_ = true; // column halos kept valid by fills (false: the backend wraps column reads)
   bool rows_wrapped_ = false; // single-rank torus read modulo its rows (no fills at all)
   bool rows_ring_ = false;    // row halos are second mappings of the owned rows (Backend::row_ring_halo)
+  std::string ring_fallback_;  // alloc_row_ring's error when the ring fell back to fills
   bool link_ = false;         // blocks may run linked (Backend::KernelChoice::link; ring tiles only)
   bool via_bits_ = false;    // byte layout computed on bit words (epoch_via_bits)
   TileGeom gb_;              // the tile in the bit layout (same rows, halos, words)

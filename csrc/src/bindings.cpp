@@ -318,6 +318,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("drift", &Engine::drift)
       .def_property_readonly("drifting", &Engine::drifting)
       .def_property_readonly("row_ring", &Engine::row_ring)
+      .def_property_readonly("row_ring_fallback", &Engine::row_ring_fallback)
       .def_property_readonly("via_bits", &Engine::via_bits)
       .def("normalize", &Engine::normalize, py::call_guard<py::gil_scoped_release>())
       .def("current_buffer", [](Engine& e) { return reinterpret_cast<std::uintptr_t>(e.current_buffer()); })

@@ -133,7 +133,8 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
           if (b) be_->release(b);
         ring_bufs[0] = ring_bufs[1] = nullptr;
         ring_dv = 0;
-        std::fprintf(stderr, "gol: row ring unavailable (%s); periodic row fills instead\n", e.what());
+        ring_fallback_ = e.what();
+        std::fprintf(stderr, "gol: WARNING: row ring unavailable (%s); periodic row fills instead\n", e.what());
       }
     }
   }

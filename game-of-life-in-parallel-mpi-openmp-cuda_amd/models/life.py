@@ -239,7 +239,7 @@ class Simulation:
                 "overlap_alternative": self._eng.trial_alternative(),
                 "triggered_sends": self._eng.triggered_sends(),
                 "u8_compute": ("bits" if self._eng.via_bits else "bytes") if self.config.resolved_layout() == "u8" else None,
-                "row_ring": bool(self._eng.row_ring),
+                "row_ring": bool(self._eng.row_ring), "row_ring_fallback": self._eng.row_ring_fallback or None,
                 "kernel": self._kernel_name(),
                 "tuning": self.tuning(), "tuning_changed": self.tuning_changed()}
 

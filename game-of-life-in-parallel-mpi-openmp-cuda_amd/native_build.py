@@ -46,6 +46,8 @@ HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block
 BIND_SRCS = ["src/bindings.cpp"]
 CLI_MAIN = "tools/gol_main.cpp"
 GEN_MAIN = "tools/gol_gen.cpp"
+# Stand-alone HIP tools (no engine code): the row-ring VMM stress test.
+TOOLS = ["tools/ring_stress.hip"]
 
 MODULE = PKG_DIR / "_gol.so"
 
@@ -121,7 +123,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     BUILD.mkdir(parents=True, exist_ok=True)
     BIN.mkdir(parents=True, exist_ok=True)
     hdr = _headers_mtime()
-    srcs = HOST_SRCS + HIP_SRCS + BIND_SRCS + [CLI_MAIN, GEN_MAIN]
+    srcs = HOST_SRCS + HIP_SRCS + BIND_SRCS + [CLI_MAIN, GEN_MAIN] + TOOLS
     objs = {s: BUILD / (s.replace("/", "_") + ".o") for s in srcs}
     todo = [s for s in srcs if force or _needs(objs[s], CSRC / s, hdr)]
     # Longest compiles first (deep byte passes, then the kernel variants), so
@@ -147,6 +149,11 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
              verbose)
         _run([_hipcc(), *core, str(objs[CLI_MAIN]), "-o", str(outs["gol"]), *rocm_libs], verbose)
         _run([_hipcc(), *core, str(objs[GEN_MAIN]), "-o", str(outs["gol_gen"]), *rocm_libs], verbose)
+    for t in TOOLS:
+        exe = BIN / Path(t).stem
+        if relink or not exe.exists() or exe.stat().st_mtime < objs[t].stat().st_mtime:
+            _run([_hipcc(), str(objs[t]), "-o", str(exe), f"-L{ROCM / 'lib'}", "-lamdhip64",
+                  f"-Wl,-rpath,{ROCM / 'lib'}"], verbose)
     LAST_BUILD.clear()
     LAST_BUILD.update(compiled=len(todo), up_to_date=len(srcs) - len(todo), relinked=relink)
     return outs

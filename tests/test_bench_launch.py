@@ -341,3 +341,23 @@ def test_band_oracle_small_grid_is_whole_grid():
     snap = random_grid(W, H, 3)
     assert b.band_starts(H) == [0]
     assert np.array_equal(b.band_oracle(snap, 0, g, "cpu"), life_step_torch_roll(snap, g))
+
+
+@pytest.mark.parametrize("layout,u8c,want", [("bits", "auto", "u1 bit-packed"),
+                                             ("u8", "bits", "u8 storage, computed on a live bit image"),
+                                             ("u8", "bytes", "u8 byte-per-cell, computed on the bytes")])
+def test_bench_dtype_label_says_what_the_loop_computes_on(native, layout, u8c, want):
+    """VERDICT r05 Weak 5: a byte-layout record whose epochs ran on the bit
+    image must not claim byte-per-cell compute."""
+    env = dict(os.environ, PYTHONPATH=str(REPO), OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--engine", "cpu", "--size", "128", "--steps", "1",
+                        "--warmup", "0", "--gens-per-step", "32", "--prewarm", "0", "--verify", "16",
+                        "--layout", layout, "--u8-compute", u8c], capture_output=True, text=True, timeout=300,
+                       env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["dtype"].startswith(want), rec["dtype"]
+    assert rec["config"]["u8_compute"] == (None if layout == "bits" else u8c)
+    assert rec["config"]["row_ring_fallback"] is None
