@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -311,13 +312,23 @@ class HipBackend final : public Backend {
     const size_t gran = ring_granularity();
     GOL_REQUIRE(gran != size_t(-1) && halo % gran == 0 && owned % gran == 0 && owned >= 2 * halo && halo > 0,
                 "row ring: geometry does not fit the mapping granularity (Backend::row_ring_halo)");
-    // HIP's bookkeeping of a handle mapped twice is fragile: setting access
-    // mapping by mapping fails on the first mapping of a doubly mapped handle,
-    // and a whole-range call on a fresh ring failed once after other rings had
-    // come and gone in the process (possibly at an address an earlier ring had used).
-    // So a ring's address range is never given back (release_ring keeps the
-    // reservation; only the memory is freed), and a failed attempt is retried
-    // once on a new range.
+    // A ring's address range is never mapped twice: bin/ring_stress (round
+    // 6, profiles/r06/ring_stress.txt) maps 300 rings of mixed geometry with
+    // allocation churn in between, and when an unmapped range is freed and
+    // reserved again (hipMemAddressFree) or reused for the next ring, reads
+    // through the new halo alias return the old pages' contents or zeros in
+    // 210 resp. 224 of 300 rings - translations of the reused range are not
+    // the new mapping - while with every range kept reserved all 300 alias
+    // correctly.  So release_ring frees the memory and keeps the reservation
+    // (address space only, 2 x (owned + 2 halo) bytes per engine), bounded
+    // by kRingVaBudget: past it rings are refused and the engine falls back
+    // to periodic fills, loudly (Engine::row_ring_fallback).  Setting access
+    // mapping by mapping also fails on the first mapping of a doubly mapped
+    // handle, hence one whole-range hipMemSetAccess; a failed attempt is
+    // retried once on a new range.
+    if (ring_va_held().load() + owned + 2 * halo > kRingVaBudget)
+      fail("row ring: address space held by released rings (" + std::to_string(ring_va_held().load() >> 30) +
+           " GiB) would pass the " + std::to_string(kRingVaBudget >> 40) + " TiB budget");
     Ring r;
     uint8_t* b = nullptr;
     for (int attempt = 0;; ++attempt) {
@@ -975,6 +986,7 @@ class HipBackend final : public Backend {
     for (auto& m : r.mapped)
       if (hipMemUnmap(m.first, m.second) != hipSuccess) clear_release_error("row ring: hipMemUnmap");
     r.mapped.clear();
+    if (r.va) ring_va_held() += r.bytes;
     r.va = nullptr;  // the reservation is kept (alloc_row_ring): address space only
     for (auto& h : r.h) {
       if (h && hipMemRelease(h) != hipSuccess) clear_release_error("row ring: hipMemRelease");
@@ -1023,6 +1035,13 @@ class HipBackend final : public Backend {
   bool check_dev_ = false;  // GOL_CHECK_DEVICE
   bool ring_on_ = true;     // GOL_ROW_RING
   mutable size_t ring_gran_ = 0;
+  // Address space of released rings in this process, never reserved again
+  // (alloc_row_ring), and its bound: a quarter of the 2^47-byte user range.
+  static std::atomic<size_t>& ring_va_held() {
+    static std::atomic<size_t> held{0};
+    return held;
+  }
+  static constexpr size_t kRingVaBudget = size_t(32) << 40;
   std::map<void*, Ring> rings_;
   std::vector<hipEvent_t> timing_pool_;  // timing_mark() events
   hipStream_t stream_ = nullptr;

@@ -1018,3 +1018,38 @@ def test_rank_tile_trigger_schedule(gpu, tune, layout, delay):
     assert rep.overlapped and rep.linked_launches > 0
     assert sim.native_engine.triggered_sends() == 2
     assert (sim.tile() == want).all()
+
+
+def test_ring_stress_tool_keep_policy(gpu, repo):
+    """bin/ring_stress (VERDICT r05 Weak 6): 200 rings of mixed geometry with
+    allocation churn, mapped exactly as HipBackend::alloc_row_ring does, every
+    address range kept reserved after release (the backend's policy): no
+    hipMemSetAccess failure and every halo alias reads its owned row.  (With
+    ranges freed or reused the same tool finds stale aliases,
+    profiles/r06/ring_stress.txt - why the backend never reuses a range.)"""
+    import subprocess
+
+    r = subprocess.run([str(repo / "bin" / "ring_stress"), "200", "keep"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = next(ln for ln in r.stdout.splitlines() if ln.startswith("keep"))
+    assert "setaccess failures 0 " in line and "alias failures 0 " in line, line
+
+
+def test_many_ring_engines_in_one_process_keep_their_rings(gpu, tune):
+    """Engines with row rings created and dropped one after another in one
+    process (a test session, repeated Simulation construction) all get their
+    rings - no silent fallback to fills - and stay exact."""
+    tune.pop("u8_via_bits", None)
+    for i in range(40):
+        W, H = (4096, 2048) if i % 2 else (8192, 1024)
+        sim = Simulation(LifeConfig(W, H, gen_limit=100, tune=tune), engine="hip")
+        d = sim.describe()
+        assert d["row_ring"] is True and d["row_ring_fallback"] is None, (i, d["row_ring_fallback"])
+        if i % 10 == 0:
+            g = random_grid(W, H, i)
+            sim.load(g)
+            sim.advance(40)
+            assert (sim.tile() == life_step_torch(g, 40, device="cuda")).all(), i
+        del sim
+        gc.collect()
