@@ -598,6 +598,8 @@ def main() -> int:
                 "overlap_trial_ms_per_epoch": {"plain": desc["overlap_trial_ms_plain"],
                                                desc["overlap_alternative"]: desc["overlap_trial_ms_early"]},
                 "triggered_sends": desc["triggered_sends"],
+                "poll_mode": desc["poll_mode"],
+                "poll_trial_ms_per_window": desc["poll_trial_ms_per_window"],
                 "graph_epochs": sum(r.graph_launches for r in rs),
                 "phase_ms_one_step": phases,
                 "verify": verify,

@@ -101,7 +101,7 @@ struct EngineConfig {
   //      (GOL_U8_VIA_BITS=0|1 overrides), else bytes.
   int u8_compute = -1;
   // Runtime tuning (gol/tuning.hpp): the engine's own knobs (u8_via_bits,
-  // side_poll, poll_copy_side, watchdog_s, pitch_pad, overlap_auto) come from here; the
+  // side_poll, cpu_side_poll, poll_copy_side, watchdog_s, pitch_pad, overlap_auto) come from here; the
   // backend's from the Tuning it was constructed with.  Default: the table's
   // defaults under the GOL_* environment overrides.
   Tuning tune = Tuning::from_env();
@@ -163,6 +163,13 @@ class Engine {
   // alternative the auto trial measured (-1: not measured), and the
   // alternative's name ("trigger" or "early").
   double trial_ms_plain() const { return auto_ms_[0]; }
+  // Termination polls: "joined" (the flag all-reduce on the compute stream),
+  // "side" (a side stream, tuning side_poll=1), "auto:trial", "auto:side" or
+  // "auto:joined" (side_poll = -1, decided on the ranks), and the trial's
+  // per-window medians (ms, MAX over ranks; -1: not measured).
+  std::string poll_mode() const;
+  double poll_trial_ms_joined() const { return poll_ms_[0]; }
+  double poll_trial_ms_side() const { return poll_ms_[1]; }
   double trial_ms_early() const { return auto_ms_[1]; }
   std::string trial_alternative() const { return auto_alt_ == 3 ? "trigger" : "early"; }
   // Epoch exchanges started by the boundary trigger so far (diagnostics).
@@ -276,6 +283,7 @@ class Engine {
   void auto_choose(bool full_epoch);
   void auto_mark();
   void auto_decide();
+  void poll_trial_step();
   // Phase timing: a mark on `stream` (nullptr when off or capturing), and
   // the span [a, now] of `phase` on that stream.
   void* phase_begin(void* stream);
@@ -355,6 +363,15 @@ class Engine {
   std::vector<AutoSpan> auto_spans_;
   int auto_counts_[2] = {0, 0};
   double auto_ms_[2] = {-1, -1};
+  void trial_medians(std::vector<AutoSpan>& spans, double out[2]);
+  // Poll placement trial (tuning side_poll = -1, poll_trial_step).
+  bool poll_trial_ = false, poll_decided_ = false;
+  int64_t ptrial_polls_ = 0;
+  int ptrial_mode_ = -1;            // placement of the open window: 0 joined, 1 side, -1 warm-up
+  void* ptrial_open_ = nullptr;
+  std::vector<AutoSpan> ptrial_spans_;
+  int ptrial_counts_[2] = {0, 0};
+  double poll_ms_[2] = {-1, -1};
   // Phase timing.
   bool phase_timing_ = false;
   struct PhaseSpan {

@@ -118,8 +118,13 @@ class ThreadTransport final : public Transport {
   void exchange(const std::vector<P2POp>& ops, void* stream) override;
   void allreduce_max_u32(uint32_t* buf, size_t n, void* stream) override;
   void barrier() override;
+  // Tuning cpu_side_poll=1 (tests): claims a flag reduction of its own, so the
+  // engine's poll placement trial runs on CPU ranks (both placements reduce
+  // through the hub in program order there).
+  bool side_reduce() const override { return side_; }
 
  private:
+  bool side_ = false;
   std::shared_ptr<ThreadHub> hub_;
   int rank_;
   Backend* backend_;

@@ -311,6 +311,9 @@ PYBIND11_MODULE(_gol, m) {
       .def_property_readonly("trial_ms_plain", &Engine::trial_ms_plain)
       .def_property_readonly("trial_ms_early", &Engine::trial_ms_early)
       .def("trial_alternative", &Engine::trial_alternative)
+      .def("poll_mode", &Engine::poll_mode)
+      .def_property_readonly("poll_trial_ms_joined", &Engine::poll_trial_ms_joined)
+      .def_property_readonly("poll_trial_ms_side", &Engine::poll_trial_ms_side)
       .def("triggered_sends", &Engine::triggered_sends)
       .def_property("phase_timing", &Engine::phase_timing, &Engine::set_phase_timing)
       .def("graphs", &Engine::graphs)

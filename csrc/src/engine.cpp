@@ -236,8 +236,13 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // Auto: deeper blocks only.
   const int pcs = cfg_.tune.i("poll_copy_side");
   poll_copy_side_ = pcs > 0 || (pcs < 0 && tmax_ > 8);
-  poll_side_ = tr_->side_reduce() && be_->is_device() && !early_ && !comm_route_ && !use_graphs_ &&
-               !auto_overlap_ && cfg_.tune.on("side_poll");
+  // side_poll = -1 (default): after the overlap trial the ranks time both
+  // poll placements (poll_trial_step) and keep the faster, as for overlap.
+  const int sp = cfg_.tune.i("side_poll");
+  const bool side_ok = tr_->side_reduce() && (be_->is_device() || cfg_.tune.on("cpu_side_poll")) && !use_graphs_ &&
+                       (tr_->size() > 1 || cfg_.self_exchange);
+  poll_side_ = side_ok && sp > 0 && !early_ && !comm_route_ && !auto_overlap_;
+  poll_trial_ = side_ok && sp < 0;
   gen_ = cfg_.start_gen;
 }
 
@@ -250,10 +255,12 @@ void Engine::release_graphs() {
 
 Engine::~Engine() {
   release_graphs();
-  for (auto& sp : auto_spans_) {
-    be_->timing_release(sp.a);
-    be_->timing_release(sp.b);
-  }
+  for (auto* spans : {&auto_spans_, &ptrial_spans_})
+    for (auto& sp : *spans) {
+      be_->timing_release(sp.a);
+      be_->timing_release(sp.b);
+    }
+  if (ptrial_open_) be_->timing_release(ptrial_open_);
   if (auto_open_) be_->timing_release(auto_open_);
   for (auto& sp : phase_spans_) {
     be_->timing_release(sp.a);
@@ -1011,6 +1018,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     }
     ++epoch;
     if (stop_early && (epoch % poll_epochs == 0 || gen_ == limit)) {
+      if (poll_trial_) poll_trial_step();
       Poll p = poll_issue(checked, gen_);
       checked = gen_;
       if (have_pending && poll_check(pending, &found)) {
@@ -1038,6 +1046,10 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   if (auto_open_) {  // an auto-trial epoch span does not continue into the next run
     be_->timing_release(auto_open_);
     auto_open_ = nullptr;
+  }
+  if (ptrial_open_) {  // nor does a poll-trial window
+    be_->timing_release(ptrial_open_);
+    ptrial_open_ = nullptr;
   }
   if (cfg_.timing_barriers) {
     settle_pending(false);
@@ -1118,28 +1130,83 @@ void Engine::auto_mark() {
   auto_open_sched_ = auto_sched_;
 }
 
-void Engine::auto_decide() {
+// Medians of two schedules' timed spans, MAX over ranks (the slowest rank
+// decides; every rank gets the same values), in ms; releases the spans.
+void Engine::trial_medians(std::vector<AutoSpan>& spans, double out[2]) {
   std::vector<double> ms[2];
-  for (auto& sp : auto_spans_) {
+  for (auto& sp : spans) {
     ms[sp.sched].push_back(be_->timing_ms(sp.a, sp.b));
     be_->timing_release(sp.a);
     be_->timing_release(sp.b);
   }
-  auto_spans_.clear();
+  spans.clear();
   uint32_t v[2];
   for (int k = 0; k < 2; ++k) {
     std::sort(ms[k].begin(), ms[k].end());
     const double med = ms[k][ms[k].size() / 2];
     v[k] = uint32_t(std::min(4.0e9, std::max(0.0, med * 1e4)));  // 0.1 us units
   }
-  // Slowest rank decides: every rank ends up with the same MAX values.
   uint32_t* dev = alive_dev_ + 4;
   be_->copy_h2d(dev, v, sizeof(v));
   if (tr_->size() > 1) tr_->allreduce_max_u32(dev, 2, be_->stream());
   be_->copy_d2h(v, dev, sizeof(v));
-  auto_ms_[0] = v[0] * 1e-4;
-  auto_ms_[1] = v[1] * 1e-4;
-  bool alt = double(v[1]) < 0.98 * double(v[0]);
+  out[0] = v[0] * 1e-4;
+  out[1] = v[1] * 1e-4;
+}
+
+// Poll placement trial (tuning side_poll = -1).  Once the overlap trial has
+// decided (and where polls do not ride the comm stream with the exchanges),
+// the poll windows - from one termination poll to the next - alternate a
+// poll whose flag all-reduce joins the compute stream and one that runs on a
+// side stream through the transport's flags communicator (poll_side_, which
+// also leaves linked launches off for that window: transport work may run
+// beside them), after two warm-up windows; each window is timed from its
+// poll's issue to the next's on the compute stream, and when kAutoTrials of
+// each are in, at the same poll on every rank, the medians are MAX-reduced
+// and every rank keeps the faster placement.  The reference all-reduces
+// every generation on the critical path (src/game_mpi_collective.c:70-109).
+void Engine::poll_trial_step() {
+  if (auto_overlap_) return;  // the overlap trial runs first
+  if (comm_route_) {          // polls already leave the compute stream, in order with the exchanges
+    poll_trial_ = false;
+    poll_side_ = false;
+    return;
+  }
+  if (ptrial_open_) {
+    void* end = be_->timing_mark(nullptr);
+    if (ptrial_mode_ >= 0) {
+      ptrial_spans_.push_back({ptrial_mode_, ptrial_open_, end});
+      ++ptrial_counts_[ptrial_mode_];
+    } else {
+      be_->timing_release(ptrial_open_);
+      be_->timing_release(end);
+    }
+    ptrial_open_ = nullptr;
+  }
+  if (ptrial_counts_[0] >= kAutoTrials && ptrial_counts_[1] >= kAutoTrials) {
+    trial_medians(ptrial_spans_, poll_ms_);
+    poll_side_ = poll_ms_[1] < 0.98 * poll_ms_[0];
+    poll_trial_ = false;
+    poll_decided_ = true;
+    return;
+  }
+  const int64_t i = ptrial_polls_++;
+  ptrial_mode_ = i < kAutoWarm ? -1 : int((i - kAutoWarm) % 2);
+  poll_side_ = ptrial_mode_ == 1;
+  ptrial_open_ = be_->timing_mark(nullptr);
+}
+
+std::string Engine::poll_mode() const {
+  if (poll_trial_) return "auto:trial";
+  if (poll_decided_) return poll_side_ ? "auto:side" : "auto:joined";
+  return poll_side_ ? "side" : "joined";
+}
+
+void Engine::auto_decide() {
+  // Slowest rank decides: every rank ends up with the same MAX values.
+  trial_medians(auto_spans_, auto_ms_);
+  const double v[2] = {auto_ms_[0], auto_ms_[1]};
+  bool alt = v[1] < 0.98 * v[0];
   const std::string& forced = cfg_.tune.s("overlap_auto");  // fault injection (tests)
   if (forced == "early" || forced == "trigger") alt = true;
   if (forced == "plain") alt = false;

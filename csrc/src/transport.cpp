@@ -20,6 +20,7 @@ ThreadHub::ThreadHub(int nranks) : red(), n_(nranks) { GOL_REQUIRE(nranks > 0, "
 ThreadTransport::ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, Backend* backend, const Tuning& tune)
     : hub_(std::move(hub)), rank_(rank), backend_(backend) {
   delay_us_ = std::max(0, tune.i("fault_delay_us"));
+  side_ = tune.on("cpu_side_poll");
   garble_at_ = tune.i("fault_garble");
   rng_ = 0x9E3779B97F4A7C15ull * uint64_t(rank + 1);
 }

@@ -93,11 +93,12 @@ class RcclTransport final : public Transport {
     {
       StdoutToStderr quiet;
       NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
-      // Side-stream polls (tuning side_poll=1, the same on every rank): the
-      // termination-flag reductions get their own communicator.  RCCL orders
-      // the operations of one communicator by issue, and two streams on one
-      // communicator could interleave differently on different ranks.
-      if (tune.on("side_poll")) NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
+      // Side-stream polls (tuning side_poll on or auto, the same on every
+      // rank): the termination-flag reductions get their own communicator.
+      // RCCL orders the operations of one communicator by issue, and two
+      // streams on one communicator could interleave differently on
+      // different ranks.
+      if (tune.i("side_poll") != 0) NCCL_CHECK(ncclCommSplit(comm_, 0, rank, &flags_comm_, nullptr));
     }
     barrier_stream_ = make_stream(dev_, tune.s("cu_partition"));
     HIP_CHECK(hipMalloc(&barrier_buf_, 64));

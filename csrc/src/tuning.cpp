@@ -40,7 +40,9 @@ const std::vector<TuningKey>& tuning_keys() {
       {"u8_pipe", "GOL_U8_PIPE", "1", 'i', "tune", "byte passes of T = 48 as level-pipelined wave pairs"},
       {"u8_via_bits", "GOL_U8_VIA_BITS", "-1", 'i', "tune",
        "byte layout computes on bit words: -1 auto, 0 bytes, 1 bits (EngineConfig::u8_compute wins when set)"},
-      {"side_poll", "GOL_SIDE_POLL", "0", 'i', "tune", "multi-rank polls reduce on the comm stream"},
+      {"side_poll", "GOL_SIDE_POLL", "-1", 'i', "tune",
+       "multi-rank polls reduce on a side stream through a flags communicator: -1 timed on the ranks after the "
+       "overlap trial, 0 off, 1 on"},
       {"poll_copy_side", "GOL_POLL_COPY_SIDE", "-1", 'i', "tune",
        "single-rank polls copy their flags on a side stream, linked chains continuing across them: -1 where "
        "blocks are deeper than 8 generations, 1 always, 0 never (join the compute streams, copy there)"},
@@ -68,6 +70,8 @@ const std::vector<TuningKey>& tuning_keys() {
       {"cpu_ring", "GOL_CPU_RING", "0", 's', "emul", "CPU backend row rings: 0, 1, or fail (mapping fails)"},
       {"cpu_drift", "GOL_CPU_DRIFT", "0", 'i', "emul", "CPU backend's drifting frame (as the adder window)"},
       {"cpu_trigger", "GOL_CPU_TRIGGER", "0", 'i', "emul", "CPU backend accepts the boundary-trigger schedule"},
+      {"cpu_side_poll", "GOL_CPU_SIDE_POLL", "0", 'i', "emul",
+       "thread transport claims a flags communicator: the poll placement trial runs on CPU ranks"},
   };
   return keys;
 }

@@ -132,7 +132,8 @@ def make_backend(engine: str = "auto", device: int = 0, threads: int = 0, tune=N
 
 # Tuning keys the engine reads from EngineConfig::tune (engine.cpp); the rest
 # are read by the backend (or the transports) at construction.
-_ENGINE_KEYS = frozenset({"u8_via_bits", "side_poll", "poll_copy_side", "watchdog_s", "pitch_pad", "overlap_auto"})
+_ENGINE_KEYS = frozenset({"u8_via_bits", "side_poll", "poll_copy_side", "watchdog_s", "pitch_pad", "overlap_auto",
+                          "cpu_side_poll"})
 
 
 @dataclasses.dataclass
@@ -237,6 +238,9 @@ class Simulation:
                 "overlap_trial_ms_plain": self._eng.trial_ms_plain,
                 "overlap_trial_ms_early": self._eng.trial_ms_early,
                 "overlap_alternative": self._eng.trial_alternative(),
+                "poll_mode": self._eng.poll_mode(),
+                "poll_trial_ms_per_window": {"joined": self._eng.poll_trial_ms_joined,
+                                             "side": self._eng.poll_trial_ms_side},
                 "triggered_sends": self._eng.triggered_sends(),
                 "u8_compute": ("bits" if self._eng.via_bits else "bytes") if self.config.resolved_layout() == "u8" else None,
                 "row_ring": bool(self._eng.row_ring), "row_ring_fallback": self._eng.row_ring_fallback or None,

@@ -33,7 +33,7 @@ python3 scripts/occupancy.py "tile8_ring=$O/occ_tile8ring" "full_32768_dpp_T16=$
   > "$O/occupancy.md" 2> "$O/occupancy.err" || echo "occupancy.py failed"
 python3 scripts/attrib.py "$O" > "$O/attrib.md" 2> "$O/attrib.err" || echo "attrib.py failed"
 # Per-wave records of launches 300 and 301 (linked) on the ring tile.
-GOL_WG_TRACE="300:$O/wg_tile8_pair.csv:pair" timeout -k 10 120 python3 bench.py --height 4096 $B > "$O/wg.out" 2> "$O/wg.err" || { tail -5 "$O/wg.err"; exit 1; }
+GOL_WG_TRACE="100:$O/wg_tile8_pair.csv:pair" timeout -k 10 120 python3 bench.py --height 4096 $B > "$O/wg.out" 2> "$O/wg.err" || { tail -5 "$O/wg.err"; exit 1; }
 python3 scripts/wg_trace.py --pair "$O/wg_tile8_pair.csv" > "$O/wg_tile8_pair.txt" 2>&1 || echo "wg_trace.py failed"
 # T sweep of the tile (DPP window), timed.
 timeout -k 10 400 python3 -u scripts/bench_matrix.py scripts/matrices/main.txt "$O/tsweep.jsonl" --timeout 120 \

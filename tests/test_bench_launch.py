@@ -361,3 +361,36 @@ def test_bench_dtype_label_says_what_the_loop_computes_on(native, layout, u8c, w
     assert rec["dtype"].startswith(want), rec["dtype"]
     assert rec["config"]["u8_compute"] == (None if layout == "bits" else u8c)
     assert rec["config"]["row_ring_fallback"] is None
+
+
+@pytest.mark.parametrize("overlap", ["off", "auto"])
+def test_poll_placement_trial_is_exact(native, monkeypatch, overlap):
+    """side_poll = -1 (default): after the overlap trial the ranks alternate
+    poll windows whose flag all-reduce joins the compute stream and windows
+    whose all-reduce runs on a side stream through the flags communicator,
+    time them, MAX-reduce the medians and keep the faster - the same decision
+    on every rank, with termination exact throughout (the thread transport
+    claims a flags communicator with cpu_side_poll)."""
+    monkeypatch.setenv("GOL_CPU_SIDE_POLL", "1")
+    W, H = 128, 3 * 64
+    g = random_grid(W, H, 21)
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=1200, decomp="1x3", tmax=4, epoch=8, poll_gens=16,
+                                    overlap=overlap, check_similarity=False), 3, engine="cpu")
+    grp.load(g)
+    modes0 = {s.describe()["poll_mode"] for s in grp.sims}
+    assert modes0 == {"auto:trial"}
+    reps = grp.run()  # termination polls every 16 generations
+    d = [s.describe() for s in grp.sims]
+    assert len({x["poll_mode"] for x in d}) == 1 and d[0]["poll_mode"] in ("auto:joined", "auto:side")
+    assert d[0]["poll_trial_ms_per_window"]["joined"] > 0 and d[0]["poll_trial_ms_per_window"]["side"] > 0
+    want, gens, _ = reference_run(g, 1200, check_similarity=False)
+    assert all(r.generations == gens for r in reps)
+    assert (grp.gather() == want).all()
+    # a terminating run while the trial is still open stops exactly where the serial loop does
+    g2 = random_grid(W, H, 95, 0.1)
+    ref, rgens, _ = reference_run(g2)
+    grp2 = InProcessGroup(LifeConfig(W, H, decomp="1x3", tmax=2, epoch=4, poll_gens=8, overlap=overlap), 3,
+                          engine="cpu")
+    grp2.load(g2)
+    assert all(r.generations == rgens for r in grp2.run())
+    assert (grp2.gather() == ref).all()
