@@ -264,7 +264,7 @@ def parse_args(argv=None):
     ap.add_argument("--tmax", type=int, default=0)
     ap.add_argument("--epoch", type=int, default=0)
     ap.add_argument("--poll", type=int, default=0)
-    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "edges", "trigger"])
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "trigger"])
     ap.add_argument("--graphs", default="off", choices=["auto", "on", "off"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--repeats", type=int, default=1, help="timed repetitions (best is reported)")

@@ -162,10 +162,6 @@ class Backend {
   virtual KernelChoice choose_kernel(Layout l, int64_t /*rows*/, int64_t /*cols*/, int tmax_req) const {
     return {tmax_req > 0 ? tmax_req : preferred_tmax(l), drifts(l)};
   }
-  // Fewest output rows a run_block of T generations accepts (the pipelined
-  // deep byte pass plans whole wave-pair groups); the engine keeps every
-  // block at least this tall or uses a smaller T.
-  virtual int64_t min_block_rows(Layout /*l*/, int /*T*/) const { return 1; }
   // Row ring (single-rank torus): a tile whose top Dv halo rows are a second
   // virtual mapping of its last Dv owned rows and whose bottom halo rows map
   // its first ones, so the periodic row halos are always valid and never

@@ -45,8 +45,6 @@ struct EngineConfig {
   //      the comm stream, waves at top issue priority), sends them, and
   //      computes the interior while they travel; every transport operation,
   //      the flag all-reduce included, runs on the comm stream;
-  //    2 edges: the edge strips are recomputed in scratch tiles while the
-  //      interior runs (round 1; eight small launches per epoch);
   //    3 trigger: the last temporal block of a full epoch runs as usual, but
   //      its boundary groups count themselves done on a device counter; with
   //      linked launches that block runs on the second compute stream, and
@@ -156,8 +154,8 @@ class Engine {
   Extent cols() const { return dec_.cols(rank_); }
   int epoch_depth() const { return D_; }
   int tmax() const { return tmax_; }
-  bool overlap() const { return overlap_ || early_ || trigger_; }
-  // "off" | "on" | "edges" | "auto:trial" | "auto:plain" | "auto:early".
+  bool overlap() const { return early_ || trigger_; }
+  // "off" | "on" | "trigger" | "auto:trial" | "auto:plain" | "auto:early" | "auto:trigger".
   std::string overlap_mode() const;
   // Median epoch time (ms, MAX over ranks) of the plain schedule and of the
   // alternative the auto trial measured (-1: not measured), and the
@@ -272,8 +270,6 @@ class Engine {
   // Waits for an early exchange still in flight; `invalidate` when the
   // buffers are about to change outside the schedule.
   void settle_pending(bool invalidate);
-  // d generations (d <= D_) with the row exchange overlapped (see engine.cpp).
-  void epoch_overlapped(int64_t d);
   void run_epoch(int64_t d);
   void release_graphs();
   int graph_key() const { return via_bits_ ? 2 * cur_ + bpar_ : cur_; }
@@ -304,7 +300,6 @@ class Engine {
   int64_t flags_base_ = 0, flags_len_ = 0;
   uint32_t* alive_dev_ = nullptr;
   void* colbuf_[4] = {nullptr, nullptr, nullptr, nullptr};  // send W, send E, recv W, recv E
-  bool overlap_ = false;             // edge-scratch schedule (overlap = 2)
   bool early_ = false;               // early-boundary schedule (overlap = 1)
   bool trigger_ = false;             // boundary-triggered sends (overlap = 3)
   bool comm_route_ = false;          // transport operations on the comm stream (multi-rank, overlap != 0)
@@ -327,8 +322,6 @@ class Engine {
   int64_t graph_runs_ = 0;
   int64_t halo_bytes_ = 0;
   double watchdog_s_ = 900;
-  TileGeom gs_;                     // edge scratch tile: D owned rows + D halo rows each side
-  void* edge_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [top|bottom][parity]
   int64_t gen_ = 0;
   int64_t exchanges_ = 0, polls_ = 0, launches_ = 0;
   bool drift_ok_ = false;   // whole-width tile of 32-cell words on a drifting backend

@@ -106,8 +106,6 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   // word per pass, so passes deeper than 16 (the byte layout's T = 24 / 32)
   // run the DPP window.
   if (x == kXlaneAdd && !(a.allow_drift && a.T <= 16 && (p.wrap_w > 0 || 32 * g.hw >= 2 * a.T))) x = kXlaneDpp;
-  // The pipelined T = 48 byte pass is compiled for the DPP window only.
-  if (g.layout == Layout::U8 && a.T > 32) x = kXlaneDpp;
   if (x == kXlaneAdd) {
     (g.layout == Layout::U8 ? launch_u8_w1_add : launch_bits_w1_add)(p, rows, a.T, tune, stream);
     return a.T;

@@ -494,7 +494,7 @@ __device__ __forceinline__ Vec<W> levels_full(Levels<T, W>& st, const Vec<W>& cu
 // Triangular prologue, fully unrolled: at step K only levels 1..K/2 hold
 // valid rows, so only those are evaluated; level K/2+1 just fills its
 // window.
-// RD: RowReader<IO>, or any source with take<S>(k) (life_pipe_impl.hpp's ring).
+// RD: RowReader<IO>, or any source with take<S>(k).
 template <int T, class IO, int K, class Save, class Bottom, class RD>
 __device__ __forceinline__ void prologue_tri(Levels<T, IO::W>& st, RD& rd, const Save& save, const Bottom& bottom) {
   if constexpr (K < 2 * T) {

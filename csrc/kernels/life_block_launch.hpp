@@ -4,14 +4,13 @@
 //   grouped  life_group_kernel (life_group_impl.hpp): default for T >= 4 when
 //            the rows allow M segments of 2T rows per group (GOL_GROUP);
 //            linked (two launches in flight) or chained where that pays
-//   pipe     life_pipe_kernel (life_pipe_impl.hpp): the byte layout's T = 48
-//            pass, each segment's levels split over a wave pair
 //   classic  life_block_kernel: T < 4, short tiles, GOL_GROUP=0
 // Schedules measured slower and removed in round 6 (docs/HISTORY.md): short
-// segments, bit-layout pipelined pairs, split and skewed schedules.
+// segments, level-pipelined wave pairs (bit layout, and the byte layout's
+// T = 48 pass, no faster than T = 32), split and skewed schedules.
 #pragma once
 
-#include "life_pipe_impl.hpp"
+#include "life_group_impl.hpp"
 
 namespace gol {
 namespace hipk {
@@ -257,48 +256,6 @@ void launch_deep(const LifeBlockParams& p, int64_t out_rows, const LifeTuning& t
   }                                                                                                \
   }
 
-// Deepest byte-layout pass (T = 48): level-pipelined wave pairs
-// (life_pipe_impl.hpp) of 24 + 24 levels with two halo lanes per wave side
-// (48 generations consume 1.5 words of the light cone; U8IO<1, XL, 2>), so
-// each wave keeps the register budget of a T = 24 grouped wave (252 VGPRs,
-// 2 waves per SIMD, no spills) while the pass reads and writes the byte
-// grid once per 48 generations:
-// two thirds of the HBM traffic per generation of the T = 32 pass, which is
-// HBM-bound at 32768^2 (docs/HISTORY.md "Byte layout").  32 + 32 levels
-// (T = 64) spill at 2 waves per SIMD (1064 VGPRs; 26 + 26 still 131).  Four
-// pairs per workgroup (108 KB of LDS).  A dual launch (the early-boundary
-// schedule's two strips) runs as two launches.
-template <int T1, int T2, class IO>
-void launch_deep_pipe(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipStream_t s) {
-  static_assert(IO::kHalo * 32 >= T1 + T2, "the wave's halo lanes must hold the pass's light cone");
-  constexpr int kWaveOut = wave_out_words<IO::XL, IO::W, IO::kHalo>();
-  p.ncolw = int(ceil_div(p.wrap_w ? p.wrap_w : p.Wp, kWaveOut));
-  p.fold = 1;
-  p.fold_lanes = 64;
-  const int64_t alt = p.row_alt;
-  p.row_alt = 0;
-  const int simds = 4 * std::max(1, tune.cus);
-  for (int half = 0; half < (alt ? 2 : 1); ++half) {
-    LifeBlockParams q = p;
-    q.row_lo += half * alt;
-    q.row_hi += half * alt;
-    const double c = plan_pipe<T1, T2, 4>(q, out_rows, simds, pipe_waves_per_simd<T1, T2, IO, 4>(),
-                                          tune.target_waves, IO::XL);
-    GOL_REQUIRE(c > 0, "life_block: " + std::to_string(out_rows) + " rows are too few for a T = " +
-                           std::to_string(T1 + T2) + " byte pass (HipBackend::choose_kernel)");
-    launch_pipe<T1, T2, IO, 4>(q, s);
-  }
-}
-#define GOL_U8_PIPE(KW, T1_, T2_, XL_)                                                                  \
-  namespace gol {                                                                                       \
-  namespace hipk {                                                                                      \
-  namespace lb {                                                                                        \
-  KW template void launch_deep_pipe<T1_, T2_, U8IO<1, XL_, 2>>(LifeBlockParams, int64_t, const LifeTuning&, \
-                                                               hipStream_t);                           \
-  }                                                                                                     \
-  }                                                                                                     \
-  }
-
 // Host entry point of one compiled variant (instantiated once per
 // translation unit, life_block_*.hip).
 template <class IO>
@@ -323,12 +280,6 @@ void launch_variant(const LifeBlockParams& p, int64_t out_rows, int T, const Lif
           launch_deep<32, IO>(p, out_rows, tune, s);
           break;
         }
-      }
-      [[fallthrough]];
-    case 48:
-      if constexpr (!IO::kBits && IO::XL == kXlaneDpp) {
-        launch_deep_pipe<24, 24, U8IO<1, kXlaneDpp, 2>>(p, out_rows, tune, s);
-        break;
       }
       [[fallthrough]];
     default: fail("life_block: unsupported temporal block size " + std::to_string(T));

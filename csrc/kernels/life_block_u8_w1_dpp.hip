@@ -3,7 +3,6 @@
 
 GOL_U8_DEEP(extern, 24, kXlaneDpp)
 GOL_U8_DEEP(extern, 32, kXlaneDpp)
-GOL_U8_PIPE(extern, 24, 24, kXlaneDpp)
 
 namespace gol {
 namespace hipk {

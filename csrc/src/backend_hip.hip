@@ -80,7 +80,6 @@ class HipBackend final : public Backend {
     tune_.wrap = t.on("wrap");
     tune_.fold = t.on("fold");
     chain_mode_ = t.i("chain");
-    u8_pipe_ = t.on("u8_pipe");
     // Linked launches: consecutive grouped launches of an epoch overlap on
     // two streams, ordered by per-group completion words (LifeBlockParams::
     // link_*): small tiles whose launches alone hold only 2 waves per SIMD.
@@ -735,11 +734,8 @@ class HipBackend final : public Backend {
   // give every SIMD one is taken; below that T = 16 (8192^2: 2.83 vs 3.03 at
   // 24; 32768 x 4096: 3.7-3.9 vs 4.4 at 24 and 4.9 at 32;
   // profiles/r02/u8_t24*.jsonl, u8_t32.jsonl).
-  //
-  // Deeper still, T = 48 runs as level-pipelined wave pairs (24 + 24
-  // levels, four pairs per workgroup, 2 waves per SIMD): taken when the tile
-  // gives every CU a workgroup of four pairs of at least 2T + 2 rows plus the
-  // group's T - 1 boundary rows (GOL_U8_PIPE=0: off).
+  // (A T = 48 pass as level-pipelined wave pairs ran no faster than T = 32,
+  // the byte kernels being VALU-bound: removed in round 6, HISTORY.md.)
   KernelChoice choose_kernel(Layout l, int64_t rows, int64_t cols, int tmax_req) const override {
     KernelChoice k{tmax_req > 0 ? tmax_req : preferred_tmax(l), false};
     if (l == Layout::U8 && tmax_req <= 0 && !tune_.u8_lds) {
@@ -750,12 +746,6 @@ class HipBackend final : public Backend {
           k.tmax = int(kT);
           break;
         }
-      if (u8_pipe_)
-        for (int64_t kT : {48})
-          if (strips * (rows / (4 * (2 * kT + 2) + kT - 1)) >= int64_t(cus_)) {
-            k.tmax = int(kT);
-            break;
-          }
     }
     if (tune_.xlane == hipk::kXlaneAdd && !(l == Layout::U8 && tune_.u8_lds)) {
       k.drift = true;
@@ -788,9 +778,6 @@ class HipBackend final : public Backend {
       k.link = strips * (rows / (2 * k.tmax)) >= int64_t(6) * cus_;
     }
     return k;
-  }
-  int64_t min_block_rows(Layout l, int T) const override {
-    return l == Layout::U8 && T > 32 ? int64_t(4) * (2 * T + 2) + T - 1 : 1;
   }
   bool wraps_columns(Layout l) const override { return tune_.wrap; }
   // The LDS-tiled byte kernels read rows modulo the torus too.
@@ -1057,7 +1044,6 @@ class HipBackend final : public Backend {
   bool link_on_ = false;  // every eligible launch (GOL_LINK=1)
   int link_mode_ = -1;
   uint32_t chain_seq_ = 0;
-  bool u8_pipe_ = true;  // GOL_U8_PIPE: T = 48 byte passes
   // Boundary trigger: cumulative device counter, increments expected so
   // far, and the target of the last armed launch (0: none pending).
   unsigned long long* trigger_counter() {

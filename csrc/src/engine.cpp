@@ -12,10 +12,9 @@
 namespace gol {
 
 namespace {
-// Temporal block sizes built for every backend; 48, 32 and 24 for the byte
-// layout only (HBM-bound there: one grid read + write per pass,
-// docs/PERFORMANCE.md; 48 as level-pipelined wave pairs).
-constexpr int kTSizes[] = {48, 32, 24, 16, 12, 8, 4, 2, 1};
+// Temporal block sizes built for every backend; 32 and 24 for the byte
+// layout only (one grid read + write per pass, docs/PERFORMANCE.md).
+constexpr int kTSizes[] = {32, 24, 16, 12, 8, 4, 2, 1};
 
 // Phases of RunResult's device-time split.
 enum Phase { kCompute = 0, kHalo = 1, kFill = 2, kReduce = 3, kPhases = 4 };
@@ -58,7 +57,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // made for the smallest tile of the decomposition, not this rank's.
   const Backend::KernelChoice kc =
       be_->choose_kernel(cl, min_tile_rows(dec_), std::max<int64_t>(1, min_tile_cols(dec_)), cfg_.tmax);
-  tmax_ = std::min(kc.tmax, cl == Layout::U8 ? 48 : 16);
+  tmax_ = std::min(kc.tmax, cl == Layout::U8 ? 32 : 16);
   // Epoch depth: a deeper halo means fewer latency-bound exchanges (or local
   // periodic fills: two ~5 us launches each) but ~D redundant rows per epoch.
   // With the grouped kernel the per-rank tile costs the same from 8T to 24T
@@ -75,16 +74,6 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   }
   D_ = std::max(1, D);
   tmax_ = std::min(tmax_, D_);
-  // The smallest block of any schedule: the owned rows (a trapezoid's last
-  // block) and, where the row exchange may overlap compute, D rows (an edge
-  // strip, the early-boundary strips) and the interior (H - 2D).  A deep pass
-  // that cannot plan that few rows steps down to the next T.
-  {
-    const int64_t h = min_tile_rows(dec_);
-    int64_t min_rows = h;
-    if (row_exchange && h >= 2 * int64_t(D_) + 1) min_rows = std::min({h, int64_t(D_), h - 2 * int64_t(D_)});
-    while (tmax_ > 1 && be_->min_block_rows(cl, tmax_) > min_rows) tmax_ = pick_T(tmax_ - 1);
-  }
   // A drifting kernel (one-sided window, Backend::drifts) consumes 2 cells of
   // left halo per generation and none on the right; it needs the tile to be
   // the whole torus width so that the drift is a relabeling of columns.
@@ -186,7 +175,6 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // epoch), which on the 32768 x 4096 per-rank tile cost 4x more than the
   // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
   const bool interior = min_tile_rows(dec_) >= 2 * int64_t(D_) + 1;  // on every rank
-  overlap_ = row_exchange && cfg_.overlap == 2 && interior && !via_bits_;
   const bool early_ok = row_exchange && dec_.Px == 1 && interior && !via_bits_;
   early_ = early_ok && cfg_.overlap == 1;
   // Boundary-triggered sends (overlap = 3; last_block_trigger): row strips
@@ -201,12 +189,6 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // cost more than the all-reduce it takes off the compute stream
   // (profiles/r02/rehearsal_overlap.jsonl).
   comm_route_ = early_;  // the trigger schedule keeps its exchanges on the compute stream
-  if (overlap_) {
-    gs_ = TileGeom::make(cfg_.layout, D_, g_.W, D_, g_.hw);
-    GOL_REQUIRE(gs_.pitch == g_.pitch, "edge scratch pitch mismatch");
-    for (auto& e : edge_)
-      for (auto& b : e) b = be_->alloc(size_t(gs_.bytes()));
-  }
   watchdog_s_ = cfg_.watchdog_s > 0 ? cfg_.watchdog_s : cfg_.tune.f("watchdog_s") > 0 ? cfg_.tune.f("watchdog_s") : 900.0;
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
@@ -273,9 +255,6 @@ Engine::~Engine() {
     if (b) be_->release(b);
   for (auto& b : bitbuf_)
     if (b) be_->release(b);
-  for (auto& e : edge_)
-    for (auto& b : e)
-      if (b) be_->release(b);
   if (flags_) be_->release(flags_);
   if (flags_host_) be_->release_host(flags_host_);
   if (alive_dev_) be_->release(alive_dev_);
@@ -447,79 +426,6 @@ void Engine::halo_exchange_on(void* buf, const TileGeom& g) {
   ++exchanges_;
 }
 
-// Overlapped epoch (Py > 1).  The reference exchanges halos and then waits
-// (MPI_Startall + MPI_Waitall, src/game_mpi.c:392-401) before computing.
-// Here the D-generation dependence cone splits the tile in three:
-//   interior  owned rows only; after d gens rows [Dv+d, Dv+H-d) are exact.
-//             Needs no halo, so it runs while the rows are in flight.
-//   top edge  scratch tile [north halo (D) | owned rows Dv..Dv+2D) ]; after
-//             d <= D gens its rows [D, 2D) = owned rows [Dv, Dv+D) are exact.
-//   bottom    mirror image.
-// The edges are copied to scratch first, so the sends read the scratch and
-// the interior may overwrite the main buffers at once.  Stream order:
-//   compute: cols -> copy edges -> mark A -> interior blocks -> wait B ->
-//            edge blocks -> copy edge results back
-//   comm:    wait A -> send/recv rows (into the scratch halos) -> mark B
-// Every computed row holds real cells, so the changed flags of all three
-// regions OR together exactly as in the plain schedule.
-void Engine::epoch_overlapped(int64_t d) {
-  trace::Range tr("gol.epoch_overlapped");
-  auto nb = dec_.neighbors(rank_);
-  const int64_t D = D_, H = g_.H, Dv = g_.Dv, pitch = g_.pitch;
-  auto* main_in = static_cast<uint8_t*>(buf_[cur_]);
-  exchange_columns(main_in, g_);
-  auto* top = static_cast<uint8_t*>(edge_[0][0]);
-  auto* bot = static_cast<uint8_t*>(edge_[1][0]);
-  be_->copy_2d_async(top + D * pitch, pitch, main_in + Dv * pitch, pitch, pitch, 2 * D);
-  be_->copy_2d_async(bot, pitch, main_in + (Dv + H - 2 * D) * pitch, pitch, pitch, 2 * D);
-  void* comm = be_->comm_stream();
-  be_->stream_wait(comm, be_->stream_mark(nullptr));
-  const size_t bytes = size_t(D * pitch);
-  std::vector<P2POp> ops = {
-      {true, nb[kNorth], top + D * pitch, bytes},      // my top rows -> north's bottom-edge halo
-      {false, nb[kSouth], bot + 2 * D * pitch, bytes},  // south's top rows -> my bottom-edge halo
-      {true, nb[kSouth], bot + D * pitch, bytes},       // my bottom rows -> south's top-edge halo
-      {false, nb[kNorth], top, bytes},                  // north's bottom rows -> my top-edge halo
-  };
-  void* t = phase_begin(comm);
-  tr_->exchange(ops, comm ? comm : be_->stream());
-  phase_end(kHalo, t, comm);
-  halo_bytes_ += 2 * int64_t(bytes);
-  void* rows_done = be_->stream_mark(comm);
-  ++exchanges_;
-
-  // Interior: trapezoid over the owned rows.
-  int64_t a = 0, rem = d;
-  int par = 0;
-  std::vector<int> Ts;
-  while (rem > 0) {
-    const int T = pick_T(rem);
-    Ts.push_back(T);
-    add_drift(launch(buf_[cur_ ^ par], buf_[cur_ ^ par ^ 1], g_, T, Dv + a + T, Dv + H - a - T, gen_ + a));
-    a += T;
-    rem -= T;
-    par ^= 1;
-  }
-  // Edges, once their halos have arrived.
-  be_->stream_wait(nullptr, rows_done);
-  for (int e = 0; e < 2; ++e) {
-    int64_t ea = 0;
-    int ep = 0;
-    for (int T : Ts) {
-      launch(edge_[e][ep], edge_[e][ep ^ 1], gs_, T, ea + T, gs_.R() - ea - T, gen_ + ea);
-      ea += T;
-      ep ^= 1;
-    }
-  }
-  auto* main_out = static_cast<uint8_t*>(buf_[cur_ ^ par]);
-  be_->copy_2d_async(main_out + Dv * pitch, pitch, static_cast<uint8_t*>(edge_[0][par]) + D * pitch, pitch,
-                     pitch, D);
-  be_->copy_2d_async(main_out + (Dv + H - D) * pitch, pitch, static_cast<uint8_t*>(edge_[1][par]) + D * pitch,
-                     pitch, pitch, D);
-  cur_ ^= par;
-  gen_ += d;
-}
-
 void* Engine::bit_scratch(int i) const {
   if (bitbuf_[i]) return bitbuf_[i];
   return static_cast<uint8_t*>(buf_[cur_ ^ 1]) + i * gb_.bytes();
@@ -581,10 +487,6 @@ void Engine::unpack_bits() {
 }
 
 void Engine::run_epoch(int64_t d) {
-  if (overlap_) {
-    epoch_overlapped(d);
-    return;
-  }
   const bool sent_early = rows_pending_;
   if (rows_pending_) {
     // The previous epoch sent this buffer's boundary rows early.
@@ -1061,7 +963,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.exchanges = exchanges_ - e0;
   res.polls = polls_ - p0;
   res.kernel_launches = launches_ - l0;
-  res.overlapped = overlap_ || early_sends_ > es0;
+  res.overlapped = early_sends_ > es0;
   res.graph_launches = graph_runs_ - g0;
   res.halo_bytes = halo_bytes_ - hb0;
   res.linked_launches = be_->linked_launches() - lk0;
@@ -1219,7 +1121,6 @@ void Engine::auto_decide() {
 }
 
 std::string Engine::overlap_mode() const {
-  if (overlap_) return "edges";
   if (cfg_.overlap == 1) return early_ ? "on" : "off";
   if (cfg_.overlap == 3) return trigger_ ? "trigger" : "off";
   if (cfg_.overlap == -1) {

@@ -37,7 +37,6 @@ const std::vector<TuningKey>& tuning_keys() {
       {"lds_pack", "GOL_LDS_PACK", "1", 'i', "tune", "LDS kernel packs its tile to bits"},
       {"lds_xcd", "GOL_LDS_XCD", "0", 'i', "tune", "XCD-aware tile order of the LDS kernel"},
       {"lds_waves", "GOL_LDS_WAVES", "0", 'i', "tune", "LDS kernel waves per block: 0 auto, 8 or 16"},
-      {"u8_pipe", "GOL_U8_PIPE", "1", 'i', "tune", "byte passes of T = 48 as level-pipelined wave pairs"},
       {"u8_via_bits", "GOL_U8_VIA_BITS", "-1", 'i', "tune",
        "byte layout computes on bit words: -1 auto, 0 bytes, 1 bits (EngineConfig::u8_compute wins when set)"},
       {"side_poll", "GOL_SIDE_POLL", "-1", 'i', "tune",

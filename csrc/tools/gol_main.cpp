@@ -100,11 +100,11 @@ struct Options {
                "                              has a GPU of its own, else thread)\n"
                "  --decomp auto|PxQ           process grid (Px columns x Py rows)\n"
                "  --tmax T --epoch D --poll N temporal block, halo depth, poll interval\n"
-               "  --overlap auto|on|off|edges|trigger\n"
+               "  --overlap auto|on|off|trigger\n"
                "                              trigger = an epoch's new boundary rows are sent as soon\n"
                "                              as the groups writing them finish; on = early boundary\n"
-               "                              strips in a launch of their own; edges = recomputed edge\n"
-               "                              strips; off = no overlap; auto = time plain against\n"
+               "                              strips in a launch of their own; off = no overlap;\n"
+               "                              auto = time plain against\n"
                "                              trigger (or early) epochs on the ranks, keep the faster\n"
                "  --graphs auto|on|off        replay full epochs as captured HIP graphs\n"
                "  --threads N                 host threads for the cpu engine\n"
@@ -168,7 +168,8 @@ Options parse(int argc, char** argv) {
     else if (a == "--poll" || a == "--poll-every") o.poll = std::atoi(next().c_str());
     else if (a == "--overlap") {
       std::string v = next();
-      o.overlap = v == "on" ? 1 : v == "off" ? 0 : v == "edges" ? 2 : v == "trigger" ? 3 : -1;
+      GOL_REQUIRE(v == "auto" || v == "on" || v == "off" || v == "trigger", "--overlap: auto, on, off or trigger");
+      o.overlap = v == "on" ? 1 : v == "off" ? 0 : v == "trigger" ? 3 : -1;
     } else if (a == "--graphs") {
       std::string v = next();
       o.graphs = v == "on" ? 1 : v == "off" ? 0 : -1;

@@ -42,7 +42,7 @@ class LifeConfig:
                                 # 16 DPP; u8 32 / 24 / 16 by tile size)
     epoch: int = 0              # generations per halo exchange (0 = 8*tmax, 16*tmax with several ranks)
     poll_gens: int = 0          # generations between termination polls (0 = 256, 512 with several ranks)
-    overlap: str = "auto"       # auto | on | off | edges | trigger: overlap the row halo exchange with compute
+    overlap: str = "auto"       # auto | on | off | trigger: overlap the row halo exchange with compute
     lagged_poll: bool = True    # check termination polls one window late (no queue drain)
     graphs: str = "off"         # auto | on | off: replay full epochs as captured HIP graphs
     start_gen: int = 0          # resume: generation number of the initial state
@@ -77,7 +77,7 @@ class LifeConfig:
         c.tmax = int(self.tmax)
         c.epoch = int(self.epoch)
         c.poll_gens = int(self.poll_gens)
-        c.overlap = {"auto": -1, "off": 0, "on": 1, "edges": 2, "trigger": 3}[self.overlap]
+        c.overlap = {"auto": -1, "off": 0, "on": 1, "trigger": 3}[self.overlap]
         c.lagged_poll = bool(self.lagged_poll)
         c.graphs = {"auto": -1, "off": 0, "on": 1}[self.graphs]
         c.start_gen = int(self.start_gen)

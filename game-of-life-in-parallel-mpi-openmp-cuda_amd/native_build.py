@@ -35,11 +35,10 @@ HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/t
 # window), so the build compiles them in parallel.  The variants measured
 # slower than these (resident epochs, persistent dataflow launches, short
 # segments, split / skewed schedules, ds_bpermute and carry-chain windows, two
-# words per lane) were removed in round 6; their code is in git history
+# words per lane, the byte layout's T = 48 pipelined pass) were removed in round 6; their code is in git history
 # (docs/HISTORY.md) and their numbers in docs/HISTORY.md / PERFORMANCE.md.
 LIFE_VARIANTS = ["bits_w1_dpp", "bits_w1_add", "u8_w1_dpp", "u8_w1_add",
-                 *[f"u8_w1_dpp_t{t}" for t in (24, 32)],  # deep byte passes
-                 "u8_w1_dpp_t48"]  # pipelined wave pairs (life_pipe_impl.hpp)
+                 *[f"u8_w1_dpp_t{t}" for t in (24, 32)]]  # deep byte passes
 HIP_SRCS = ["src/backend_hip.hip", "src/transport_rccl.hip", "kernels/life_block.hip",
             *[f"kernels/life_block_{v}.hip" for v in LIFE_VARIANTS], "kernels/life_step_lds.hip",
             "kernels/tile_ops.hip"]

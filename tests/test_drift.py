@@ -68,12 +68,13 @@ def test_drift_needs_whole_width_tiles(native, tune):
 
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x3", 3), ("1x4", 4)])
-@pytest.mark.parametrize("overlap", ["off", "on", "edges"])
+@pytest.mark.parametrize("overlap", ["off", "on", "trigger"])
 def test_drift_row_strips_and_overlap(native, tune, spec, P, overlap):
     """Row strips (the multi-GPU default) drift in lockstep on every rank;
-    the early-boundary launches and the edge scratch tiles drift with the
+    the early-boundary and boundary-trigger launches drift with the
     interior."""
     tune["cpu_drift"] = "1"
+    tune["cpu_trigger"] = "1"
     W, H = 192, 120
     g = random_grid(W, H, P + 40)
     ref, rgens, _ = reference_run(g, 200)

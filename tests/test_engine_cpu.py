@@ -35,11 +35,11 @@ def test_temporal_block_and_epoch_variants(native, tmax, epoch):
 
 
 @pytest.mark.parametrize("epoch", [0, 50, 96, 200])
-def test_deep_byte_schedule_t48(native, epoch):
-    """The byte layout's T = 48 schedule (kTSizes 48 / 32 / 24 ... split of
-    an epoch) on the CPU backend, with and without an early-stop poll."""
+def test_deep_byte_schedule_t32(native, epoch):
+    """The byte layout's deep schedule (kTSizes 32 / 24 / 16 ... split of an
+    epoch) on the CPU backend, with and without an early-stop poll."""
     g = random_grid(70, 120, 5)
-    got = life_step(g, 211, engine="cpu", layout="u8", tmax=48, epoch=epoch)
+    got = life_step(g, 211, engine="cpu", layout="u8", tmax=32, epoch=epoch)
     assert (got == life_step_numpy(g, 211)).all()
 
 

@@ -60,14 +60,13 @@ def test_random_init_decomposition_independent(native, tune):
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x3", 3), ("2x2", 4), ("2x3", 6)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("tmax,epoch", [(4, 8), (8, 8), (4, 12), (2, 5)])
-@pytest.mark.parametrize("mode", ["on", "edges", "trigger"])
+@pytest.mark.parametrize("mode", ["on", "trigger"])
 def test_overlapped_exchange_matches_serial(native, tune, spec, P, layout, tmax, epoch, mode):
     """Overlapped epochs are bit-identical to the serial reference, including
     a short final epoch (gens not a multiple of the epoch depth):
       on       early boundary rows: the last block of an epoch computes the 2D
                boundary rows, sends them, then computes the interior (row
                strips only, Px == 1);
-      edges    interior during the row exchange, edge strips in scratch tiles;
       trigger  the last block's boundary rows are sent once the groups
                writing them are done (row strips; the CPU backend emulates
                the counter, tuning cpu_trigger)."""
@@ -81,7 +80,7 @@ def test_overlapped_exchange_matches_serial(native, tune, spec, P, layout, tmax,
     grp = InProcessGroup(cfg, P, engine="cpu")
     grp.load(g)
     reps = grp.run()
-    want = mode == "edges" or spec.startswith("1x")
+    want = spec.startswith("1x")
     assert all(r.overlapped == want for r in reps)
     if mode == "trigger":
         assert all(s.native_engine.triggered_sends() == (3 if want else 0) for s in grp.sims)
@@ -90,7 +89,7 @@ def test_overlapped_exchange_matches_serial(native, tune, spec, P, layout, tmax,
 
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
 @pytest.mark.parametrize("lagged", [True, False])
-@pytest.mark.parametrize("mode", ["on", "edges", "trigger"])
+@pytest.mark.parametrize("mode", ["on", "trigger"])
 def test_overlapped_termination(native, tune, W, H, seed, density, lagged, mode):
     tune["cpu_trigger"] = "1"
     g = random_grid(W, H, seed, density)
@@ -107,15 +106,15 @@ def test_overlapped_termination(native, tune, W, H, seed, density, lagged, mode)
 
 
 def test_overlap_modes(native, tune):
-    """on = early boundary rows on row strips with H > 2D; edges = the
-    round-1 edge-strip schedule; auto only moves the transport operations to
-    the comm stream; column decompositions do not overlap."""
+    """on = early boundary rows on row strips with H > 2D; trigger = the
+    boundary rows sent once the groups writing them are done; auto decides
+    on the ranks; column decompositions do not overlap."""
     def ov(**kw):
         cfg = dict(decomp="1x2", tmax=4, epoch=16)
         cfg.update(kw)
         H = cfg.pop("H", 512)
         return InProcessGroup(LifeConfig(64, H, **cfg, tune=tune), 2, engine="cpu").sims[0].native_engine.overlap()
-    assert ov(overlap="on") and ov(overlap="edges")
+    assert ov(overlap="on")
     assert not ov() and not ov(overlap="off")
     assert not ov(H=40, overlap="on")  # tile rows 20 <= 2D
     assert not ov(decomp="2x1", overlap="on")
@@ -210,7 +209,7 @@ def test_thread_transport_pair_matching_two_ranks(native, tune):
         assert (halo_n[r] == bot[1 - r]).all()  # north neighbour's bottom rows -> my top halo
 
 
-@pytest.mark.parametrize("mode", ["auto", "edges"])
+@pytest.mark.parametrize("mode", ["auto", "on"])
 def test_overlap_decision_is_global_on_uneven_tiles(native, tune, mode):
     """37 rows over 3 ranks = tiles of 12, 12, 13 rows; with D = 6 only the
     13-row tile has H > 2D.  Every rank must take the same schedule (a rank
@@ -228,12 +227,13 @@ def test_overlap_decision_is_global_on_uneven_tiles(native, tune, mode):
     assert (grp.gather() == ref).all()
 
 
-@pytest.mark.parametrize("overlap", ["off", "on", "edges"])
+@pytest.mark.parametrize("overlap", ["off", "on", "trigger"])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 def test_self_exchange_rehearsal(native, tune, overlap, layout):
     """One rank rehearsing the multi-rank row-strip schedule (bench.py
     --rehearse-rccl): halos go through the transport to itself, with the
     multi-rank epoch depth and overlap; results equal the serial loop."""
+    tune["cpu_trigger"] = "1"
     W, H = 128, 200
     g = random_grid(W, H, 12)
     ref, rgens, _ = reference_run(g, 120)

@@ -44,7 +44,7 @@ def _torchrun(nproc, args, timeout=240):
 
 
 @pytest.mark.parametrize("nproc,cases", [
-    (2, "1x2:bits:auto,1x2:u8:on,2x1:bits:off,1x2:bits:edges"),
+    (2, "1x2:bits:auto,1x2:u8:on,2x1:bits:off,1x2:bits:trigger"),
     (4, "1x4:bits:auto,2x2:bits:off,2x2:u8:auto,1x4:u8:off"),
     # The node's rank count (bench.py --gpus 8): 1x8 row strips (the default
     # split) and 2x4 blocks with column halos, plus termination.
