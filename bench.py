@@ -269,7 +269,7 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--repeats", type=int, default=1, help="timed repetitions (best is reported)")
     ap.add_argument("--rehearse-rccl", action="store_true",
-                    help="one GPU: run the multi-rank row-strip schedule (epoch depth, early-boundary overlap, "
+                    help="one GPU: run the multi-rank row-strip schedule (epoch depth, boundary-trigger overlap, "
                          "RCCL send/recv + all-reduce) against a 1-rank RCCL communicator that exchanges with "
                          "itself; use with --height H/N to rehearse one rank of an N-GPU run")
     ap.add_argument("--share-gpus", action="store_true",
@@ -596,7 +596,7 @@ def main() -> int:
                 "overlapped_halo_exchange": bool(rs and rs[-1].overlapped),
                 "overlap_mode": desc["overlap_mode"],
                 "overlap_trial_ms_per_epoch": {"plain": desc["overlap_trial_ms_plain"],
-                                               desc["overlap_alternative"]: desc["overlap_trial_ms_early"]},
+                                               "trigger": desc["overlap_trial_ms_trigger"]},
                 "triggered_sends": desc["triggered_sends"],
                 "poll_mode": desc["poll_mode"],
                 "poll_trial_ms_per_window": desc["poll_trial_ms_per_window"],

@@ -38,14 +38,8 @@ struct EngineConfig {
   int tmax = 0;                    // max generations per kernel launch (0 = backend default)
   int epoch = 0;                   // generations per halo exchange (0 = auto)
   int poll_gens = 0;               // generations between termination polls (0 = auto)
-  // Overlap communication with compute (multi-rank, opt-in; measured slower
-  // than the plain schedule with deep halos, docs/PERFORMANCE.md):
-  //    1 on: early boundary (row strips, H > 2D): the last temporal block of
-  //      an epoch computes the 2 x D boundary rows first (one dual launch on
-  //      the comm stream, waves at top issue priority), sends them, and
-  //      computes the interior while they travel; every transport operation,
-  //      the flag all-reduce included, runs on the comm stream;
-  //    3 trigger: the last temporal block of a full epoch runs as usual, but
+  // Overlap the epoch's halo exchange with compute (row strips, Px == 1):
+  //    3 trigger (1 on is the same): the last temporal block of a full epoch runs as usual, but
   //      its boundary groups count themselves done on a device counter; with
   //      linked launches that block runs on the second compute stream, and
   //      the first one - idle once the block before it is done - waits on the
@@ -54,15 +48,16 @@ struct EngineConfig {
   //      block follows the exchange on that stream and still links to the
   //      last block, so the chain runs through the epoch boundary.  No dual
   //      launch, no spinning consumer, no comm-stream hop; byte tiles on bit
-  //      words included;
+  //      words included.  (Rounds 1-5 also had an early-boundary schedule - a
+  //      dual launch of the boundary strips on the comm stream - and an edge-
+  //      strip schedule; both measured slower and were removed, docs/HISTORY.md);
   //    0 off: everything on the compute stream;
-  //   -1 auto: where an overlapped schedule applies (row strips), the first
-  //      epochs alternate the plain schedule and the alternative (trigger
-  //      where the backend supports it, else early boundary), every rank
-  //      times them with events, the per-epoch medians are MAX-reduced over
-  //      ranks, and all ranks keep the faster one (GOL_OVERLAP_AUTO=plain|
-  //      early|trigger forces the outcome after the trial, for tests);
-  //      elsewhere as off.
+  //   -1 auto: where the trigger schedule applies (row strips on a backend
+  //      that supports it), the first epochs alternate it with the plain
+  //      schedule, every rank times them with events, the per-epoch medians
+  //      are MAX-reduced over ranks, and all ranks keep the faster one
+  //      (GOL_OVERLAP_AUTO=plain|trigger forces the outcome after the trial,
+  //      for tests); elsewhere as off.
   int overlap = -1;
   // Check each termination poll one poll window later, so the host never
   // drains the device queue (stops are absorbing, so running past is exact).
@@ -95,8 +90,8 @@ struct EngineConfig {
   //      rows back: two byte passes per run instead of one per temporal block
   //      (docs/PERFORMANCE.md);
   //    0 bytes: temporal blocks on the byte grid itself (the byte kernels);
-  //   -1 auto: bits on a device backend with the plain or auto schedule
-  //      (GOL_U8_VIA_BITS=0|1 overrides), else bytes.
+  //   -1 auto: bits on a device backend (GOL_U8_VIA_BITS=0|1 overrides),
+  //      else bytes.
   int u8_compute = -1;
   // Runtime tuning (gol/tuning.hpp): the engine's own knobs (u8_via_bits,
   // side_poll, cpu_side_poll, poll_copy_side, watchdog_s, pitch_pad, overlap_auto) come from here; the
@@ -154,13 +149,13 @@ class Engine {
   Extent cols() const { return dec_.cols(rank_); }
   int epoch_depth() const { return D_; }
   int tmax() const { return tmax_; }
-  bool overlap() const { return early_ || trigger_; }
-  // "off" | "on" | "trigger" | "auto:trial" | "auto:plain" | "auto:early" | "auto:trigger".
+  bool overlap() const { return trigger_; }
+  // "off" | "trigger" | "auto:trial" | "auto:plain" | "auto:trigger".
   std::string overlap_mode() const;
-  // Median epoch time (ms, MAX over ranks) of the plain schedule and of the
-  // alternative the auto trial measured (-1: not measured), and the
-  // alternative's name ("trigger" or "early").
+  // Median epoch time (ms, MAX over ranks) of the plain and the trigger
+  // schedule in the auto trial (-1: not measured).
   double trial_ms_plain() const { return auto_ms_[0]; }
+  double trial_ms_trigger() const { return auto_ms_[1]; }
   // Termination polls: "joined" (the flag all-reduce on the compute stream),
   // "side" (a side stream, tuning side_poll=1), "auto:trial", "auto:side" or
   // "auto:joined" (side_poll = -1, decided on the ranks), and the trial's
@@ -168,8 +163,6 @@ class Engine {
   std::string poll_mode() const;
   double poll_trial_ms_joined() const { return poll_ms_[0]; }
   double poll_trial_ms_side() const { return poll_ms_[1]; }
-  double trial_ms_early() const { return auto_ms_[1]; }
-  std::string trial_alternative() const { return auto_alt_ == 3 ? "trigger" : "early"; }
   // Epoch exchanges started by the boundary trigger so far (diagnostics).
   int64_t triggered_sends() const { return triggered_sends_; }
   // Sample per-phase device times into RunResult (event pairs around every
@@ -240,7 +233,6 @@ class Engine {
   // One temporal block in <in> -> <out> for generations (gen_base, gen_base+T];
   // returns the frame drift of the launch (cells).
   int launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t gen_base,
-             void* stream = nullptr, int64_t dual_offset = 0, bool prio_boost = false,
              const int64_t* trigger_rows = nullptr, bool hot_only = false);
   // A block of a trigger epoch before its last: the boundary rows' light
   // cone at top issue priority (engine.cpp).
@@ -255,19 +247,10 @@ class Engine {
   void unpack_bits();
   void sync_bytes();  // unpack a live bit image into the byte tile (pack_bits in engine.cpp)
   void* bit_scratch(int i) const;
-  // Stream carrying this engine's transport operations (comm stream in the
-  // early-boundary schedule, else the compute stream), and the two orderings.
-  void* rccl_stream() const;
-  void comm_after_compute();
-  void compute_after_comm();
-  // Last block of a full epoch in the early-boundary schedule (engine.cpp).
-  void last_block_early(int T);
   // Last block of a full epoch in the trigger schedule, in -> out on tile g
   // (the byte tile or its bit image); the caller flips its buffer parity.
   void last_block_trigger(void* in, void* out, const TileGeom& g, int T);
-  // Schedule of the next epochs: 0 plain, 1 early boundary, 3 trigger.
-  void set_schedule(int s);
-  // Waits for an early exchange still in flight; `invalidate` when the
+  // Waits for a triggered exchange still in flight; `invalidate` when the
   // buffers are about to change outside the schedule.
   void settle_pending(bool invalidate);
   void run_epoch(int64_t d);
@@ -300,13 +283,10 @@ class Engine {
   int64_t flags_base_ = 0, flags_len_ = 0;
   uint32_t* alive_dev_ = nullptr;
   void* colbuf_[4] = {nullptr, nullptr, nullptr, nullptr};  // send W, send E, recv W, recv E
-  bool early_ = false;               // early-boundary schedule (overlap = 1)
   bool trigger_ = false;             // boundary-triggered sends (overlap = 3)
-  bool comm_route_ = false;          // transport operations on the comm stream (multi-rank, overlap != 0)
   int64_t triggered_sends_ = 0;
   bool send_next_ = false;           // the current epoch is followed by another one in this run
-  bool rows_pending_ = false;        // halo rows of buf_[cur_] were sent early
-  void* rows_arrived_ = nullptr;     // comm-stream mark: they have arrived
+  bool rows_pending_ = false;        // halo rows of buf_[cur_] were sent by the last block
   int64_t early_sends_ = 0;
   bool use_graphs_ = false, capturing_ = false;
   int64_t* gen_dev_ = nullptr;        // device: (epoch start - flags_base_) for graph replays
@@ -343,8 +323,7 @@ class Engine {
   // Overlap auto trial.
   bool auto_overlap_ = false;       // trial still running
   bool auto_decided_ = false;
-  int auto_sched_ = 0;              // trial slot of the current epoch: 0 plain, 1 the alternative
-  int auto_alt_ = 1;                // the alternative: 1 early boundary, 3 trigger
+  int auto_sched_ = 0;              // trial slot of the current epoch: 0 plain, 1 trigger
   int64_t auto_full_epochs_ = 0;    // full epochs seen so far
   void* auto_open_ = nullptr;       // start mark of the current epoch
   int auto_open_sched_ = -1;        // its schedule (-1: not a trial epoch)

@@ -78,14 +78,6 @@ struct BlockArgs {
   // drifts right by T cells, which run_block reports.  Only valid when the
   // tile is the whole torus width (the drift is a relabeling of columns).
   bool allow_drift = false;
-  // Also evaluate the same rows shifted down by dual_offset (> 0) in the same
-  // launch (the two boundary strips of an epoch's last block), and the
-  // stream to enqueue on (nullptr = the backend's compute stream).
-  int64_t dual_offset = 0;
-  void* stream = nullptr;
-  // Run the launch's waves at the highest issue priority (s_setprio 3): the
-  // small boundary launch that runs beside the interior of the same block.
-  bool prio_boost = false;
   // The tile is the whole torus (one rank): a backend that wraps row reads
   // too (Backend::wraps_rows) reads rows modulo the owned rows, so the engine
   // neither fills nor exchanges halo rows.

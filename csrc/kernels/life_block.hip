@@ -38,8 +38,7 @@ int life_block_max_T(Layout layout, const LifeTuning& tune) {
 
 int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t stream) {
   const TileGeom& g = a.g;
-  GOL_REQUIRE(a.row_lo - a.T >= 0 && a.row_hi + a.T + a.dual_offset <= g.R() && a.row_lo < a.row_hi &&
-                  a.dual_offset >= 0 && (a.dual_offset == 0 || a.dual_offset >= a.row_hi - a.row_lo),
+  GOL_REQUIRE(a.row_lo - a.T >= 0 && a.row_hi + a.T <= g.R() && a.row_lo < a.row_hi,
               "life_block: row range outside the tile");
   GOL_REQUIRE(g.Wp() < (int64_t(1) << 30), "life_block: row too wide");
   // Row stores go through a buffer descriptor per row (num_records = pitch)
@@ -69,8 +68,6 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   p.err = tune.err;
   p.chain_spin_log2 = tune.chain_spin_log2;
   p.chain_acquire = tune.chain_acquire ? 1 : 0;
-  p.row_alt = a.dual_offset;
-  p.prio_boost = a.prio_boost ? 1 : 0;
   p.wrap_w = a.full_width && tune.wrap && g.W % 32 == 0 ? int(g.W / 32) : 0;
   p.fold = 1;
   p.fold_lanes = 64;
@@ -79,23 +76,15 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   const int64_t rows = a.row_hi - a.row_lo;
   int x = tune.xlane == kXlaneAdd || tune.xlane == kXlaneAuto ? tune.xlane : kXlaneDpp;
   if (g.layout == Layout::U8 && tune.u8_lds && (a.T == 1 || a.T == 2 || a.T == 4 || a.T == 8 || a.T == 16 || a.T == 32)) {
-    BlockArgs b = a;
-    b.dual_offset = 0;
     // Packed tiles need 32-cell aligned rows (pitch) and owned cells.
     const bool pack = a.T >= 8 && (tune.lds_pack || a.T > 8) && g.pitch % 32 == 0 && g.cell0() % 32 == 0;
     GOL_REQUIRE(a.T <= 8 || pack, "life_block: LDS-tiled byte passes deeper than 8 need the packed tile");
-    int drift = 0;
-    for (int half = 0; half < (a.dual_offset ? 2 : 1); ++half) {
-      if (a.T == 1)
-        launch_life_step_lds(b, tune.lds_rows, tune.wrap, stream);
-      else if (pack)
-        drift = launch_life_lds_bits(b, tune.wrap, tune.lds_xcd, tune.lds_waves, tune.cus, stream);
-      else
-        launch_life_lds_multi(b, tune.wrap, stream);
-      b.row_lo += a.dual_offset;
-      b.row_hi += a.dual_offset;
-    }
-    return drift;
+    if (pack) return launch_life_lds_bits(a, tune.wrap, tune.lds_xcd, tune.lds_waves, tune.cus, stream);
+    if (a.T == 1)
+      launch_life_step_lds(a, tune.lds_rows, tune.wrap, stream);
+    else
+      launch_life_lds_multi(a, tune.wrap, stream);
+    return 0;
   }
   // The adder window drifts the storage frame by T cells (see kXlaneAdd); the
   // engine allows that only for whole-width tiles of 32-cell words, and the

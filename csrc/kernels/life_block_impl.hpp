@@ -564,17 +564,12 @@ void life_block_kernel(const LifeBlockParams p) {
   const int lane = threadIdx.x & 63;
   // readfirstlane: the wave index is uniform, so everything derived from it
   // (segment bounds, loop trip counts) lives in SGPRs with scalar branches.
-  int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int64_t roff = 0;
-  if (p.row_alt && gw >= p.ncolw * p.nseg) {  // second range of a dual launch
-    gw -= p.ncolw * p.nseg;
-    roff = p.row_alt;
-  }
+  const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (gw >= p.ncolw * p.nseg) return;  // wave-uniform
   const int kcol = gw / p.nseg;
   const int seg = gw - kcol * p.nseg;
   // Balanced segments: the first `seg_rem` segments get one extra row.
-  const int64_t base = p.row_lo + roff;
+  const int64_t base = p.row_lo;
   const int64_t o0 = base + int64_t(seg) * p.seg_rows + min(seg, p.seg_rem);  // level-T output rows [o0, o1)
   const int64_t o1 = o0 + p.seg_rows + (seg < p.seg_rem ? 1 : 0);
   if (o0 >= o1) return;  // wave-uniform
@@ -593,7 +588,6 @@ void life_block_kernel(const LifeBlockParams p) {
     fmask[i] = lc.fmask[i];
   }
 
-  if (p.prio_boost) __builtin_amdgcn_s_setprio(3);  // wave-uniform
   Levels<T, W> st;
 #pragma unroll
   for (int L = 0; L < T; ++L) {

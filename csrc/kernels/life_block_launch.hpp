@@ -133,16 +133,13 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
   constexpr int kWaveOut = wave_out_words<IO::XL, IO::W>();
   // Wrap mode (p.wrap_w > 0) covers the owned words only (lane_cols).
   p.ncolw = int(ceil_div(p.wrap_w ? p.wrap_w : p.Wp, kWaveOut));
-  // A dual launch (two row ranges) has twice the waves per segment plan:
-  // the planners see 2 x ncolw strips, the kernels map the second half.
-  const int dual = p.row_alt ? 2 : 1;
   // Folded last strip (grouped kernel): 32768 cells are 16 strips of 63
   // words + 16 words; the last strip's 17 lanes fit three times in a wave,
   // so it costs a third of a strip instead of a whole one.  Lane offsets of
   // a folded wave span its groups' rows in one descriptor (< 2^30 bytes).
   p.fold = 1;
   p.fold_lanes = 64;
-  if (p.wrap_w && IO::W == 1 && dual == 1 && tune.fold && p.ncolw >= 2 &&
+  if (p.wrap_w && IO::W == 1 && tune.fold && p.ncolw >= 2 &&
       (out_rows + 2) * p.pitch < (int64_t(1) << 30)) {
     const int lanes = p.wrap_w - (p.ncolw - 1) * kWaveOut + (IO::XL == kXlaneAdd ? 1 : 2);
     const int f = std::min(4, 64 / lanes);
@@ -151,7 +148,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       p.fold_lanes = lanes;
     }
   }
-  const int simds = 4 * std::max(1, tune.cus) / dual;
+  const int simds = 4 * std::max(1, tune.cus);
   // Linked launches (GOL_LINK): this launch starts while the previous one
   // still runs, on the other stream, when both fit on the GPU at once (small
   // tiles, whose launches alone hold 2 waves per SIMD).  Any other launch
@@ -159,7 +156,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
   if (tune.link) {
     if constexpr (IO::kBits && IO::W == 1 && (T == 8 || T == 12 || T == 16) &&
                   (IO::XL == kXlaneDpp || IO::XL == kXlaneAdd)) {
-      if (tune.group != 0 && dual == 1) {
+      if (tune.group != 0) {
         // Blocks of T <= 8 link 4-wave groups where the unlinked path would
         // group 4 waves (tune group_small).
         if constexpr (T <= 8) {
@@ -204,7 +201,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
       // global memory, so no wave carries a redundant triangle but the
       // strip's last.  Stream launches only (the flags count launches, so a
       // replayed graph would see its own stale flags).
-      if (tune.chain && tune.chain_ok && tune.chain_mem && tune.chain_seq && dual == 1) {
+      if (tune.chain && tune.chain_ok && tune.chain_mem && tune.chain_seq) {
         LifeBlockParams ch = p;
         ch.fold = 1;
         ch.fold_lanes = 64;
@@ -234,7 +231,7 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
     }
   }
   plan(p, T, out_rows, simds, waves_per_simd<T, IO>(), tune.min_seg_rows, tune.target_waves, -1, nullptr, IO::XL);
-  const int waves = p.ncolw * p.nseg * dual;
+  const int waves = p.ncolw * p.nseg;
   const dim3 grid(unsigned(ceil_div(waves, 4))), block(256);
   hipLaunchKernelGGL((life_block_kernel<T, IO>), grid, block, 0, s, p);
 }

@@ -230,7 +230,7 @@ struct Prio {
   int done0 = 0;
   int next = 0;  // work at which the priority drops next
   int cur = kLevels - 1;
-  bool boost = false;  // stay at priority 3 (prio_boost launches)
+  bool boost = false;  // stay at priority 3 (hot groups of a trigger epoch)
   __device__ __forceinline__ Prio(int wtot, bool boost_)
       : quarter(max(1, wtot / max(kLevels, 1))), next(max(1, wtot / max(kLevels, 1))), boost(boost_) {
     if (boost) {
@@ -341,20 +341,14 @@ void life_group_kernel(const LifeBlockParams p) {
   const int lane = threadIdx.x & 63;
   const int m = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t t_start = p.wg_trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  if (p.prio_boost) __builtin_amdgcn_s_setprio(3);  // wave-uniform
-  int blk = blockIdx.x;
-  int64_t roff = 0;
-  if (p.row_alt && blk >= p.ncolw * p.nseg) {  // second range of a dual launch
-    blk -= p.ncolw * p.nseg;
-    roff = p.row_alt;
-  }
+  const int blk = blockIdx.x;
   // Folded last strip (wrap mode): one block runs p.fold groups of the
   // narrow last strip side by side in lane sub-strips.  Every sub-strip then
   // takes the largest group size (a smaller group starts one row early and
   // recomputes its upper neighbour's last row, identically), so the wave's
   // control flow is the same for all of them; lanes carry their group's row
   // offset in their read / store offsets.
-  const bool chain = p.chain_buf != nullptr;  // fold == 1, row_alt == 0 (launch_T)
+  const bool chain = p.chain_buf != nullptr;  // fold == 1 (launch_T)
   int kcol, grp, nsub = 1, sub_lanes = 64;
   if (p.fold > 1 && blk >= (p.ncolw - 1) * p.nseg) {
     kcol = p.ncolw - 1;
@@ -367,12 +361,12 @@ void life_group_kernel(const LifeBlockParams p) {
     if (chain) grp = p.nseg - 1 - grp;  // bottom group first: see chain_fetch
   }
   const auto group_end = [&](int g) {
-    return p.row_lo + roff + int64_t(g) * p.seg_rows + min(g, p.seg_rem) + p.seg_rows + (g < p.seg_rem ? 1 : 0);
+    return p.row_lo + int64_t(g) * p.seg_rows + min(g, p.seg_rem) + p.seg_rows + (g < p.seg_rem ? 1 : 0);
   };
   // Boundary trigger: the groups whose rows the exchange waits for run at
   // top issue priority throughout, so their count completes ahead of the
   // interior groups sharing their SIMDs (wave-uniform).
-  bool hot = p.prio_boost != 0;
+  bool hot = false;
   if (p.bnd_hot) {
     for (int j = 0; j < nsub && grp + j < p.nseg; ++j) {
       const int64_t e = group_end(grp + j);
@@ -676,7 +670,7 @@ int group_waves_per_simd() {
 template <int T, class IO, int M>
 void launch_group(const LifeBlockParams& p, hipStream_t s) {
   const int64_t blocks = p.fold > 1 ? int64_t(p.ncolw - 1) * p.nseg + ceil_div(int64_t(p.nseg), int64_t(p.fold))
-                                    : int64_t(p.ncolw) * p.nseg * (p.row_alt ? 2 : 1);
+                                    : int64_t(p.ncolw) * p.nseg;
   hipLaunchKernelGGL((life_group_kernel<T, IO, M>), dim3(unsigned(blocks)), dim3(64 * M), 0, s, p);
 }
 

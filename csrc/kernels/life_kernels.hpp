@@ -40,10 +40,6 @@ struct LifeBlockParams {
   uint32_t* err;
   // Chained-group spin bound, log2 of polls (GOL_CHAIN_SPIN, default 16).
   int chain_spin_log2;
-  // Dual launch (BlockArgs::dual_offset): blocks / waves past the first
-  // ncolw x nseg evaluate the same row range shifted by row_alt rows.
-  int64_t row_alt;
-  int prio_boost;  // BlockArgs::prio_boost
   // Wrap mode (BlockArgs::full_width): owned words per row, 0 = halo mode
   // (life_block_impl.hpp lane_cols).
   int wrap_w;

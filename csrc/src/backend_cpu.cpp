@@ -104,7 +104,7 @@ class CpuBackend final : public Backend {
   // GOL_CPU_TRIGGER=1: the engine's boundary-trigger schedule (overlap =
   // trigger) on the host.  Every operation completes in program order, so the
   // boundary rows of a trigger launch are written when run_block returns and
-  // the wait is armed at once; the engine's bookkeeping (early sends, the
+  // the wait is armed at once; the engine's bookkeeping (triggered sends, the
   // arrival before the next epoch, the auto trial) is what this tests.
   bool supports_trigger() const override { return trigger_; }
   void* trigger_stream(bool* armed) override {
@@ -244,15 +244,6 @@ class CpuBackend final : public Backend {
 
 int CpuBackend::run_block(const BlockArgs& a) {
   armed_ = a.trigger && trigger_;
-  if (a.dual_offset) {  // two row ranges: one block each, flags OR together
-    BlockArgs b = a;
-    b.dual_offset = 0;
-    const int drift = run_block(b);
-    b.row_lo += a.dual_offset;
-    b.row_hi += a.dual_offset;
-    run_block(b);
-    return drift;
-  }
   const TileGeom& g = a.g;
   const int T = a.T;
   const int64_t Wp = g.Wp();

@@ -591,14 +591,14 @@ class HipBackend final : public Backend {
       check_ptr(a.out, "run_block output");
     }
     const bool capturing = capturing_;  // capture_begin / capture_end (no query per launch)
-    // A launch may join a linked chain only on the compute stream, outside a
-    // capture, for one row range of the bit layout; anything else first joins.
-    const bool linkable = (link_on_ || (a.link && link_mode_ < 0)) && link_.stream[1] && !a.stream && !capturing &&
-                          a.dual_offset == 0 && a.g.layout == Layout::Bits;
+    // A launch may join a linked chain only outside a capture, for the bit
+    // layout; anything else first joins.
+    const bool linkable =
+        (link_on_ || (a.link && link_mode_ < 0)) && link_.stream[1] && !capturing && a.g.layout == Layout::Bits;
     if (!linkable) join_streams();
     tune_.link = linkable ? &link_ : nullptr;
     if (chain_mode_) {  // chained groups: own stream only, never inside a graph capture
-      tune_.chain_ok = (!a.stream || a.stream == stream_) && !capturing && !linkable;
+      tune_.chain_ok = !capturing && !linkable;
     }
     if (trace_at_ >= 0 && trace_pair_ && (launches_ == trace_at_ || launches_ == trace_at_ + 1))
       return run_block_traced_pair(a, linkable);
@@ -608,7 +608,7 @@ class HipBackend final : public Backend {
       return run_block_traced(a);
     }
     ++launches_;
-    hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
+    hipStream_t s = stream_;
     // Boundary trigger: armed only if the launch runs linked (the grouped
     // kernel's publish path counts the boundary groups).
     trigger_target_ = 0;
@@ -639,14 +639,14 @@ class HipBackend final : public Backend {
   // Launch-shape autotuning of the chained groups (GOL_CHAIN=-1).  Chaining
   // changes nothing but the inside of a launch (same rows, same flags), so
   // every rank may decide for itself.  Per launch shape (layout, T, rows / 256,
-  // row width, dual, drift, whole width) the first kTrials launches of each
+  // row width, drift, whole width) the first kTrials launches of each
   // option are timed with events, alternating; the completed timings are
   // collected without blocking at later launches, and the shape keeps the
   // option whose median is >= 1 % faster (else the plain grouped kernel).
   // Measured: +2 % on the 8-GPU rank tile, -1...-12 % on other tiles
   // (docs/PERFORMANCE.md), so no static rule picks it well.
   static constexpr int kTrials = 3;
-  using TuneKey = std::array<int64_t, 7>;
+  using TuneKey = std::array<int64_t, 6>;
   struct TuneStats {
     std::vector<float> ms[2];
     int issued[2] = {0, 0};
@@ -661,8 +661,8 @@ class HipBackend final : public Backend {
     collect_tuning();
     tune_.chain = 0;
     if (!tune_.chain_ok) return nullptr;
-    const TuneKey key{int64_t(a.g.layout), a.T, (a.row_hi - a.row_lo) >> 8, a.g.Wp(), a.dual_offset != 0,
-                      a.allow_drift, a.full_width};
+    const TuneKey key{int64_t(a.g.layout), a.T, (a.row_hi - a.row_lo) >> 8, a.g.Wp(), a.allow_drift,
+                      a.full_width};
     TuneStats& st = tuned_[key];
     if (st.pick >= 0) {
       tune_.chain = st.pick;
@@ -845,7 +845,7 @@ class HipBackend final : public Backend {
       pair_T_ = a.T;
     }
     ++launches_;
-    hipStream_t s = a.stream ? static_cast<hipStream_t>(a.stream) : stream_;
+    hipStream_t s = stream_;
     if (linkable) tune_.chain = 0;
     tune_.wg_trace = pair_trace_[which];
     const int drift = hipk::launch_life_block(a, tune_, s);

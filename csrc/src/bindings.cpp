@@ -309,8 +309,7 @@ PYBIND11_MODULE(_gol, m) {
       .def("overlap", &Engine::overlap)
       .def("overlap_mode", &Engine::overlap_mode)
       .def_property_readonly("trial_ms_plain", &Engine::trial_ms_plain)
-      .def_property_readonly("trial_ms_early", &Engine::trial_ms_early)
-      .def("trial_alternative", &Engine::trial_alternative)
+      .def_property_readonly("trial_ms_trigger", &Engine::trial_ms_trigger)
       .def("poll_mode", &Engine::poll_mode)
       .def_property_readonly("poll_trial_ms_joined", &Engine::poll_trial_ms_joined)
       .def_property_readonly("poll_trial_ms_side", &Engine::poll_trial_ms_side)

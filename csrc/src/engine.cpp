@@ -36,6 +36,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   GOL_REQUIRE(cfg_.sim_freq > 0, "similarity frequency must be positive");
   GOL_REQUIRE(cfg_.gen_limit >= 0, "generation limit must be >= 0");
   rank_ = tr_->rank();
+  if (cfg_.overlap == 1) cfg_.overlap = 3;  // "on" is the trigger schedule
   int64_t unit = (cfg_.layout == Layout::Bits || cfg_.W % 32 == 0) ? 32 : 1;
   if (cfg_.layout == Layout::Bits)
     GOL_REQUIRE(cfg_.W % 32 == 0, "bit-packed layout needs width % 32 == 0 (use the u8 layout)");
@@ -46,7 +47,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   if (cfg_.layout == Layout::U8 && cfg_.W % 32 == 0) {
     int mode = cfg_.u8_compute;
     if (mode < 0) mode = cfg_.tune.i("u8_via_bits");
-    if (mode < 0) mode = be_->is_device() && cfg_.overlap != 1 && cfg_.overlap != 2;
+    if (mode < 0) mode = be_->is_device();
     else mode = mode != 0;
     via_bits_ = mode == 1;
   }
@@ -170,39 +171,20 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
     size_t n = size_t(gc.span_bytes(32 * int64_t(gc.hw)) * gc.H);
     for (auto& b : colbuf_) b = be_->alloc(n);
   }
-  // The overlapped schedule needs a non-empty interior (H > 2D).  It is
-  // opt-in: its edge strips run as small, latency-bound launches (eight per
-  // epoch), which on the 32768 x 4096 per-rank tile cost 4x more than the
-  // RCCL exchange they hide (scripts/overlap_cost.sh, docs/PERFORMANCE.md).
-  const bool interior = min_tile_rows(dec_) >= 2 * int64_t(D_) + 1;  // on every rank
-  const bool early_ok = row_exchange && dec_.Px == 1 && interior && !via_bits_;
-  early_ = early_ok && cfg_.overlap == 1;
   // Boundary-triggered sends (overlap = 3; last_block_trigger): row strips
   // on a backend that can count boundary groups done.  Byte tiles on bit
   // words too: the trigger runs on the bit image.
   const bool trigger_ok = row_exchange && dec_.Px == 1 && be_->supports_trigger();
   trigger_ = trigger_ok && cfg_.overlap == 3;
-  // With the early-boundary schedule every transport operation runs on the
-  // comm stream (one stream per communicator, in issue order), so the flag
-  // all-reduce of a poll runs beside the compute stream.  Not by default: in
-  // the one-GPU RCCL rehearsal each cross-stream event hop around an exchange
-  // cost more than the all-reduce it takes off the compute stream
-  // (profiles/r02/rehearsal_overlap.jsonl).
-  comm_route_ = early_;  // the trigger schedule keeps its exchanges on the compute stream
   watchdog_s_ = cfg_.watchdog_s > 0 ? cfg_.watchdog_s : cfg_.tune.f("watchdog_s") > 0 ? cfg_.tune.f("watchdog_s") : 900.0;
   use_graphs_ = cfg_.graphs != 0 && be_->supports_graphs() && tr_->capturable() &&
                 (cfg_.graphs > 0 || tr_->size() == 1);
   if (use_graphs_) gen_dev_ = static_cast<int64_t*>(be_->alloc(sizeof(int64_t)));
-  if (use_graphs_) early_ = trigger_ = comm_route_ = false;  // captured epochs stay on one stream
-  // Overlap auto: measure both schedules on the real ranks (see auto_choose).
-  // The one-GPU RCCL rehearsal measured the early-boundary schedule slower
-  // (profiles/r02/rehearsal_overlap.jsonl), but it has no xGMI latency in it;
-  // on a multi-GPU node the decision is taken from the node itself.
-  // The alternative measured against the plain schedule: the trigger where
-  // it applies (no dual launch, no cross-stream hop before the send), else
-  // the early-boundary schedule.
-  auto_overlap_ = cfg_.overlap == -1 && (early_ok || trigger_ok) && !use_graphs_;
-  auto_alt_ = trigger_ok ? 3 : 1;
+  if (use_graphs_) trigger_ = false;  // captured epochs stay on one stream
+  // Overlap auto: measure both schedules on the real ranks (see auto_choose);
+  // the one-GPU rehearsal has no xGMI latency in it, so on a multi-GPU node
+  // the decision is taken from the node itself.
+  auto_overlap_ = cfg_.overlap == -1 && trigger_ok && !use_graphs_;
   // Side polls: with a transport whose flag reduction has its own
   // communicator (RCCL), a poll's all-reduce and D2H copy run on the comm
   // stream after a mark on the compute stream, which never waits for them:
@@ -223,7 +205,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   const int sp = cfg_.tune.i("side_poll");
   const bool side_ok = tr_->side_reduce() && (be_->is_device() || cfg_.tune.on("cpu_side_poll")) && !use_graphs_ &&
                        (tr_->size() > 1 || cfg_.self_exchange);
-  poll_side_ = side_ok && sp > 0 && !early_ && !comm_route_ && !auto_overlap_;
+  poll_side_ = side_ok && sp > 0 && !auto_overlap_;
   poll_trial_ = side_ok && sp < 0;
   gen_ = cfg_.start_gen;
 }
@@ -416,11 +398,9 @@ void Engine::halo_exchange_on(void* buf, const TileGeom& g) {
         {true, nb[kSouth], base + H * pitch, bytes},          // my bottom rows -> south's top halo
         {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
     };
-    comm_after_compute();
-    void* t = phase_begin(rccl_stream());
-    tr_->exchange(ops, rccl_stream());
-    phase_end(kHalo, t, rccl_stream());
-    compute_after_comm();
+    void* t = phase_begin(nullptr);
+    tr_->exchange(ops, be_->stream());
+    phase_end(kHalo, t, nullptr);
     halo_bytes_ += 2 * int64_t(bytes);
   }
   ++exchanges_;
@@ -488,13 +468,10 @@ void Engine::unpack_bits() {
 
 void Engine::run_epoch(int64_t d) {
   const bool sent_early = rows_pending_;
-  if (rows_pending_) {
-    // The previous epoch sent this buffer's boundary rows early.
-    if (rows_arrived_) be_->stream_wait(nullptr, rows_arrived_);
-    rows_pending_ = false;
-    rows_arrived_ = nullptr;
-  }
-  // The previous epoch ends here (its early rows have arrived).
+  // The previous epoch's last block sent this buffer's boundary rows
+  // (stream-ordered before this epoch's first block).
+  rows_pending_ = false;
+  // The previous epoch ends here.
   if (auto_overlap_) auto_mark();
   if (via_bits_) {
     epoch_via_bits(d, sent_early);
@@ -508,9 +485,7 @@ void Engine::run_epoch(int64_t d) {
   while (d > 0) {
     const int T = pick_T(d);
     if (rows_ring_) a = g_.Dv - T;  // every block covers exactly the owned rows
-    if (d == T && early_ && send_next_ && full) {
-      last_block_early(T);
-    } else if (d == T && trigger_ && send_next_ && full) {
+    if (d == T && trigger_ && send_next_ && full) {
       last_block_trigger(buf_[cur_], buf_[cur_ ^ 1], g_, T);
       cur_ ^= 1;
       gen_ += T;
@@ -526,81 +501,10 @@ void Engine::run_epoch(int64_t d) {
   }
 }
 
-void* Engine::rccl_stream() const {
-  void* c = (comm_route_ || early_) ? be_->comm_stream() : nullptr;
-  return c ? c : be_->stream();
-}
-
-void Engine::comm_after_compute() {
-  if (void* c = (comm_route_ || early_) ? be_->comm_stream() : nullptr) be_->stream_wait(c, be_->stream_mark(nullptr));
-}
-
-void Engine::compute_after_comm() {
-  if (void* c = (comm_route_ || early_) ? be_->comm_stream() : nullptr) be_->stream_wait(nullptr, be_->stream_mark(c));
-}
-
 void Engine::settle_pending(bool invalidate) {
   if (!rows_pending_) return;
-  if (rows_arrived_) be_->stream_wait(nullptr, rows_arrived_);
   be_->synchronize();
-  if (invalidate) {
-    rows_pending_ = false;
-    rows_arrived_ = nullptr;
-  }
-}
-
-// Early-boundary schedule (Py > 1, Px == 1, H > 2D).  The reference waits for
-// every halo before computing (MPI_Startall + MPI_Waitall, src/game_mpi.c:
-// 392-401).  Here the last temporal block of a full epoch writes exactly the
-// owned rows, and the next epoch's halos are the first and last D of them.
-// So that block is split: on the comm stream, one dual launch computes the two
-// D-row boundary strips, fills their periodic column halos and starts the row
-// exchange; on the compute stream the interior runs at the same time (the
-// GPU runs both kernels concurrently: the boundary launch has few waves).  The
-// next epoch's first block waits for the exchange's arrival mark.  Every row
-// is still computed once, so the per-generation flags of both launches OR
-// together exactly; the poll's flag reduction is ordered after both.
-void Engine::last_block_early(int T) {
-  trace::Range tr("gol.last_block_early");
-  const int64_t Dv = g_.Dv, H = g_.H, D = D_, pitch = g_.pitch;
-  void* in = buf_[cur_];
-  void* out = buf_[cur_ ^ 1];
-  auto* base = static_cast<uint8_t*>(out);
-  void* comm = be_->comm_stream();
-  if (comm) be_->stream_wait(comm, be_->stream_mark(nullptr));  // this block's input is complete
-  // Boundary strips [Dv, Dv + D) and [Dv + H - D, Dv + H), one launch.
-  const int drift = launch(in, out, g_, T, Dv, Dv + D, gen_, comm, H - D, /*prio_boost=*/true);
-  if (cols_filled_) {
-    void* t = phase_begin(comm);
-    be_->fill_cols_rows(out, g_, Dv, D, comm);
-    be_->fill_cols_rows(out, g_, Dv + H - D, D, comm);
-    phase_end(kFill, t, comm);
-  }
-  auto nb = dec_.neighbors(rank_);
-  const size_t bytes = size_t(Dv * pitch);
-  std::vector<P2POp> ops = {
-      {true, nb[kNorth], base + Dv * pitch, bytes},
-      {false, nb[kSouth], base + (Dv + H) * pitch, bytes},
-      {true, nb[kSouth], base + H * pitch, bytes},
-      {false, nb[kNorth], base, bytes},
-  };
-  void* tx = phase_begin(comm);
-  tr_->exchange(ops, comm ? comm : be_->stream());
-  phase_end(kHalo, tx, comm);
-  rows_arrived_ = comm ? be_->stream_mark(comm) : nullptr;
-  rows_pending_ = true;
-  halo_bytes_ += 2 * int64_t(bytes);
-  ++exchanges_;
-  ++early_sends_;
-  launch(in, out, g_, T, Dv + D, Dv + H - D, gen_);  // interior, concurrent with the above
-  if (cols_filled_) {
-    void* t = phase_begin(nullptr);
-    be_->fill_cols_rows(out, g_, Dv + D, H - 2 * D);
-    phase_end(kFill, t, nullptr);
-  }
-  add_drift(drift);
-  cur_ ^= 1;
-  gen_ += T;
+  if (invalidate) rows_pending_ = false;
 }
 
 // Trigger schedule (overlap = 3; Py > 1 or the one-rank RCCL rehearsal, Px
@@ -622,7 +526,7 @@ void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
   trace::Range tr("gol.last_block_trigger");
   const int64_t Dv = g.Dv, H = g.H, pitch = g.pitch;
   const int64_t rows[4] = {Dv, 2 * Dv, H, H + Dv};
-  add_drift(launch(in, out, g, T, Dv, Dv + H, gen_, nullptr, 0, false, rows));
+  add_drift(launch(in, out, g, T, Dv, Dv + H, gen_, rows));
   bool armed = false;
   void* s = be_->trigger_stream(&armed);  // not armed: after the whole block (a join)
   if (armed) ++triggered_sends_;
@@ -644,8 +548,7 @@ void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
   void* tx = phase_begin(s);
   tr_->exchange(ops, s ? s : be_->stream());
   phase_end(kHalo, tx, s);
-  rows_arrived_ = nullptr;  // stream-ordered before the next block on the compute stream
-  rows_pending_ = true;
+  rows_pending_ = true;  // stream-ordered before the next block on the compute stream
   halo_bytes_ += 2 * int64_t(bytes);
   ++exchanges_;
   ++early_sends_;
@@ -659,12 +562,11 @@ void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
 void Engine::hot_block(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t d) {
   const int64_t Dv = g.Dv, H = g.H, w = d - T;
   const int64_t rows[4] = {row_lo, 2 * Dv + w, H - w, row_hi};
-  add_drift(launch(in, out, g, T, row_lo, row_hi, gen_, nullptr, 0, false, rows, /*hot_only=*/true));
+  add_drift(launch(in, out, g, T, row_lo, row_hi, gen_, rows, /*hot_only=*/true));
 }
 
 int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi,
-                   int64_t gen_base, void* stream, int64_t dual_offset, bool prio_boost,
-                   const int64_t* trigger_rows, bool hot_only) {
+                   int64_t gen_base, const int64_t* trigger_rows, bool hot_only) {
   BlockArgs a;
   a.in = in;
   a.out = out;
@@ -686,24 +588,20 @@ int Engine::launch(void* in, void* out, const TileGeom& g, int T, int64_t row_lo
   a.allow_drift = drift_ok_;
   a.full_width = dec_.Px == 1 && cfg_.W % 32 == 0;
   a.wrap_rows = rows_wrapped_;
-  a.stream = stream;
   // Linked launches assume the device to themselves: not while transport
-  // work may run beside them on the comm stream (early-boundary schedule,
-  // side polls).  The trigger schedule links: its sends start only once the
-  // boundary groups are done, and the launch after them (the next epoch's
-  // first block) waits for their arrival and starts a new chain.
-  a.link = link_ && !early_ && !comm_route_ && !poll_side_;
+  // work may run beside them on the comm stream (side polls).  The trigger
+  // schedule links: its sends start only once the boundary groups are done,
+  // and the next epoch's first block follows them on the same stream.
+  a.link = link_ && !poll_side_;
   if (trigger_rows) {
     a.trigger = !hot_only;
     a.hot = hot_only;
     for (int i = 0; i < 4; ++i) a.trigger_rows[i] = trigger_rows[i];
   }
   a.ring = rows_ring_;
-  a.dual_offset = dual_offset;
-  a.prio_boost = prio_boost;
-  void* t = phase_begin(stream);
+  void* t = phase_begin(nullptr);
   const int drift = be_->run_block(a);
-  phase_end(kCompute, t, stream);
+  phase_end(kCompute, t, nullptr);
   ++launches_;
   return drift;
 }
@@ -736,8 +634,7 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
   // join, the copy and the restart left the GPU idle ~20 us per poll).
   // Phase timing keeps the compute-stream path (it times the reduction there).
   void* side = nullptr;
-  if (!comm_route_ && !early_ &&
-      (poll_side_ || (tr_->size() == 1 && !cfg_.self_exchange && !phase_timing_ && poll_copy_side_)))
+  if (poll_side_ || (tr_->size() == 1 && !cfg_.self_exchange && !phase_timing_ && poll_copy_side_))
     side = be_->poll_side();
   if (side) {
     polled_side_ = true;
@@ -751,15 +648,11 @@ Engine::Poll Engine::poll_issue(int64_t from, int64_t to) {
     return p;
   }
   be_->join_streams();  // transports enqueue on the compute stream directly
-  // Early-boundary schedule: reduce and copy on the comm stream, off the
-  // compute stream's critical path, in issue order with the halo exchanges.
-  void* comm = (comm_route_ || early_) ? be_->comm_stream() : nullptr;
-  comm_after_compute();
-  void* t = phase_begin(comm);
-  if (tr_->size() > 1) tr_->allreduce_max_u32(dev, size_t(n), rccl_stream());
-  be_->copy_d2h_async_on(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t), comm);
-  phase_end(kReduce, t, comm);
-  p.ev = be_->event_record_on(comm);
+  void* t = phase_begin(nullptr);
+  if (tr_->size() > 1) tr_->allreduce_max_u32(dev, size_t(n), be_->stream());
+  be_->copy_d2h_async_on(flags_host_ + (from + 1 - flags_base_), dev, size_t(n) * sizeof(uint32_t), nullptr);
+  phase_end(kReduce, t, nullptr);
+  p.ev = be_->event_record_on(nullptr);
   ++polls_;
   return p;
 }
@@ -975,9 +868,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
       be_->alive_any(bit_scratch(bpar_), gb_, alive_dev_);
     else
       be_->alive_any(buf_[cur_], g_, alive_dev_);
-    comm_after_compute();
-    if (tr_->size() > 1) tr_->allreduce_max_u32(alive_dev_, 1, rccl_stream());
-    compute_after_comm();
+    if (tr_->size() > 1) tr_->allreduce_max_u32(alive_dev_, 1, be_->stream());
     uint32_t alive = 0;
     be_->copy_d2h(&alive, alive_dev_, 4);
     res.extinct = !alive;
@@ -1002,14 +893,8 @@ void Engine::auto_choose(bool full_epoch) {
       trial = sched;
     }
   }
-  set_schedule(sched == 1 ? auto_alt_ : 0);
+  trigger_ = sched == 1;
   auto_sched_ = trial;
-}
-
-void Engine::set_schedule(int s) {
-  early_ = s == 1;
-  trigger_ = s == 3;
-  comm_route_ = early_;
 }
 
 void Engine::auto_mark() {
@@ -1069,11 +954,6 @@ void Engine::trial_medians(std::vector<AutoSpan>& spans, double out[2]) {
 // every generation on the critical path (src/game_mpi_collective.c:70-109).
 void Engine::poll_trial_step() {
   if (auto_overlap_) return;  // the overlap trial runs first
-  if (comm_route_) {          // polls already leave the compute stream, in order with the exchanges
-    poll_trial_ = false;
-    poll_side_ = false;
-    return;
-  }
   if (ptrial_open_) {
     void* end = be_->timing_mark(nullptr);
     if (ptrial_mode_ >= 0) {
@@ -1110,22 +990,19 @@ void Engine::auto_decide() {
   const double v[2] = {auto_ms_[0], auto_ms_[1]};
   bool alt = v[1] < 0.98 * v[0];
   const std::string& forced = cfg_.tune.s("overlap_auto");  // fault injection (tests)
-  if (forced == "early" || forced == "trigger") alt = true;
-  if (forced == "plain") alt = false;
-  GOL_REQUIRE(forced.empty() || forced == "plain" || forced == (auto_alt_ == 3 ? "trigger" : "early"),
-              "tuning overlap_auto=" + forced + ": this tile's alternative schedule is " +
-                  (auto_alt_ == 3 ? "trigger" : "early"));
-  set_schedule(alt ? auto_alt_ : 0);
+  GOL_REQUIRE(forced.empty() || forced == "plain" || forced == "trigger",
+              "tuning overlap_auto=" + forced + ": plain or trigger");
+  if (!forced.empty()) alt = forced == "trigger";
+  trigger_ = alt;
   auto_overlap_ = false;
   auto_decided_ = true;
 }
 
 std::string Engine::overlap_mode() const {
-  if (cfg_.overlap == 1) return early_ ? "on" : "off";
   if (cfg_.overlap == 3) return trigger_ ? "trigger" : "off";
   if (cfg_.overlap == -1) {
     if (auto_overlap_) return "auto:trial";
-    if (auto_decided_) return early_ ? "auto:early" : trigger_ ? "auto:trigger" : "auto:plain";
+    if (auto_decided_) return trigger_ ? "auto:trigger" : "auto:plain";
   }
   return "off";
 }

@@ -64,7 +64,7 @@ const std::vector<TuningKey>& tuning_keys() {
       {"fault_garble", "GOL_FAULT_GARBLE", "0", 'i', "fault", "thread transport corrupts the N-th message"},
       {"fault_checkpoint_crash", "GOL_FAULT_CHECKPOINT_CRASH", "0", 'i', "fault",
        "bin/gol exits after writing (not committing) the N-th checkpoint"},
-      {"overlap_auto", "GOL_OVERLAP_AUTO", "", 's', "fault", "plain | early | trigger: force the overlap trial's outcome"},
+      {"overlap_auto", "GOL_OVERLAP_AUTO", "", 's', "fault", "plain | trigger: force the overlap trial's outcome"},
       // --- CPU emulation of device features ----------------------------------
       {"cpu_ring", "GOL_CPU_RING", "0", 's', "emul", "CPU backend row rings: 0, 1, or fail (mapping fails)"},
       {"cpu_drift", "GOL_CPU_DRIFT", "0", 'i', "emul", "CPU backend's drifting frame (as the adder window)"},

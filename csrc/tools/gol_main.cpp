@@ -102,10 +102,9 @@ struct Options {
                "  --tmax T --epoch D --poll N temporal block, halo depth, poll interval\n"
                "  --overlap auto|on|off|trigger\n"
                "                              trigger = an epoch's new boundary rows are sent as soon\n"
-               "                              as the groups writing them finish; on = early boundary\n"
-               "                              strips in a launch of their own; off = no overlap;\n"
-               "                              auto = time plain against\n"
-               "                              trigger (or early) epochs on the ranks, keep the faster\n"
+               "                              as the groups writing them finish (on = trigger);\n"
+               "                              off = no overlap; auto = time plain against trigger\n"
+               "                              epochs on the ranks, keep the faster\n"
                "  --graphs auto|on|off        replay full epochs as captured HIP graphs\n"
                "  --threads N                 host threads for the cpu engine\n"
                "  --tune KEY=VALUE            runtime tuning (repeatable; --tune help lists the keys,\n"
@@ -169,7 +168,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--overlap") {
       std::string v = next();
       GOL_REQUIRE(v == "auto" || v == "on" || v == "off" || v == "trigger", "--overlap: auto, on, off or trigger");
-      o.overlap = v == "on" ? 1 : v == "off" ? 0 : v == "trigger" ? 3 : -1;
+      o.overlap = v == "on" ? 3 : v == "off" ? 0 : v == "trigger" ? 3 : -1;
     } else if (a == "--graphs") {
       std::string v = next();
       o.graphs = v == "on" ? 1 : v == "off" ? 0 : -1;
@@ -499,7 +498,7 @@ int run(const Options& o) {
         << ", \"kernel_launches\": " << res.kernel_launches << ", \"comm\": " << jstr(P > 1 ? comm : "self")
         << ", \"overlap_mode\": " << jstr(engines[0]->overlap_mode())
         << ", \"overlap_trial_ms_plain\": " << engines[0]->trial_ms_plain()
-        << ", \"overlap_trial_ms_early\": " << engines[0]->trial_ms_early()
+        << ", \"overlap_trial_ms_trigger\": " << engines[0]->trial_ms_trigger()
         << ", \"phase_timed\": " << (res.phase_timed ? "true" : "false") << ", \"compute_ms\": " << res.compute_ms
         << ", \"halo_ms\": " << res.halo_ms << ", \"fill_ms\": " << res.fill_ms
         << ", \"allreduce_ms\": " << res.allreduce_ms << "}\n";

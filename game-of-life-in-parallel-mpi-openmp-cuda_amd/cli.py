@@ -42,9 +42,9 @@ def parse_args(argv=None):
     p.add_argument("--poll", "--poll-every", dest="poll", type=int, default=0,
                    help="generations between termination polls")
     p.add_argument("--overlap", default="auto", choices=["auto", "on", "off", "trigger"],
-                   help="trigger = an epoch's boundary rows sent once the groups writing them are done; on = "
-                        "early boundary strips in a launch of their own; off = no overlap; auto = time plain "
-                        "against the alternative on the ranks and keep the faster (row strips only)")
+                   help="trigger (= on) = an epoch's boundary rows sent once the groups writing them are done; "
+                        "off = no overlap; auto = time plain against trigger epochs on the ranks and keep the "
+                        "faster (row strips only)")
     p.add_argument("--graphs", default="off", choices=["auto", "on", "off"],
                    help="replay full epochs as captured HIP graphs")
     p.add_argument("--threads", type=int, default=0)

@@ -42,7 +42,7 @@ class LifeConfig:
                                 # 16 DPP; u8 32 / 24 / 16 by tile size)
     epoch: int = 0              # generations per halo exchange (0 = 8*tmax, 16*tmax with several ranks)
     poll_gens: int = 0          # generations between termination polls (0 = 256, 512 with several ranks)
-    overlap: str = "auto"       # auto | on | off | trigger: overlap the row halo exchange with compute
+    overlap: str = "auto"       # auto | on (= trigger) | off | trigger: overlap the row halo exchange with compute
     lagged_poll: bool = True    # check termination polls one window late (no queue drain)
     graphs: str = "off"         # auto | on | off: replay full epochs as captured HIP graphs
     start_gen: int = 0          # resume: generation number of the initial state
@@ -77,7 +77,7 @@ class LifeConfig:
         c.tmax = int(self.tmax)
         c.epoch = int(self.epoch)
         c.poll_gens = int(self.poll_gens)
-        c.overlap = {"auto": -1, "off": 0, "on": 1, "trigger": 3}[self.overlap]
+        c.overlap = {"auto": -1, "off": 0, "on": 3, "trigger": 3}[self.overlap]
         c.lagged_poll = bool(self.lagged_poll)
         c.graphs = {"auto": -1, "off": 0, "on": 1}[self.graphs]
         c.start_gen = int(self.start_gen)
@@ -236,8 +236,7 @@ class Simulation:
                 "epoch": self._eng.epoch_depth, "pitch": self._eng.geom.pitch, "overlap": self._eng.overlap(),
                 "graphs": self._eng.graphs(), "overlap_mode": self._eng.overlap_mode(),
                 "overlap_trial_ms_plain": self._eng.trial_ms_plain,
-                "overlap_trial_ms_early": self._eng.trial_ms_early,
-                "overlap_alternative": self._eng.trial_alternative(),
+                "overlap_trial_ms_trigger": self._eng.trial_ms_trigger,
                 "poll_mode": self._eng.poll_mode(),
                 "poll_trial_ms_per_window": {"joined": self._eng.poll_trial_ms_joined,
                                              "side": self._eng.poll_trial_ms_side},

@@ -6,7 +6,7 @@ the CPU (gloo / thread transports).
   a launcher whose WORLD_SIZE differs from --gpus is refused.
 * Per-phase device times are present and account for the
   generation loop.
-* ``overlap=auto`` alternates the plain and early-boundary schedules, decides
+* ``overlap=auto`` alternates the plain and trigger schedules, decides
   at the same epoch on every rank, and is exact in both outcomes and across
   the switch.
 """
@@ -197,17 +197,15 @@ def test_phase_times_with_ranks(native):
     assert (grp.gather() == want).all()
 
 
-@pytest.mark.parametrize("pick,alt", [("plain", "early"), ("early", "early"), ("", "early"), ("plain", "trigger"),
-                                      ("trigger", "trigger"), ("", "trigger")])
+@pytest.mark.parametrize("pick", ["plain", "trigger", ""])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-def test_overlap_auto_trial_is_exact(native, monkeypatch, pick, alt, layout):
-    """Trial epochs alternate the plain schedule and the alternative (the
-    boundary trigger where the backend supports it - the CPU backend with
-    cpu_trigger - else early boundary), then every rank keeps the decided
-    one; forced either way (and measured) the final grid and Generations
-    equal the serial loop's."""
+def test_overlap_auto_trial_is_exact(native, monkeypatch, pick, layout):
+    """Trial epochs alternate the plain schedule and the boundary trigger
+    (the CPU backend emulates its counter with cpu_trigger), then every rank
+    keeps the decided one; forced either way (and measured) the final grid
+    and Generations equal the serial loop's."""
     monkeypatch.setenv("GOL_OVERLAP_AUTO", pick)
-    monkeypatch.setenv("GOL_CPU_TRIGGER", "1" if alt == "trigger" else "0")
+    monkeypatch.setenv("GOL_CPU_TRIGGER", "1")
     W, H, gens = 256, 3 * 200, 700
     g = random_grid(W, H, 7)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=gens, decomp="1x3", layout=layout, tmax=8, epoch=32,
@@ -220,13 +218,11 @@ def test_overlap_auto_trial_is_exact(native, monkeypatch, pick, alt, layout):
     if pick:
         assert mode == f"auto:{pick}"
     else:
-        assert mode in ("auto:plain", f"auto:{alt}")
+        assert mode in ("auto:plain", "auto:trigger")
     d = grp.sims[0].describe()
-    assert d["overlap_alternative"] == alt
-    assert d["overlap_trial_ms_plain"] > 0 and d["overlap_trial_ms_early"] > 0
-    assert all(r.overlapped for r in reps)  # the trial ran epochs of the alternative
-    if alt == "trigger":
-        assert d["triggered_sends"] > 0
+    assert d["overlap_trial_ms_plain"] > 0 and d["overlap_trial_ms_trigger"] > 0
+    assert all(r.overlapped for r in reps)  # the trial ran trigger epochs
+    assert d["triggered_sends"] > 0
     want, _, _ = reference_run(g, gens, check_similarity=False)
     assert (grp.gather() == want).all()
 
@@ -234,7 +230,8 @@ def test_overlap_auto_trial_is_exact(native, monkeypatch, pick, alt, layout):
 def test_overlap_auto_with_termination(native, monkeypatch):
     """A run that stops at a fixed point during the trial keeps the exact
     Generations line, and the next run continues the trial."""
-    monkeypatch.setenv("GOL_OVERLAP_AUTO", "early")
+    monkeypatch.setenv("GOL_OVERLAP_AUTO", "trigger")
+    monkeypatch.setenv("GOL_CPU_TRIGGER", "1")
     W, H = 32, 96
     g = random_grid(W, H, 95, 0.1)
     ref, rgens, _ = reference_run(g)
@@ -289,7 +286,7 @@ def test_native_cli_metrics_carry_phases_and_comm(gol_bin, tmp_path):
     assert rec["comm"] == "thread" and rec["ranks"] == 3
     assert rec["phase_timed"] is True and rec["compute_ms"] > 0 and rec["halo_ms"] > 0
     assert rec["compute_ms"] + rec["halo_ms"] + rec["fill_ms"] + rec["allreduce_ms"] <= 1.01 * rec["loop_ms"]
-    assert rec["overlap_mode"] in ("auto:plain", "auto:early")
+    assert rec["overlap_mode"] == "off"  # no trigger counter on the CPU backend
 
 
 def test_native_cli_rccl_needs_a_gpu_per_rank(gol_bin, tmp_path):

@@ -156,11 +156,11 @@ def test_adder_window_vs_torch(gpu, tune, group, tmax, layout):
 
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("1x8", 8)])
-@pytest.mark.parametrize("overlap", ["off", "on"])
+@pytest.mark.parametrize("overlap", ["off", "trigger"])
 def test_adder_window_row_strips_and_termination(gpu, tune, spec, P, overlap):
     """Row-strip subdomains on one GPU (the multi-GPU default decomposition)
-    with the drifting adder window: lockstep drift, overlapped edges, exact
-    Generations."""
+    with the drifting adder window: lockstep drift, the trigger schedule's
+    boundary sends, exact Generations."""
     tune["xlane"] = "3"
     for W, H, seed, density in [c for c in CONVERGING if c[0] % 32 == 0][:3] + [(256, 512, 77, 0.5)]:
         if H < 8 * P:
@@ -455,7 +455,7 @@ def test_termination_gpu(gpu, W, H, seed, density):
 
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x4", 4), ("2x2", 4), ("2x4", 8), ("3x3", 9)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
-@pytest.mark.parametrize("overlap", ["off", "on", "trigger"])
+@pytest.mark.parametrize("overlap", ["off", "trigger"])
 def test_multi_subdomain_one_gpu(gpu, tune, spec, P, layout, overlap):
     W, H = 32 * 12, 300
     g = random_grid(W, H, 42)
@@ -465,7 +465,7 @@ def test_multi_subdomain_one_gpu(gpu, tune, spec, P, layout, overlap):
     grp.load(g)
     reps = grp.run()
     assert all(r.generations == 150 for r in reps)
-    assert all(r.overlapped == (overlap in ("on", "trigger") and spec.startswith("1x")) for r in reps)
+    assert all(r.overlapped == (overlap == "trigger" and spec.startswith("1x")) for r in reps)
     assert (grp.gather() == want).all()
 
 
@@ -516,15 +516,15 @@ def test_rccl_single_rank_self_exchange(gpu, tune):
     assert flags.tolist() == [3, 0, 7]
 
 
-@pytest.mark.parametrize("overlap,side", [("off", "1"), ("off", "0"), ("on", "1"), ("trigger", "-1"), ("off", "-1")])
+@pytest.mark.parametrize("overlap,side", [("off", "1"), ("off", "0"), ("trigger", "1"), ("trigger", "-1"), ("off", "-1")])
 @pytest.mark.parametrize("xlane", [0, -1])
 def test_rccl_self_exchange_rehearsal(gpu, tune, overlap, side, xlane):
     """The multi-rank row-strip schedule on one GPU (bench.py --rehearse-rccl):
-    row halos through a 1-rank RCCL communicator sending to itself on the
-    comm stream, early-boundary dual launch concurrent with the interior,
-    termination polls reduced on the side stream through the transport's
-    flags communicator (GOL_SIDE_POLL, overlap off), against the fp32 conv
-    oracle and the exact Generations."""
+    row halos through a 1-rank RCCL communicator sending to itself, the
+    boundary-trigger sends, termination polls reduced on the side stream
+    through the transport's flags communicator (GOL_SIDE_POLL = 1, or timed
+    on the ranks with -1), against the fp32 conv oracle and the exact
+    Generations."""
     tune["xlane"] = str(xlane)
     tune["side_poll"] = side
     C = gpu
@@ -929,26 +929,27 @@ def test_linked_ring_late_seam_producers_vs_torch(gpu, tune):
     assert (sim.tile() == life_step_torch(g, 8 * 12 + 3, device="cuda")).all()
 
 
-@pytest.mark.parametrize("overlap", ["off", "on"])
-def test_rank_tile_links_only_without_comm_stream_work(gpu, tune, overlap):
+@pytest.mark.parametrize("side", ["0", "1"])
+def test_rank_tile_links_only_without_comm_stream_work(gpu, tune, side):
     """Linked launches assume the device to themselves (the "two launches
     fit" cap counts only the pair): the engine links blocks of
     the multi-rank schedule only while no transport work can run beside them
     on the comm stream.  The 8-GPU rank tile's schedule, rehearsed with a
-    1-rank RCCL communicator: linked with the plain schedule, never with the
-    early-boundary one - and exact either way."""
+    1-rank RCCL communicator: linked with polls on the compute stream, never
+    with side polls (tuning side_poll = 1) - and exact either way."""
     native = gpu
+    tune["side_poll"] = side
     W, H = 32768, 4096
     tr = native.rccl_transport(native.rccl_unique_id(), 0, 1, 0, tune=make_tuning(tune))
-    sim = Simulation(LifeConfig(W, H, gen_limit=100_000, overlap=overlap, self_exchange=True, epoch=256, tune=tune),
+    sim = Simulation(LifeConfig(W, H, gen_limit=600, overlap="off", self_exchange=True, epoch=256, tune=tune),
                      engine="hip", transport=tr)
     g = random_grid(W, H, 77)
     sim.load(g)
-    rep = sim.advance(600)
-    if overlap == "off":
+    rep = sim.run()  # with termination polls
+    if side == "0":
         assert rep.linked_launches > 0
     else:
-        assert rep.linked_launches == 0 and rep.overlapped
+        assert rep.linked_launches == 0
     assert (sim.tile() == life_step_torch(g, 600, device="cuda")).all()
 
 

@@ -60,80 +60,73 @@ def test_random_init_decomposition_independent(native, tune):
 @pytest.mark.parametrize("spec,P", [("1x2", 2), ("1x3", 3), ("2x2", 4), ("2x3", 6)])
 @pytest.mark.parametrize("layout", ["bits", "u8"])
 @pytest.mark.parametrize("tmax,epoch", [(4, 8), (8, 8), (4, 12), (2, 5)])
-@pytest.mark.parametrize("mode", ["on", "trigger"])
-def test_overlapped_exchange_matches_serial(native, tune, spec, P, layout, tmax, epoch, mode):
-    """Overlapped epochs are bit-identical to the serial reference, including
-    a short final epoch (gens not a multiple of the epoch depth):
-      on       early boundary rows: the last block of an epoch computes the 2D
-               boundary rows, sends them, then computes the interior (row
-               strips only, Px == 1);
-      trigger  the last block's boundary rows are sent once the groups
-               writing them are done (row strips; the CPU backend emulates
-               the counter, tuning cpu_trigger)."""
-    if mode == "trigger":
-        tune["cpu_trigger"] = "1"
+def test_overlapped_exchange_matches_serial(native, tune, spec, P, layout, tmax, epoch):
+    """Overlapped (trigger) epochs are bit-identical to the serial reference,
+    including a short final epoch (gens not a multiple of the epoch depth):
+    the last block's boundary rows are sent once the groups writing them are
+    done (row strips, Px == 1; the CPU backend emulates the counter, tuning
+    cpu_trigger)."""
+    tune["cpu_trigger"] = "1"
     W, H = 192, 150
     g = random_grid(W, H, 77 + tmax)
     gens = 3 * epoch + epoch // 2 + 1
     ref, _, _ = reference_run(g, gens)
-    cfg = LifeConfig(W, H, gen_limit=gens, decomp=spec, layout=layout, tmax=tmax, epoch=epoch, overlap=mode, tune=tune)
+    cfg = LifeConfig(W, H, gen_limit=gens, decomp=spec, layout=layout, tmax=tmax, epoch=epoch, overlap="trigger", tune=tune)
     grp = InProcessGroup(cfg, P, engine="cpu")
     grp.load(g)
     reps = grp.run()
     want = spec.startswith("1x")
     assert all(r.overlapped == want for r in reps)
-    if mode == "trigger":
-        assert all(s.native_engine.triggered_sends() == (3 if want else 0) for s in grp.sims)
+    assert all(s.native_engine.triggered_sends() == (3 if want else 0) for s in grp.sims)
     assert (grp.gather() == ref).all()
 
 
 @pytest.mark.parametrize("W,H,seed,density", CONVERGING)
 @pytest.mark.parametrize("lagged", [True, False])
-@pytest.mark.parametrize("mode", ["on", "trigger"])
-def test_overlapped_termination(native, tune, W, H, seed, density, lagged, mode):
+def test_overlapped_termination(native, tune, W, H, seed, density, lagged):
     tune["cpu_trigger"] = "1"
     g = random_grid(W, H, seed, density)
     ref, rgens, _ = reference_run(g)
-    cfg = LifeConfig(W, H, decomp="1x2", layout="u8", tmax=2, epoch=3, poll_gens=4, overlap=mode,
+    cfg = LifeConfig(W, H, decomp="1x2", layout="u8", tmax=2, epoch=3, poll_gens=4, overlap="trigger",
                      lagged_poll=lagged, tune=tune)
     grp = InProcessGroup(cfg, 2, engine="cpu")
     grp.load(g)
     reps = grp.run()
     assert {r.generations for r in reps} == {rgens}
     # The trigger needs no interior (H > 2D): only a second epoch in the run.
-    assert all(r.overlapped == ((H // 2 >= 7 or mode == "trigger") and r.executed > 3) for r in reps)
+    assert all(r.overlapped == (r.executed > 3) for r in reps)
     assert (grp.gather() == ref).all()
 
 
 def test_overlap_modes(native, tune):
-    """on = early boundary rows on row strips with H > 2D; trigger = the
-    boundary rows sent once the groups writing them are done; auto decides
-    on the ranks; column decompositions do not overlap."""
+    """trigger (= on) = the boundary rows sent once the groups writing them
+    are done, on row strips of a backend that counts boundary groups done;
+    auto decides on the ranks; column decompositions do not overlap."""
     def ov(**kw):
         cfg = dict(decomp="1x2", tmax=4, epoch=16)
         cfg.update(kw)
         H = cfg.pop("H", 512)
-        return InProcessGroup(LifeConfig(64, H, **cfg, tune=tune), 2, engine="cpu").sims[0].native_engine.overlap()
-    assert ov(overlap="on")
-    assert not ov() and not ov(overlap="off")
-    assert not ov(H=40, overlap="on")  # tile rows 20 <= 2D
-    assert not ov(decomp="2x1", overlap="on")
-    # trigger: row strips on a backend that counts boundary groups done
-    assert not ov(overlap="trigger")
+        eng = InProcessGroup(LifeConfig(64, H, **cfg, tune=tune), 2, engine="cpu").sims[0].native_engine
+        return eng.overlap(), eng.overlap_mode()
+    assert ov(overlap="trigger") == (False, "off")  # no counter on this backend
+    assert ov() == (False, "off")
     tune["cpu_trigger"] = "1"
-    assert ov(overlap="trigger") and ov(H=40, overlap="trigger")
-    assert not ov(decomp="2x1", overlap="trigger")
+    assert ov(overlap="trigger") == (True, "trigger") and ov(H=40, overlap="trigger")[0]
+    assert ov(overlap="on") == (True, "trigger")
+    assert ov() == (False, "auto:trial") and ov(overlap="off") == (False, "off")
+    assert not ov(decomp="2x1", overlap="trigger")[0]
 
 
 @pytest.mark.parametrize("lagged", [True, False])
-def test_early_boundary_across_runs_and_readouts(native, tune, lagged):
+def test_trigger_across_runs_and_readouts(native, tune, lagged):
     """Chunked runs (run_until) and read-outs between them: an exchange sent at
     the end of one run is consumed by the next, and a read-out in between
     (tile(), which may rotate a drift out) never sees stale halos."""
+    tune["cpu_trigger"] = "1"
     W, H = 128, 160
     g = random_grid(W, H, 5)
     grp = InProcessGroup(LifeConfig(W, H, gen_limit=10_000, decomp="1x2", tmax=4, epoch=8, poll_gens=8,
-                                    lagged_poll=lagged, tune=tune), 2, engine="cpu")
+                                    overlap="trigger", lagged_poll=lagged, tune=tune), 2, engine="cpu")
     grp.load(g)
     want = g
     done = 0
@@ -144,16 +137,17 @@ def test_early_boundary_across_runs_and_readouts(native, tune, lagged):
         assert (grp.gather() == want).all(), done
 
 
-@pytest.mark.parametrize("overlap", ["off", "on"])
-def test_random_transport_delays_do_not_change_results(native, tune, overlap):
+@pytest.mark.parametrize("overlap,decomp", [("off", "2x3"), ("trigger", "1x3")])
+def test_random_transport_delays_do_not_change_results(native, tune, overlap, decomp):
     """Fault injection: random delays before every publish and
     consume shake the message interleaving; results must stay exact."""
     tune["fault_delay_us"] = "300"
+    tune["cpu_trigger"] = "1"
     W, H = 128, 120
     g = random_grid(W, H, 8)
     ref, _, _ = reference_run(g, 40)
-    grp = InProcessGroup(LifeConfig(W, H, gen_limit=40, decomp="2x3", layout="u8", tmax=2, epoch=6,
-                                    overlap=overlap, tune=tune), 6, engine="cpu")
+    grp = InProcessGroup(LifeConfig(W, H, gen_limit=40, decomp=decomp, layout="u8", tmax=2, epoch=6,
+                                    overlap=overlap, tune=tune), 6 if decomp == "2x3" else 3, engine="cpu")
     grp.load(g)
     grp.run()
     assert (grp.gather() == ref).all()
@@ -209,12 +203,13 @@ def test_thread_transport_pair_matching_two_ranks(native, tune):
         assert (halo_n[r] == bot[1 - r]).all()  # north neighbour's bottom rows -> my top halo
 
 
-@pytest.mark.parametrize("mode", ["auto", "on"])
+@pytest.mark.parametrize("mode", ["auto", "trigger"])
 def test_overlap_decision_is_global_on_uneven_tiles(native, tune, mode):
-    """37 rows over 3 ranks = tiles of 12, 12, 13 rows; with D = 6 only the
-    13-row tile has H > 2D.  Every rank must take the same schedule (a rank
-    that exchanges early while the others reduce flags would deadlock), so
-    the decision uses the smallest tile."""
+    """37 rows over 3 ranks = tiles of 12, 12, 13 rows.  Every rank must take
+    the same schedule (a rank that sends from its last block while the others
+    reduce flags would deadlock), so the decision depends on the
+    decomposition, not on this rank's tile."""
+    tune["cpu_trigger"] = "1"
     W, H = 96, 37
     g = random_grid(W, H, 3)
     ref, rgens, _ = reference_run(g, 50)
