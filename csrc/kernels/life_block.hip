@@ -24,10 +24,7 @@ std::string life_block_variant(Layout layout, const LifeTuning& tune) {
   const bool grouped = tune.group != 0;
   return std::string(layout == Layout::Bits ? "bits" : "u8") + " wpl=1 " + xlane_name(tune.xlane) +
          (grouped ? (tune.group < 0 ? std::string(" group=auto") : " group=" + std::to_string(tune.group)) : "") +
-         (grouped && tune.chain == 1    ? " chain"
-          : grouped && tune.chain == 2 ? " chain=probe"
-          : grouped && tune.chain < 0  ? " chain=tuned"
-                                       : "");
+         (grouped && tune.chain == 1 ? " chain" : grouped && tune.chain < 0 ? " chain=tuned" : "");
 }
 
 int life_block_max_T(Layout layout, const LifeTuning& tune) {
@@ -67,7 +64,6 @@ int launch_life_block(const BlockArgs& a, const LifeTuning& tune, hipStream_t st
   p.wg_trace = tune.wg_trace;
   p.err = tune.err;
   p.chain_spin_log2 = tune.chain_spin_log2;
-  p.chain_acquire = tune.chain_acquire ? 1 : 0;
   p.wrap_w = a.full_width && tune.wrap && g.W % 32 == 0 ? int(g.W / 32) : 0;
   p.fold = 1;
   p.fold_lanes = 64;

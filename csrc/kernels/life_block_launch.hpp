@@ -104,19 +104,19 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
     // Only the chain's second launch waits for the first one's start (an
     // event): the first follows whatever the stream held before it (fills,
     // an exchange), which may take long, and a linked group's wait is
-    // bounded.  Later launches need no event: each becomes eligible when the
-    // launch two back on its own stream ends, after the previous launch did,
-    // so it never waits long; its groups touch no memory before their
-    // completion-word waits, and two launches fit on the GPU together (cap).
+    // bounded.  Every later launch waits on one too: without them the early
+    // consumers' spinning waves took the producer's slots (8192^2 1.81-1.85
+    // vs 1.61 ms per 1000 generations, profiles/r04/linked_events_ab.jsonl),
+    // although an event wait between two streams costs ~10 us of device time.
     // Its stream also orders it after the launch two back, whose completion
     // words (flags[seq % 3]) it overwrites.
-    if (L.events || L.chain == 1) (void)hipStreamWaitEvent(st, L.before[L.cur], 0);
+    (void)hipStreamWaitEvent(st, L.before[L.cur], 0);
     ++L.linked;
   } else {
     link_join(L);
     L.chain = 0;
   }
-  if (L.events || L.chain == 0) (void)hipEventRecord(L.before[which], st);
+  (void)hipEventRecord(L.before[which], st);
   ++L.chain;
   hipLaunchKernelGGL((life_group_kernel<T, LIO, M>), dim3(unsigned(blocks)), dim3(64 * M), 0, st, q);
   L.cur = which;
@@ -219,10 +219,8 @@ void launch_T(LifeBlockParams p, int64_t out_rows, const LifeTuning& tune, hipSt
           const int64_t slots = int64_t(ch.ncolw) * ch.nseg;
           ch.chain_flag = tune.chain_mem(0, size_t(slots) * 4);
           ch.chain_buf = tune.chain_mem(1, size_t(slots * kSlot) * 4);
-          // 0 = never written, ~0 = the probe's marker
-          if (++*tune.chain_seq == 0 || *tune.chain_seq == 0xFFFFFFFFu) *tune.chain_seq = 1;
+          if (++*tune.chain_seq == 0) *tune.chain_seq = 1;  // 0 = never written
           ch.chain_seq = *tune.chain_seq;
-          if (tune.chain == 2) ch.chain_seq = 0xFFFFFFFFu;  // timing probe: no wait, no fetch (wrong rows)
           return m4 ? launch_group<T, IO, 4>(ch, s) : launch_group<T, IO, 8>(ch, s);
         }
       }

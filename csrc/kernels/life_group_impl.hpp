@@ -97,13 +97,11 @@ struct ChainSaver {
 // flag with an agent-scope atomic; the consumer wave polls that one word
 // relaxed at agent scope and, after the match, performs an agent-scope
 // acquire (L1 invalidate + wait) before reading the payload with sc1 buffer
-// loads to registers.  That is the formal release/acquire pair; the sc1
-// loads alone (no acquire, LifeTuning::chain_acquire = false,
-// GOL_CHAIN_ACQUIRE=0) match the guide's "valid forms" table row for one
-// signalling lane per storing workgroup, which was measured only at one
-// workgroup per CU, so the acquire stays on by default (its cost on the
-// 8-GPU rank tile: docs/PERFORMANCE.md).  (An LDS-DMA copy, global_load_lds,
-// would not qualify either way: it is not a load to registers.)
+// loads to registers.  That is the formal release/acquire pair (the sc1
+// loads alone match the guide's "valid forms" table row for one signalling
+// lane per storing workgroup, which was measured only at one workgroup per
+// CU, so the acquire stays).  (An LDS-DMA copy, global_load_lds, would not
+// qualify either way: it is not a load to registers.)
 template <int T, int W>
 __device__ __forceinline__ void chain_fetch(const LifeBlockParams& p, int64_t slot_below, int64_t flag_below,
                                             uint32_t* lds_slot, int lane) {
@@ -125,15 +123,11 @@ __device__ __forceinline__ void chain_fetch(const LifeBlockParams& p, int64_t sl
     __hip_atomic_store(p.err + 3, uint32_t(flag_below), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(p.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (p.chain_acquire) {  // wave-uniform
-    // The formal pair of the producer's write-through stores: an agent-scope
-    // acquire drops this CU's L1 lines, and the wait holds the loads below
-    // until the invalidate has completed (MI355X_MICROARCH.md, visibility).
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
+  // The formal pair of the producer's write-through stores: an agent-scope
+  // acquire drops this CU's L1 lines, and the wait holds the loads below
+  // until the invalidate has completed (MI355X_MICROARCH.md, visibility).
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const BufRsrc src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p.chain_buf + slot_below), short(0),
                                                         kRows * 64 * 4, kBufFlags);
   // Eight rows in flight per batch (8 VGPRs), sc1 loads to registers, then LDS.
@@ -468,7 +462,7 @@ void life_group_kernel(const LifeBlockParams p) {
   }
 
   prio.done0 = (kmain - kPro) * T;
-  if (chain_down && p.chain_seq != 0xFFFFFFFFu) chain_fetch<T, W>(p, (chain_at + 1) * kSlot, chain_at + 1, saved, lane);
+  if (chain_down) chain_fetch<T, W>(p, (chain_at + 1) * kSlot, chain_at + 1, saved, lane);
   epilogue_tri<T, IO, 0, S0>(st, rd, saved + (chain_down ? 0 : m + 1) * kSlot, lane, wr, k, nfull,
                              prio);  // k == kmain
   prio.reset();

@@ -58,9 +58,6 @@ struct LifeBlockParams {
   uint32_t* chain_flag;
   uint32_t chain_seq;
   int64_t chain_end;
-  // 1: the consumer adds an agent-scope acquire (L1 invalidate) after its
-  // poll matched, on top of the sc1 loads (LifeTuning::chain_acquire).
-  int chain_acquire;
   // Linked launches (LifeTuning::link, life_group_kernel<..., LINK = true>):
   // this launch may run while the previous grouped launch, whose output is
   // its input, still runs.  Group (kcol, grp) first waits until every group
@@ -125,15 +122,6 @@ struct LinkState {
   size_t flag_words = 0;
   uint32_t seq = 0;
   int64_t linked = 0;                           // launches that ran linked (diagnostics)
-  // Order every linked launch after the previous one's start with a cross-
-  // stream event (GOL_LINK_EVENTS, default 1).  With 0 only a chain's second
-  // launch does; the completion words still order the data (launch_linked).
-  // An event wait between two streams costs ~10 us of device time on MI355X
-  // (csrc/tools/ubench_launch.hip), yet without them 8192^2 runs slower
-  // (1.81-1.85 vs 1.61 ms per 1000 generations; the early consumers' spinning
-  // waves take the producer's slots), the rank tile the same
-  // (profiles/r04/linked_events_ab.jsonl).
-  bool events = true;
   int chain = 0;  // launches in the current chain
   // Boundary trigger of the next launch (BlockArgs::trigger): requested
   // rows, the counter, and how many increments the launch will make
@@ -190,7 +178,6 @@ struct LifeTuning {
   uint64_t* wg_trace = nullptr;  // per-wave placement/timing record of the next launch (LifeBlockParams)
   uint32_t* err = nullptr;       // LifeBlockParams::err (4 words: code, then a give-up's diagnostics)
   int chain_spin_log2 = 16;      // LifeBlockParams::chain_spin_log2
-  bool chain_acquire = true;     // LifeBlockParams::chain_acquire (GOL_CHAIN_ACQUIRE)
   int fault_delay = 0;  // LifeBlockParams::fault_delay (GOL_FAULT_DELAY_SPINS)
 };
 

@@ -80,6 +80,7 @@ class HipBackend final : public Backend {
     tune_.wrap = t.on("wrap");
     tune_.fold = t.on("fold");
     chain_mode_ = t.i("chain");
+    GOL_REQUIRE(chain_mode_ >= -1 && chain_mode_ <= 1, "tuning chain: -1, 0 or 1");
     // Linked launches: consecutive grouped launches of an epoch overlap on
     // two streams, ordered by per-group completion words (LifeBlockParams::
     // link_*): small tiles whose launches alone hold only 2 waves per SIMD.
@@ -91,7 +92,6 @@ class HipBackend final : public Backend {
       link_.stream[0] = stream_;
       link_.stream[1] = make_stream(dev_, tuning_.s("cu_partition"));
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      link_.events = t.on("link_events");
       tune_.link_force = t.on("link_force");
     }
     // A GPU shared by several processes (a CU partition) time-slices their
@@ -139,7 +139,6 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 4 * sizeof(uint32_t), hipHostMallocMapped));
     for (int i = 0; i < 4; ++i) err_host_[i] = 0;
     tune_.chain_spin_log2 = std::min(24, std::max(4, t.i("chain_spin")));
-    tune_.chain_acquire = t.on("chain_acquire");
     HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&tune_.err), err_host_, 0));
   }
   ~HipBackend() override {
@@ -1060,7 +1059,7 @@ class HipBackend final : public Backend {
   unsigned long long* trigger_mem_ = nullptr;
   uint64_t trigger_total_ = 0, trigger_target_ = 0;
   bool trigger_ok_ = false;
-  int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, 2 timing probe, -1 autotuned per launch shape
+  int chain_mode_ = 0;  // GOL_CHAIN: 0 off, 1 on, -1 autotuned per launch shape
   bool tune_log_ = false;
   std::map<TuneKey, TuneStats> tuned_;
   std::deque<Pending> pending_;  // timed trial launches not collected yet

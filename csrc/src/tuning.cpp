@@ -22,12 +22,10 @@ const std::vector<TuningKey>& tuning_keys() {
       {"min_seg_rows", "GOL_MIN_SEG_ROWS", "16", 'i', "tune",
        "shortest row segment a wave of the classic schedule is given"},
       {"chain", "GOL_CHAIN", "-1", 'i', "tune",
-       "chained groups: -1 timed per launch shape, 0 off, 1 on, 2 timing probe (no waits: wrong cells)"},
+       "chained groups: -1 timed per launch shape, 0 off, 1 on"},
       {"chain_spin", "GOL_CHAIN_SPIN", "16", 'i', "tune", "log2 of a chained wave's spin budget"},
-      {"chain_acquire", "GOL_CHAIN_ACQUIRE", "1", 'i', "tune", "chained waits end with an acquire (L1 invalidate)"},
       {"link", "GOL_LINK", "-1", 'i', "tune",
        "linked launches: -1 where the engine asks (small ring tiles, rank tiles), 0 never, 1 every eligible launch"},
-      {"link_events", "GOL_LINK_EVENTS", "1", 'i', "tune", "order linked launches' stream joins with events"},
       {"wrap", "GOL_WRAP", "1", 'i', "tune", "full-width tiles wrap column reads (no halo columns)"},
       {"fold", "GOL_FOLD", "1", 'i', "tune", "fold a narrow last column strip into the others' waves"},
       {"row_ring", "GOL_ROW_RING", "1", 'i', "tune", "single-rank tiles on a row ring (aliased halo rows)"},
