@@ -32,12 +32,8 @@ class Backend {
   virtual void memset_async(void* p, int v, size_t bytes) = 0;
   virtual void copy_h2d(void* dst, const void* src, size_t bytes) = 0;        // synchronous
   virtual void copy_d2h(void* dst, const void* src, size_t bytes) = 0;        // synchronous
-  virtual void copy_d2h_async(void* dst, const void* src, size_t bytes) = 0;  // into pinned
-  // Same, on `stream` (nullptr = the compute stream).
-  virtual void copy_d2h_async_on(void* dst, const void* src, size_t bytes, void* stream) {
-    (void)stream;
-    copy_d2h_async(dst, src, bytes);
-  }
+  // Into pinned memory, on `stream` (nullptr = the compute stream).
+  virtual void copy_d2h_async_on(void* dst, const void* src, size_t bytes, void* stream) = 0;
   virtual void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch,
                              int64_t width_bytes, int64_t rows) = 0;
   virtual void synchronize() = 0;
@@ -46,18 +42,16 @@ class Backend {
     (void)stream;
     synchronize();
   }
-  // Events: returns an opaque handle recorded on the stream.
-  virtual void* event_record() = 0;
-  // Same, recorded on `stream` (nullptr = the compute stream).
-  virtual void* event_record_on(void* stream) { return stream ? nullptr : event_record(); }
+  // Events: an opaque handle recorded on `stream` (nullptr = the compute
+  // stream).
+  virtual void* event_record_on(void* stream) = 0;
   virtual void event_wait(void* ev) = 0;  // host blocks until the event completes
   virtual void event_destroy(void* ev) = 0;
   // Non-blocking: has the event completed?  (Synchronous backends: always.)
   virtual bool event_query(void* /*ev*/) { return true; }
   // Second queue for communication that overlaps compute (HIP: a separate
-  // non-blocking stream; synchronous backends return nullptr and run
-  // everything in program order).  stream_mark() records a point on `from`
-  // (nullptr = the compute stream) that stream_wait() makes `on` wait for.
+  // non-blocking stream, poll_side's; synchronous backends return nullptr and
+  // run everything in program order).
   virtual void* comm_stream() { return nullptr; }
   // Stream capture into replayable graphs (HIP graphs).  capture_end()
   // returns an executable graph handle; graph_launch() enqueues it.
@@ -73,8 +67,6 @@ class Backend {
     else
       *dev = v;
   }
-  virtual void* stream_mark(void* /*from*/) { return nullptr; }
-  virtual void stream_wait(void* /*on*/, void* /*mark*/) {}
   // Boundary trigger (BlockArgs::trigger).  trigger_stream() returns the
   // compute stream, ordered so that work enqueued on it next starts once the
   // groups of the last run_block that met the trigger rows have written them

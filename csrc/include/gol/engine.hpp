@@ -94,7 +94,7 @@ struct EngineConfig {
   //      else bytes.
   int u8_compute = -1;
   // Runtime tuning (gol/tuning.hpp): the engine's own knobs (u8_via_bits,
-  // side_poll, cpu_side_poll, poll_copy_side, watchdog_s, pitch_pad, overlap_auto) come from here; the
+  // side_poll, cpu_side_poll, poll_copy_side, watchdog_s, overlap_auto) come from here; the
   // backend's from the Tuning it was constructed with.  Default: the table's
   // defaults under the GOL_* environment overrides.
   Tuning tune = Tuning::from_env();
@@ -239,6 +239,7 @@ class Engine {
   void hot_block(void* in, void* out, const TileGeom& g, int T, int64_t row_lo, int64_t row_hi, int64_t d);
   void add_drift(int64_t cells);
   void exchange_columns(void* buf, const TileGeom& g);
+  std::vector<P2POp> row_ops(void* buf, const TileGeom& g) const;
   void halo_exchange_on(void* buf, const TileGeom& g);
   // Byte layout on bit words (EngineConfig::u8_compute = 1): one epoch on
   // the bit tile, and the per-run pack / unpack of the byte tile.

@@ -13,10 +13,9 @@
 // construction: a knob never changes under a live object.
 //
 // Classes:
-//   tune          performance knobs of the default build;
-//   probe         timing probes of the default kernels (exact but measured
-//                 slower, or wrong cells by design); the measured-slower
-//                 variants themselves were removed in round 6 (HISTORY.md);
+//   tune          performance knobs of the default build (the measured-
+//                 slower variants and their probes were removed in round 6,
+//                 HISTORY.md);
 //   diag          traces, logs and consistency checks;
 //   fault         fault injection (tests);
 //   emul          the CPU backend emulating a device feature (tests).
@@ -38,7 +37,7 @@ struct TuningKey {
   const char* env;
   const char* dflt;
   char type;        // 'i' integer, 'f' number, 's' string
-  const char* cls;  // tune | probe | diag | fault | emul
+  const char* cls;  // tune | diag | fault | emul
   const char* doc;
 };
 const std::vector<TuningKey>& tuning_keys();

@@ -43,7 +43,7 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   const int64_t cap = int64_t(std::max(1, tune.cus)) * per_cu;
   // Two such launches never fit beside each other: the plain kernel (no
   // write-through stores, no completion words) serves the whole chain.
-  if (2 * blocks > cap && !tune.link_force) {
+  if (2 * blocks > cap) {
     link_join(L);
     L.prev_valid = false;
     return false;

@@ -153,7 +153,6 @@ inline void link_join(LinkState& L) {
 
 struct LifeTuning {
   int cus = 256;            // compute units of the device
-  bool link_force = false;  // GOL_LINK_FORCE=1 (probe): the linked kernel even where two launches do not fit
   int target_waves = 0;     // waves per launch round (0 = occupancy x CUs x 4 SIMDs)
   int min_seg_rows = 16;    // lower bound on rows per wave segment
   int xlane = kXlaneAuto;   // cross-lane primitive

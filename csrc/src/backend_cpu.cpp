@@ -185,7 +185,7 @@ class CpuBackend final : public Backend {
   void memset_async(void* p, int v, size_t bytes) override { std::memset(p, v, bytes); }
   void copy_h2d(void* d, const void* s, size_t n) override { std::memcpy(d, s, n); }
   void copy_d2h(void* d, const void* s, size_t n) override { std::memcpy(d, s, n); }
-  void copy_d2h_async(void* d, const void* s, size_t n) override { std::memcpy(d, s, n); }
+  void copy_d2h_async_on(void* d, const void* s, size_t n, void*) override { std::memcpy(d, s, n); }
   void copy_2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
                      int64_t rows) override {
     auto* d = static_cast<uint8_t*>(dst);
@@ -193,7 +193,7 @@ class CpuBackend final : public Backend {
     for (int64_t r = 0; r < rows; ++r) std::memmove(d + r * dpitch, s + r * spitch, size_t(width));
   }
   void synchronize() override {}
-  void* event_record() override { return nullptr; }
+  void* event_record_on(void*) override { return nullptr; }
   void event_wait(void*) override {}
   void event_destroy(void*) override {}
   // Every operation completes before it returns: a mark is the host clock.

@@ -92,7 +92,6 @@ class HipBackend final : public Backend {
       link_.stream[0] = stream_;
       link_.stream[1] = make_stream(dev_, tuning_.s("cu_partition"));
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      tune_.link_force = t.on("link_force");
     }
     // A GPU shared by several processes (a CU partition) time-slices their
     // queues, so a producer workgroup can be switched out for longer than a
@@ -164,8 +163,6 @@ class HipBackend final : public Backend {
     for (hipEvent_t e : free_events_) hipEventDestroy(e);
     for (hipEvent_t e : timing_pool_) hipEventDestroy(e);
     if (err_host_) hipHostFree(err_host_);
-    for (auto& e : marks_)
-      if (e) hipEventDestroy(e);
     for (auto& e : tail_)
       if (e) hipEventDestroy(e);
     if (comm_) hipStreamDestroy(comm_);
@@ -376,13 +373,8 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
-  void copy_d2h_async(void* d, const void* s, size_t n) override {
-    join_streams();
-    GOL_ON_DEVICE();
-    HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream_));
-  }
   void copy_d2h_async_on(void* d, const void* s, size_t n, void* stream) override {
-    if (!stream) join_streams();  // a side stream was ordered by its caller (stream_wait / poll_side)
+    if (!stream) join_streams();  // a side stream was ordered by its caller (poll_side)
     GOL_ON_DEVICE();
     HIP_CHECK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream ? static_cast<hipStream_t>(stream) : stream_));
   }
@@ -403,7 +395,6 @@ class HipBackend final : public Backend {
     GOL_ON_DEVICE();
     HIP_CHECK(hipStreamSynchronize(s ? static_cast<hipStream_t>(s) : stream_));
   }
-  void* event_record() override { return event_record_on(nullptr); }
   void* event_record_on(void* stream) override {
     if (!stream) join_streams();
     GOL_ON_DEVICE();
@@ -555,21 +546,6 @@ class HipBackend final : public Backend {
     return stream_;
   }
   bool supports_trigger() const override { return trigger_ok_; }
-  // Marks come from a small ring of reusable timing-free events: a mark is
-  // only waited on by the next few operations of an epoch.
-  void* stream_mark(void* from) override {
-    join_streams();
-    GOL_ON_DEVICE();
-    hipEvent_t& e = marks_[mark_next_++ % marks_.size()];
-    if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIP_CHECK(hipEventRecord(e, from ? static_cast<hipStream_t>(from) : stream_));
-    return e;
-  }
-  void stream_wait(void* on, void* mark) override {
-    join_streams();
-    GOL_ON_DEVICE();
-    HIP_CHECK(hipStreamWaitEvent(on ? static_cast<hipStream_t>(on) : stream_, static_cast<hipEvent_t>(mark), 0));
-  }
 
   // GOL_HOST_PROFILE=1: host time per block, printed when the backend goes:
   // the engine between blocks, run_block itself, and its launch call.
@@ -1074,10 +1050,8 @@ class HipBackend final : public Backend {
   bool trace_pair_ = false;
   uint64_t* pair_trace_[2] = {nullptr, nullptr};
   int pair_T_ = 0;
-  std::array<hipEvent_t, 16> marks_{};
   hipEvent_t tail_[2] = {nullptr, nullptr};  // poll_side(): the compute streams' tails
   bool capturing_ = false;                    // between capture_begin and capture_end
-  size_t mark_next_ = 0;
   void* stage_ = nullptr;
   int64_t stage_bytes_ = 0;
   uint32_t* err_host_ = nullptr;

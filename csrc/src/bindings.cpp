@@ -268,29 +268,7 @@ PYBIND11_MODULE(_gol, m) {
       .def_readonly("compute_ms", &RunResult::compute_ms)
       .def_readonly("halo_ms", &RunResult::halo_ms)
       .def_readonly("fill_ms", &RunResult::fill_ms)
-      .def_readonly("allreduce_ms", &RunResult::allreduce_ms)
-      .def("as_dict", [](const RunResult& r) {
-        py::dict d;
-        d["generations"] = r.generations;
-        d["executed"] = r.executed;
-        d["first_unchanged"] = r.first_unchanged;
-        d["extinct"] = r.extinct;
-        d["stop_reason"] = r.stop_reason;
-        d["loop_ms"] = r.loop_ms;
-        d["exchanges"] = r.exchanges;
-        d["polls"] = r.polls;
-        d["kernel_launches"] = r.kernel_launches;
-        d["overlapped"] = r.overlapped;
-        d["graph_launches"] = r.graph_launches;
-        d["halo_bytes"] = r.halo_bytes;
-        d["linked_launches"] = r.linked_launches;
-        d["phase_timed"] = r.phase_timed;
-        d["compute_ms"] = r.compute_ms;
-        d["halo_ms"] = r.halo_ms;
-        d["fill_ms"] = r.fill_ms;
-        d["allreduce_ms"] = r.allreduce_ms;
-        return d;
-      });
+      .def_readonly("allreduce_ms", &RunResult::allreduce_ms);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const EngineConfig& c, std::shared_ptr<Backend> be, std::shared_ptr<Transport> tr) {

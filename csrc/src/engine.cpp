@@ -99,7 +99,7 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // falls back to plain buffers with periodic fills.
   int ring_dv = 0;
   void* ring_bufs[2] = {nullptr, nullptr};
-  if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !rows_wrapped_ && cfg_.tune.i("pitch_pad") == 0) {
+  if (dec_.Px == 1 && dec_.Py == 1 && !cfg_.self_exchange && !rows_wrapped_) {
     const TileGeom probe = TileGeom::make(cl, r.size(), c.size(), 0, hw);
     ring_dv = be_->row_ring_halo(probe.H, probe.pitch, tmax_);
     // The byte layout on bit words keeps its byte tiles too: the rings must
@@ -144,8 +144,6 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // epoch overlap; anything else on the stream (fills, exchanges, polls)
   // joins the streams first.  Not with column fills between blocks.
   link_ = kc.link && !cols_filled_;
-  // Experiment knob: extra bytes per padded row (multiple of 256).
-  g_.pitch += 256 * (std::max(0, cfg_.tune.i("pitch_pad")) / 256);
   // Several ranks: every poll is a flag all-reduce on the compute stream
   // (latency-bound), so poll half as often; a stop is still exact and at most
   // two windows late.
@@ -312,10 +310,9 @@ int Engine::pick_T(int64_t remaining) const {
   return 1;
 }
 
-// Two-phase halo exchange (columns, then full-width rows so the corner
-// cells travel with the rows): 4 messages instead of the reference's 8
-// per-generation messages with a strided MPI_Type_vector column
-// (src/game_mpi.c:335-383).
+// Phase A of the halo exchange (halo_exchange_on): west / east halo columns
+// of the owned rows, packed into contiguous buffers (RCCL has no strided
+// datatype, unlike the reference's MPI_Type_vector column).
 void Engine::exchange_columns(void* buf, const TileGeom& g) {
   auto* base = static_cast<uint8_t*>(buf);
   auto nb = dec_.neighbors(rank_);
@@ -355,9 +352,6 @@ void Engine::halo_exchange() { halo_exchange_on(buf_[cur_], g_); }
 
 void Engine::halo_exchange_on(void* buf, const TileGeom& g) {
   trace::Range tr("gol.halo_exchange");
-  auto* base = static_cast<uint8_t*>(buf);
-  auto nb = dec_.neighbors(rank_);
-  const int64_t H = g.H, pitch = g.pitch;
   if (rows_wrapped_ || (rows_ring_ && !cols_filled_)) {
     // Nothing to move: the kernels read the torus modulo its rows, or the
     // row halos alias the owned rows.  No stream join either, so linked
@@ -390,20 +384,26 @@ void Engine::halo_exchange_on(void* buf, const TileGeom& g) {
     be_->fill_periodic(buf, g, /*cols=*/false, /*rows=*/true);
     phase_end(kFill, t, nullptr);
   } else {
-    const int64_t Dv = g.Dv;
-    const size_t bytes = size_t(Dv * pitch);
-    std::vector<P2POp> ops = {
-        {true, nb[kNorth], base + Dv * pitch, bytes},        // my top rows -> north's bottom halo
-        {false, nb[kSouth], base + (Dv + H) * pitch, bytes},  // south's top rows -> my bottom halo
-        {true, nb[kSouth], base + H * pitch, bytes},          // my bottom rows -> south's top halo
-        {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
-    };
     void* t = phase_begin(nullptr);
-    tr_->exchange(ops, be_->stream());
+    tr_->exchange(row_ops(buf, g), be_->stream());
     phase_end(kHalo, t, nullptr);
-    halo_bytes_ += 2 * int64_t(bytes);
+    halo_bytes_ += 2 * g.Dv * g.pitch;
   }
   ++exchanges_;
+}
+
+// North / south halo rows over the full padded width, Dv rows each way.
+std::vector<P2POp> Engine::row_ops(void* buf, const TileGeom& g) const {
+  auto* base = static_cast<uint8_t*>(buf);
+  const auto nb = dec_.neighbors(rank_);
+  const int64_t Dv = g.Dv, H = g.H, pitch = g.pitch;
+  const size_t bytes = size_t(Dv * pitch);
+  return {
+      {true, nb[kNorth], base + Dv * pitch, bytes},        // my top rows -> north's bottom halo
+      {false, nb[kSouth], base + (Dv + H) * pitch, bytes},  // south's top rows -> my bottom halo
+      {true, nb[kSouth], base + H * pitch, bytes},          // my bottom rows -> south's top halo
+      {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
+  };
 }
 
 void* Engine::bit_scratch(int i) const {
@@ -535,21 +535,12 @@ void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
     be_->fill_cols_rows(out, g, Dv, H);
     phase_end(kFill, t, nullptr);
   }
-  auto* base = static_cast<uint8_t*>(out);
-  auto nb = dec_.neighbors(rank_);
-  const size_t bytes = size_t(Dv * pitch);
-  std::vector<P2POp> ops = {
-      {true, nb[kNorth], base + Dv * pitch, bytes},        // my top rows -> north's bottom halo
-      {false, nb[kSouth], base + (Dv + H) * pitch, bytes},  // south's top rows -> my bottom halo
-      {true, nb[kSouth], base + H * pitch, bytes},          // my bottom rows -> south's top halo
-      {false, nb[kNorth], base, bytes},                     // north's bottom rows -> my top halo
-  };
   // Phase timing would join the streams (timing_mark): only when it is on.
   void* tx = phase_begin(s);
-  tr_->exchange(ops, s ? s : be_->stream());
+  tr_->exchange(row_ops(out, g), s ? s : be_->stream());
   phase_end(kHalo, tx, s);
   rows_pending_ = true;  // stream-ordered before the next block on the compute stream
-  halo_bytes_ += 2 * int64_t(bytes);
+  halo_bytes_ += 2 * Dv * pitch;
   ++exchanges_;
   ++early_sends_;
 }

@@ -47,9 +47,6 @@ const std::vector<TuningKey>& tuning_keys() {
       {"host_threads", "GOL_HOST_THREADS", "0", 'i', "tune", "host thread pool size (0: min(cores, 16))"},
       {"cu_partition", "GOL_CU_PARTITION", "", 's', "tune",
        "k/n: this process's streams run on the k-th of n CU slices (ranks sharing a GPU)"},
-      // --- probe: timing probes (exact but measured slower, or wrong cells) -
-      {"link_force", "GOL_LINK_FORCE", "0", 'i', "probe", "run the linked kernel unlinked (its cost probe)"},
-      {"pitch_pad", "GOL_PITCH_PAD", "0", 'i', "probe", "extra bytes per padded row (multiple of 256)"},
       // --- diag ------------------------------------------------------------
       {"check_device", "GOL_CHECK_DEVICE", "0", 'i', "diag", "assert device affinity of every call and buffer"},
       {"tune_log", "GOL_TUNE_LOG", "0", 'i', "diag", "log per-launch-shape autotuning decisions"},

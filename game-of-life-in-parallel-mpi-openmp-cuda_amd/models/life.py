@@ -132,7 +132,7 @@ def make_backend(engine: str = "auto", device: int = 0, threads: int = 0, tune=N
 
 # Tuning keys the engine reads from EngineConfig::tune (engine.cpp); the rest
 # are read by the backend (or the transports) at construction.
-_ENGINE_KEYS = frozenset({"u8_via_bits", "side_poll", "poll_copy_side", "watchdog_s", "pitch_pad", "overlap_auto",
+_ENGINE_KEYS = frozenset({"u8_via_bits", "side_poll", "poll_copy_side", "watchdog_s", "overlap_auto",
                           "cpu_side_poll"})
 
 

@@ -9,8 +9,6 @@ per-phase times and the parallel layout.
 from __future__ import annotations
 
 import json
-import time
-from contextlib import contextmanager
 from typing import Any, Optional
 
 
@@ -28,25 +26,6 @@ def stdout_lines(style: str, generations: int, loop_ms: float, read_ms: float = 
     if style == "cuda":
         return f"Generations:\t{generations}\nExecution time:\t{loop_ms:.2f} msecs\nFinished\n"
     return f"Finished.\n\nGenerations:\t{generations}\nExecution time:\t{loop_ms:.2f} msecs\nFinished\n"
-
-
-class PhaseTimer:
-    """Wall-clock phase accounting (steady host clock)."""
-
-    def __init__(self) -> None:
-        self.ms: dict[str, float] = {}
-
-    @contextmanager
-    def phase(self, name: str, sync=None):
-        if sync:
-            sync()
-        t0 = time.perf_counter()
-        try:
-            yield
-        finally:
-            if sync:
-                sync()
-            self.ms[name] = self.ms.get(name, 0.0) + (time.perf_counter() - t0) * 1e3
 
 
 def write_json(path: Optional[str], record: dict[str, Any]) -> None:

@@ -12,7 +12,6 @@ sys.path.insert(0, REPO)
 from gol_amd._native import native  # noqa: E402
 
 CLASSES = {"tune": "Performance knobs of the default build",
-           "probe": "Timing probes of the default kernels (exact but slower, or wrong cells by design)",
            "diag": "Traces, logs and consistency checks",
            "fault": "Fault injection (tests)",
            "emul": "CPU backend emulating device features (tests)"}

@@ -26,14 +26,13 @@ def test_table_defaults_and_classes(native):
     t = native.Tuning()
     assert t.changed() == {} and t.summary() == "defaults"
     assert len({k["key"] for k in keys}) == len(keys) and len({k["env"] for k in keys}) == len(keys)
-    assert {k["class"] for k in keys} == {"tune", "probe", "diag", "fault", "emul"}
+    assert {k["class"] for k in keys} == {"tune", "diag", "fault", "emul"}
     for k in keys:
         assert k["env"].startswith("GOL_") and t.get(k["key"]) == k["default"] and t.source(k["key"]) == "default"
-    # the timing probes are probe-class; the measured-slower variants are gone
+    # the measured-slower variants and their probes are gone
     cls = {k["key"]: k["class"] for k in keys}
-    for key in ("link_force", "pitch_pad"):
-        assert cls[key] == "probe", key
-    for gone in ("flow", "resident", "split", "short", "pipe", "skew", "wpl", "lds_add"):
+    for gone in ("flow", "resident", "split", "short", "pipe", "skew", "wpl", "lds_add", "link_force", "pitch_pad",
+                 "chain_acquire", "link_events"):
         assert gone not in cls, gone
 
 
