@@ -73,19 +73,13 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   // adds one per such group when it publishes).
   L.bnd_n = 0;
   q.bnd_count = nullptr;
-  q.bnd_hot = L.bnd_req ? 1 : 0;
-  if (L.bnd_req)
-    for (int i = 0; i < 4; ++i) q.bnd_r[i] = L.bnd_r[i];
-  if (L.bnd_req && L.bnd_count_req && L.bnd_count) {
-    int64_t n = 0;
-    for (int g = 0; g < q.nseg; ++g) {
-      const int64_t e = q.row_lo + int64_t(g) * q.seg_rows + std::min(g, q.seg_rem) + q.seg_rows +
-                        (g < q.seg_rem ? 1 : 0);
-      const int64_t b = e - q.seg_rows - (g < q.seg_rem ? 1 : 0);
-      n += group_meets(b, e, L.bnd_r) ? 1 : 0;
+  for (int& g : q.bnd_g) g = 0;
+  if (L.bnd_req) {
+    const int n = trigger_groups(q, L.bnd_r, q.bnd_g);
+    if (L.bnd_count_req && L.bnd_count) {
+      L.bnd_n = int64_t(n) * q.ncolw;
+      q.bnd_count = L.bnd_count;
     }
-    L.bnd_n = n * q.ncolw;
-    q.bnd_count = L.bnd_count;
   }
   L.bnd_req = false;
   q.link_flag = L.flags[L.seq % 3];

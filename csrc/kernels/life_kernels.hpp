@@ -75,13 +75,16 @@ struct LifeBlockParams {
   // > 0: both launches cover the owned rows of a row ring of this many rows;
   // the rows a group reads beyond them wrap around the torus (link_wait).
   int64_t link_ring_rows;
-  // Boundary trigger (BlockArgs::trigger; linked launches only): after its
-  // link_flag store, every group whose output rows meet [bnd_r[0], bnd_r[1])
-  // or [bnd_r[2], bnd_r[3]) adds 1 to *bnd_count (system scope: a stream
-  // waits on it with hipStreamWaitValue64).  Null: off.
+  // Boundary trigger (BlockArgs::trigger / hot; linked launches only): the
+  // groups grp in [bnd_g[0], bnd_g[1]) or [bnd_g[2], bnd_g[3]) - those whose
+  // output rows meet the trigger rows, trigger_groups() - run at top issue
+  // priority, and with bnd_count set each adds 1 to *bnd_count after its
+  // link_flag store (a one-wave kernel on another stream waits on it,
+  // launch_wait_counter).  Group indices, not rows, so the kernel's test is
+  // a few scalar compares (row bounds in 64 bits cost the linked kernels
+  // SGPR spills).
   unsigned long long* bnd_count;
-  int64_t bnd_r[4];
-  int bnd_hot;  // groups meeting bnd_r run at top issue priority (with or without bnd_count)
+  int bnd_g[4];
   // Fault injection (GOL_FAULT_DELAY_SPINS, tests): producers at the torus
   // seam - a linked launch's first and last groups - sleep this many s_sleep 127
   // rounds (~3.4 us each) before publishing, so a missing dependency wait
@@ -133,11 +136,27 @@ struct LinkState {
   int64_t bnd_n = 0;
 };
 
-// Groups of a grouped plan whose output rows meet the two trigger ranges,
-// counted per column strip (a folded strip publishes each of its groups
-// once, so the launch makes ncolw times this many increments).
-inline __host__ __device__ bool group_meets(int64_t g0, int64_t g1, const int64_t* r) {
-  return (g0 < r[1] && g1 > r[0]) || (g0 < r[3] && g1 > r[2]);
+// The groups of a grouped plan whose output rows meet the trigger rows
+// [r[0], r[1]) and [r[2], r[3]): index ranges [g[0], g[1]) and [g[2], g[3])
+// (each contiguous: groups are ordered by row); returns how many groups meet
+// either, per column strip (a folded strip publishes each of its groups once,
+// so a counting launch makes ncolw times this many increments).
+inline int trigger_groups(const LifeBlockParams& q, const int64_t* r, int* g) {
+  int n = 0;
+  g[0] = g[1] = g[2] = g[3] = 0;
+  for (int s = 0; s < q.nseg; ++s) {
+    const int64_t e = q.row_lo + int64_t(s) * q.seg_rows + std::min(s, q.seg_rem) + q.seg_rows + (s < q.seg_rem ? 1 : 0);
+    const int64_t b = e - q.seg_rows - (s < q.seg_rem ? 1 : 0);
+    bool any = false;
+    for (int k = 0; k < 2; ++k)
+      if (b < r[2 * k + 1] && e > r[2 * k]) {
+        if (g[2 * k + 1] == 0) g[2 * k] = s;
+        g[2 * k + 1] = s + 1;
+        any = true;
+      }
+    n += any ? 1 : 0;
+  }
+  return n;
 }
 
 // Everything enqueued on stream[1] precedes what comes next on stream[0];

@@ -73,7 +73,9 @@ def test_bench_launches_its_own_ranks_on_gpu(gpu):
     cfg = rec["config"]
     assert cfg["shared_gpus"] is (_ndev() < 2) and cfg["generations_timed"] == 400
     assert "rccl" in cfg["parallelism"] and cfg["halo_bytes_per_step"] > 0
-    assert cfg["overlap_mode"] in ("auto:plain", "auto:trigger")
+    # Ranks sharing a GPU run on CU partitions, where linked launches - and
+    # with them the trigger schedule - are off: nothing to trial there.
+    assert cfg["overlap_mode"] in (("off",) if cfg["shared_gpus"] else ("auto:plain", "auto:trigger"))
     ph = cfg["phase_ms_one_step"]
     assert ph["compute_ms"] > 0 and ph["halo_ms"] > 0 and ph["allreduce_ms"] > 0
 
@@ -94,7 +96,9 @@ def test_bench_node_rehearsal_8_ranks_full_grid(gpu):
     assert sorted(d["rank"] for d in rec["devices"]) == list(range(8))
     cfg = rec["config"]
     assert cfg["parallelism"].startswith("1x8") and cfg["generations_timed"] == 2000
-    assert cfg["overlap_mode"] in ("auto:plain", "auto:trigger")
+    # Ranks sharing a GPU run on CU partitions, where linked launches - and
+    # with them the trigger schedule - are off: nothing to trial there.
+    assert cfg["overlap_mode"] in (("off",) if cfg["shared_gpus"] else ("auto:plain", "auto:trigger"))
     if cfg["shared_gpus"]:
         # A rehearsal is labelled as one (VERDICT r04 Weak 5), and every rank
         # ran on a CU partition of its own with no hand-set knobs.
