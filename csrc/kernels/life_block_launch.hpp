@@ -103,8 +103,9 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
     // vs 1.61 ms per 1000 generations, profiles/r04/linked_events_ab.jsonl),
     // although an event wait between two streams costs ~10 us of device time.
     // Its stream also orders it after the launch two back, whose completion
-    // words (flags[seq % 3]) it overwrites.
-    (void)hipStreamWaitEvent(st, L.before[L.cur], 0);
+    // words (flags[seq % 3]) it overwrites.  After an armed boundary trigger
+    // the stream's wait kernel already implies that start (LinkState::started).
+    if (!L.started) (void)hipStreamWaitEvent(st, L.before[L.cur], 0);
     ++L.linked;
   } else {
     link_join(L);
@@ -113,6 +114,7 @@ bool launch_linked(const LifeBlockParams& p0, int64_t out_rows, int simds, const
   (void)hipEventRecord(L.before[which], st);
   ++L.chain;
   hipLaunchKernelGGL((life_group_kernel<T, LIO, M>), dim3(unsigned(blocks)), dim3(64 * M), 0, st, q);
+  L.started = false;
   L.cur = which;
   L.prev = q;
   L.prev_out = q.out;

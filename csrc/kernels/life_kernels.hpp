@@ -126,6 +126,11 @@ struct LinkState {
   uint32_t seq = 0;
   int64_t linked = 0;                           // launches that ran linked (diagnostics)
   int chain = 0;  // launches in the current chain
+  // The stream of the next launch already follows the last launch's start
+  // (Backend::trigger_stream: its wait kernel returns only once that
+  // launch's boundary groups are done), so a linked next launch needs no
+  // cross-stream event wait (~10 us of device time on the epoch boundary).
+  bool started = false;
   // Boundary trigger of the next launch (BlockArgs::trigger): requested
   // rows, the counter, and how many increments the launch will make
   // (launch_linked sets it; 0: the launch could not carry the trigger).
@@ -162,6 +167,7 @@ inline int trigger_groups(const LifeBlockParams& q, const int64_t* r, int* g) {
 // Everything enqueued on stream[1] precedes what comes next on stream[0];
 // the next launch starts a new chain.
 inline void link_join(LinkState& L) {
+  L.started = false;
   if (L.cur != 0) {
     (void)hipEventRecord(L.before[1], L.stream[1]);
     (void)hipStreamWaitEvent(L.stream[0], L.before[1], 0);

@@ -538,6 +538,7 @@ class HipBackend final : public Backend {
       GOL_ON_DEVICE();
       hipk::launch_wait_counter(trigger_counter(), trigger_target_, tune_.err, stream_);
       HIP_CHECK(hipGetLastError());
+      link_.started = true;  // the next launch on this stream follows the trigger launch's start
       *armed = true;
     } else {
       join_streams();
