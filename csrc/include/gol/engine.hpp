@@ -243,7 +243,7 @@ class Engine {
   void halo_exchange_on(void* buf, const TileGeom& g);
   // Byte layout on bit words (EngineConfig::u8_compute = 1): one epoch on
   // the bit tile, and the per-run pack / unpack of the byte tile.
-  void epoch_via_bits(int64_t d, bool sent_early);
+  void epoch_via_bits(int64_t d, bool sent_ahead);
   void pack_bits();
   void unpack_bits();
   void sync_bytes();  // unpack a live bit image into the byte tile (pack_bits in engine.cpp)
@@ -288,7 +288,7 @@ class Engine {
   int64_t triggered_sends_ = 0;
   bool send_next_ = false;           // the current epoch is followed by another one in this run
   bool rows_pending_ = false;        // halo rows of buf_[cur_] were sent by the last block
-  int64_t early_sends_ = 0;
+  int64_t boundary_sends_ = 0;      // exchanges sent from an epoch's last block (RunResult::overlapped)
   bool use_graphs_ = false, capturing_ = false;
   int64_t* gen_dev_ = nullptr;        // device: (epoch start - flags_base_) for graph replays
   int64_t epoch_start_ = 0;

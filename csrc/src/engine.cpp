@@ -415,9 +415,9 @@ void* Engine::bit_scratch(int i) const {
 // bit_scratch(bpar_) when a run starts and unpacks it when the run ends): the
 // halo exchange or fill and every temporal block run on the bit tile, whose
 // per-generation flags are those of the same cells.
-void Engine::epoch_via_bits(int64_t d, bool sent_early) {
+void Engine::epoch_via_bits(int64_t d, bool sent_ahead) {
   trace::Range tr("gol.epoch_via_bits");
-  if (!sent_early) halo_exchange_on(bit_scratch(bpar_), gb_);
+  if (!sent_ahead) halo_exchange_on(bit_scratch(bpar_), gb_);
   // A partial epoch's trapezoid starts d rows outside the owned rows; a row
   // ring's blocks all cover exactly the owned rows (a = Dv - T).
   const bool full = d == D_;
@@ -467,17 +467,17 @@ void Engine::unpack_bits() {
 }
 
 void Engine::run_epoch(int64_t d) {
-  const bool sent_early = rows_pending_;
+  const bool sent_ahead = rows_pending_;
   // The previous epoch's last block sent this buffer's boundary rows
   // (stream-ordered before this epoch's first block).
   rows_pending_ = false;
   // The previous epoch ends here.
   if (auto_overlap_) auto_mark();
   if (via_bits_) {
-    epoch_via_bits(d, sent_early);
+    epoch_via_bits(d, sent_ahead);
     return;
   }
-  if (!sent_early) halo_exchange();
+  if (!sent_ahead) halo_exchange();
   // A partial epoch (d < D) needs only d halo rows: its trapezoid starts d
   // rows outside the owned rows, not D.
   const bool full = d == D_;
@@ -542,7 +542,7 @@ void Engine::last_block_trigger(void* in, void* out, const TileGeom& g, int T) {
   rows_pending_ = true;  // stream-ordered before the next block on the compute stream
   halo_bytes_ += 2 * Dv * pitch;
   ++exchanges_;
-  ++early_sends_;
+  ++boundary_sends_;
 }
 
 // An earlier block of a trigger epoch (d generations left before it): the
@@ -745,7 +745,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     be_->i64_async(gen_dev_, 0, /*add=*/false);  // first epoch starts at flags_base_
   }
   const int64_t g0 = graph_runs_;
-  const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_, es0 = early_sends_;
+  const int64_t e0 = exchanges_, p0 = polls_, l0 = launches_, hb0 = halo_bytes_, es0 = boundary_sends_;
   const int64_t lk0 = be_->linked_launches();
   trace::Range trace_run("gol.run");
   if (cfg_.timing_barriers) {
@@ -847,7 +847,7 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
   res.exchanges = exchanges_ - e0;
   res.polls = polls_ - p0;
   res.kernel_launches = launches_ - l0;
-  res.overlapped = early_sends_ > es0;
+  res.overlapped = boundary_sends_ > es0;
   res.graph_launches = graph_runs_ - g0;
   res.halo_bytes = halo_bytes_ - hb0;
   res.linked_launches = be_->linked_launches() - lk0;
