@@ -198,6 +198,13 @@ Engine::Engine(const EngineConfig& cfg, Backend* backend, Transport* transport)
   // Auto: deeper blocks only.
   const int pcs = cfg_.tune.i("poll_copy_side");
   poll_copy_side_ = pcs > 0 || (pcs < 0 && tmax_ > 8);
+  // A single-rank device tile whose polls join the compute streams (T <= 8:
+  // each join restarts the linked chain) polls every 1024 generations: 8192^2
+  // 1.52 vs 1.62 ms per 1000 generations, 4096^2 1.20 vs 1.22 (medians of 8,
+  // profiles/r06/poll_interval.jsonl).  A stop is still exact, and at most two
+  // windows late.
+  if (cfg_.poll_gens <= 0 && be_->is_device() && tr_->size() == 1 && !cfg_.self_exchange && !poll_copy_side_)
+    poll_gens_ = 1024;
   // side_poll = -1 (default): after the overlap trial the ranks time both
   // poll placements (poll_trial_step) and keep the faster, as for overlap.
   const int sp = cfg_.tune.i("side_poll");
