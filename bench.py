@@ -9,7 +9,7 @@ src/game_mpi.c:385-424, src/game_cuda.cu:219-279).
 One *step* = one run of the reference's benchmark unit: GEN_LIMIT = 1000
 generations of the full 32768^2 grid (--gens-per-step), B3/S23 on a torus
 with the reference's termination checks on (per-generation change flags
-fused into the kernel, polled every 256 generations and resolved exactly at
+fused into the kernel, polled every 256-1024 generations and resolved exactly at
 the end of the step) and every halo exchange the decomposition needs.  Each
 step continues the same grid (a random 32768^2 soup never reaches a fixed
 point within the run; if it did, the step would stop there exactly as the
