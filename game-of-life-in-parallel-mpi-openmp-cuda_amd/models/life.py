@@ -41,7 +41,8 @@ class LifeConfig:
     tmax: int = 0               # generations per kernel launch (0 = the backend's choice: bits 12 adder /
                                 # 16 DPP; u8 32 / 24 / 16 by tile size)
     epoch: int = 0              # generations per halo exchange (0 = 8*tmax, 16*tmax with several ranks)
-    poll_gens: int = 0          # generations between termination polls (0 = 256, 512 with several ranks)
+    poll_gens: int = 0          # generations between termination polls (0: 256; 512 with several ranks;
+                                # 1024 on single-rank device tiles whose polls join the compute streams)
     overlap: str = "auto"       # auto | on (= trigger) | off | trigger: overlap the row halo exchange with compute
     lagged_poll: bool = True    # check termination polls one window late (no queue drain)
     graphs: str = "off"         # auto | on | off: replay full epochs as captured HIP graphs

@@ -875,6 +875,28 @@ def test_linked_chain_continues_across_polls(gpu, tune, seed, density):
         assert a.kernel_launches == 75 and a.linked_launches == 74 and a.polls >= 9, a
 
 
+@pytest.mark.parametrize("seed,density", [(77, 0.004), (3, 0.01), (5, 0.5)])
+def test_default_poll_interval_termination_exact(gpu, tune, seed, density):
+    """A single-rank tile whose polls join the linked streams (T <= 8) polls
+    every 1024 generations by default (round 6): the stop is still exact -
+    the same Generations, reason and final grid as polling every 64 - and a
+    run to the limit makes one poll per 1024 generations (plus the last)."""
+    tune.pop("u8_via_bits", None)
+    W = H = 8192
+    g = random_grid(W, H, seed, density)
+    out = []
+    for poll in (0, 64):
+        sim = Simulation(LifeConfig(W, H, gen_limit=2500, poll_gens=poll, tune=tune), engine="hip")
+        assert sim.describe()["tmax"] == 8
+        sim.load(g)
+        out.append((sim.run(), sim.tile()))
+    (a, ta), (b, tb) = out
+    assert (a.generations, a.stop_reason) == (b.generations, b.stop_reason)
+    assert (ta == tb).all()
+    if a.stop_reason == "limit":
+        assert a.polls == 3 and b.polls > 30, (a.polls, b.polls)
+
+
 @pytest.mark.parametrize("part", ["0/2", "1/4", "3/8"])
 def test_cu_partition_single_process(gpu, tune, part):
     """tuning cu_partition=k/n (ranks sharing a GPU): the backend's streams
