@@ -31,9 +31,10 @@ class InProcessGroup:
         devs = list(devices) if devices else [0]
         self.sims: list[Simulation] = []
         self.backends = []
-        # Every backend before any engine: an engine's schedule may depend on
-        # how many ranks share its device (resident epochs need a whole GPU),
-        # and all ranks must take the same decision.
+        # Every backend before any engine, so that all ranks' devices are set
+        # up before any schedule is decided.  (Several engines on one device
+        # share its hardware queues: their linked launches may serialise,
+        # docs/PERFORMANCE.md "Open problems"; results are exact either way.)
         self.backends = [make_backend(engine, devs[r % len(devs)], threads_per_rank, config.tune)
                          for r in range(self.nranks)]
         for r, be in enumerate(self.backends):
