@@ -10,4 +10,4 @@ for i in $(seq 1 "$N"); do
   timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$O/r$i" -o run -- python3 bench.py "$@" \
     > "$O/r$i.json" 2> "$O/r$i.err" || { echo "run $i failed"; exit 1; }
 done
-python3 scripts/queue_check.py "$O"/r[0-9]*[0-9]
+python3 scripts/queue_check.py "$O"/r[0-9] "$O"/r[0-9][0-9] 2>/dev/null
