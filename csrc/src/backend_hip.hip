@@ -6,6 +6,7 @@
 // the backend's stream and only the engine's periodic flag poll and the
 // final copy-out block the host.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <array>
@@ -24,6 +25,7 @@
 #include "../kernels/life_kernels.hpp"
 #include "gol/backend.hpp"
 #include "gol/hip_util.hpp"
+#include "gol/numa.hpp"
 #include "gol/trace.hpp"
 
 namespace gol {
@@ -51,6 +53,14 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
     cus_ = prop.multiProcessorCount;
+    // The process's host threads on this GPU's NUMA node (gol/numa.hpp).
+    if (t.i("numa_pin") > 0) {
+      char bus[64] = {0};
+      if (hipDeviceGetPCIBusId(bus, int(sizeof(bus)), dev_) == hipSuccess)
+        numa_ = pin_process_to_numa(bus, t.i("numa_pin") == 2 && t.s("cu_partition").empty());
+      cpu_set_t s;
+      if (numa_ >= 0 && sched_getaffinity(0, sizeof(s), &s) == 0) numa_cpus_ = CPU_COUNT(&s);
+    }
     // A CU partition (tuning cu_partition, ranks sharing a GPU): every stream
     // of this backend runs on the slice, and launches are planned for it.
     if (const int part = mask_cus(cu_partition_mask(t.s("cu_partition"), cus_))) {
@@ -185,7 +195,8 @@ class HipBackend final : public Backend {
   std::string name() const override {
     hipk::LifeTuning t = tune_;
     t.chain = chain_mode_;
-    return "hip:" + std::to_string(dev_) + ":" + arch_ + cu_part_ + " [" + hipk::life_block_variant(Layout::Bits, t) +
+    const std::string numa = numa_ >= 0 ? " numa=" + std::to_string(numa_) + ":" + std::to_string(numa_cpus_) + "cpus" : "";
+    return "hip:" + std::to_string(dev_) + ":" + arch_ + cu_part_ + numa + " [" + hipk::life_block_variant(Layout::Bits, t) +
            "; " + hipk::life_block_variant(Layout::U8, t) + "]";
   }
   int preferred_tmax(Layout l) const override { return hipk::life_block_max_T(l, tune_); }
@@ -1011,6 +1022,8 @@ class HipBackend final : public Backend {
   std::string arch_;
   int cus_ = 256;          // CUs this backend's launches may use (its partition, if any)
   std::string cu_part_;    // GOL_CU_PARTITION, for name()
+  int numa_ = -1;          // NUMA node the process was pinned to (tuning numa_pin), for name()
+  int numa_cpus_ = 0;      // CPUs it may run on there
   hipk::LifeTuning tune_;
   hipStream_t comm_ = nullptr;
   // chain_mem: chained groups' flags, slots; linked launches' 3 x completion words.

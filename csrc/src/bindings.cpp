@@ -19,6 +19,7 @@
 #include "gol/decomp.hpp"
 #include "gol/engine.hpp"
 #include "gol/io.hpp"
+#include "gol/numa.hpp"
 #include "gol/transport.hpp"
 
 namespace py = pybind11;
@@ -172,6 +173,9 @@ PYBIND11_MODULE(_gol, m) {
   m.def("hip_pci_bus_id", &hip_pci_bus_id);
   m.def("hip_release_errors", &hip_release_errors);
   m.def("hip_uuid", &hip_uuid);
+  m.def("parse_cpulist", &parse_cpulist);
+  m.def("pci_numa_node", &pci_numa_node);
+  m.def("pinned_numa_node", &pinned_numa_node);
 
   py::class_<Transport, std::shared_ptr<Transport>>(m, "Transport")
       .def("rank", &Transport::rank)

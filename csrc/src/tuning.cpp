@@ -45,6 +45,9 @@ const std::vector<TuningKey>& tuning_keys() {
        "blocks are deeper than 8 generations, 1 always, 0 never (join the compute streams, copy there)"},
       {"watchdog_s", "GOL_WATCHDOG_S", "0", 'f', "tune", "poll watchdog in seconds (0: 900; EngineConfig wins)"},
       {"host_threads", "GOL_HOST_THREADS", "0", 'i', "tune", "host thread pool size (0: min(cores, 16))"},
+      {"numa_pin", "GOL_NUMA_PIN", "1", 'i', "tune",
+       "device backends pin the process's host threads to their GPU's NUMA node: 1 the node, 2 one L3 cache of it "
+       "(per GPU of the node), 0 leave placement alone"},
       {"cu_partition", "GOL_CU_PARTITION", "", 's', "tune",
        "k/n: this process's streams run on the k-th of n CU slices (ranks sharing a GPU)"},
       // --- diag ------------------------------------------------------------

@@ -30,7 +30,8 @@ ARCH = os.environ.get("GOL_OFFLOAD_ARCH", "gfx950")
 BUILD = REPO / "build" / "obj"
 
 HOST_SRCS = ["src/decomp.cpp", "src/parallel.cpp", "src/backend_cpu.cpp", "src/transport.cpp",
-             "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp", "src/tuning.cpp"]
+             "src/engine.cpp", "src/io.cpp", "src/cpu_ref.cpp", "src/checkpoint.cpp", "src/tuning.cpp",
+             "src/numa.cpp"]
 # One translation unit per compiled kernel variant (layout x cross-lane
 # window), so the build compiles them in parallel.  The variants measured
 # slower than these (resident epochs, persistent dataflow launches, short
