@@ -93,11 +93,15 @@ inline int mask_cus(const std::vector<uint32_t>& m) {
   return c;
 }
 // A stream for `dev`'s work: non-blocking, or restricted to the CU partition
-// `cu_partition` when it names one (HIP's CU-masked streams).
-inline hipStream_t make_stream(int dev, const std::string& cu_partition) {
+// `cu_partition` when it names one (HIP's CU-masked streams).  `own_queue`:
+// CU-masked to the whole device when no partition is named - HIP gives a
+// CU-masked stream a hardware queue of its own instead of one from the
+// process's shared pool.
+inline hipStream_t make_stream(int dev, const std::string& cu_partition, bool own_queue = false) {
   hipDeviceProp_t prop;
   HIP_CHECK(hipGetDeviceProperties(&prop, dev));
-  const std::vector<uint32_t> m = cu_partition_mask(cu_partition, prop.multiProcessorCount);
+  std::vector<uint32_t> m = cu_partition_mask(cu_partition, prop.multiProcessorCount);
+  if (m.empty() && own_queue) m = cu_partition_mask("0/1", prop.multiProcessorCount);
   hipStream_t s = nullptr;
   if (m.empty())
     HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));

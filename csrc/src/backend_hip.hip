@@ -100,7 +100,10 @@ class HipBackend final : public Backend {
     link_on_ = link_mode_ > 0;
     if (link_mode_ != 0) {
       link_.stream[0] = stream_;
-      link_.stream[1] = make_stream(dev_, tuning_.s("cu_partition"));
+      // A queue of its own (tuning link_queue): from HIP's pool of
+      // GPU_MAX_HW_QUEUES queues it could share one with the first stream or
+      // with another engine's, and linked launches on one queue serialise.
+      link_.stream[1] = make_stream(dev_, tuning_.s("cu_partition"), t.on("link_queue"));
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     // A GPU shared by several processes (a CU partition) time-slices their
