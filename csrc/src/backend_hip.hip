@@ -48,7 +48,7 @@ class HipBackend final : public Backend {
     check_dev_ = t.on("check_device");
     ring_on_ = t.on("row_ring");
     GOL_ON_DEVICE();
-    stream_ = make_stream(dev_, tuning_.s("cu_partition"));
+    stream_ = make_stream(dev_, tuning_.s("cu_partition"), t.i("link_queue") >= 2);
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;

@@ -27,8 +27,8 @@ const std::vector<TuningKey>& tuning_keys() {
       {"link", "GOL_LINK", "-1", 'i', "tune",
        "linked launches: -1 where the engine asks (small ring tiles, rank tiles), 0 never, 1 every eligible launch"},
       {"link_queue", "GOL_LINK_QUEUE", "1", 'i', "tune",
-       "the second linked stream gets a hardware queue of its own (CU-masked to the whole device); 0: HIP's "
-       "shared queue pool"},
+       "the second linked stream gets a hardware queue of its own (CU-masked to the whole device); 2: the first "
+       "too; 0: HIP's shared queue pool"},
       {"wrap", "GOL_WRAP", "1", 'i', "tune", "full-width tiles wrap column reads (no halo columns)"},
       {"fold", "GOL_FOLD", "1", 'i', "tune", "fold a narrow last column strip into the others' waves"},
       {"row_ring", "GOL_ROW_RING", "1", 'i', "tune", "single-rank tiles on a row ring (aliased halo rows)"},
