@@ -48,7 +48,13 @@ class HipBackend final : public Backend {
     check_dev_ = t.on("check_device");
     ring_on_ = t.on("row_ring");
     GOL_ON_DEVICE();
-    stream_ = make_stream(dev_, tuning_.s("cu_partition"), t.i("link_queue") >= 2);
+    // Tuning link_queue: -1 (default) the second linked stream gets a
+    // hardware queue of its own when another backend already lives on this
+    // device in this process, 1 always, 2 both linked streams, 0 never.
+    const int lq = t.i("link_queue");
+    GOL_REQUIRE(lq >= -1 && lq <= 2, "tuning link_queue: -1, 0, 1 or 2");
+    const bool shared_dev = live_backends(dev_).fetch_add(1) > 0;
+    stream_ = make_stream(dev_, tuning_.s("cu_partition"), lq >= 2);
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
@@ -101,9 +107,13 @@ class HipBackend final : public Backend {
     if (link_mode_ != 0) {
       link_.stream[0] = stream_;
       // A queue of its own (tuning link_queue): from HIP's pool of
-      // GPU_MAX_HW_QUEUES queues it could share one with the first stream or
-      // with another engine's, and linked launches on one queue serialise.
-      link_.stream[1] = make_stream(dev_, tuning_.s("cu_partition"), t.on("link_queue"));
+      // GPU_MAX_HW_QUEUES queues a later backend's second stream can share one
+      // with its first, and linked launches on one queue serialise (8192^2
+      // 2.68 vs 1.47 ms).  Not for a process's only backend: there the
+      // CU-masked queue measured the same on single-rank tiles but made the
+      // rehearsed rank tile's side-stream polls 2x slower
+      // (profiles/r06/link_queue/).
+      link_.stream[1] = make_stream(dev_, tuning_.s("cu_partition"), lq >= 1 || (lq < 0 && shared_dev));
       for (auto& e : link_.before) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     // A GPU shared by several processes (a CU partition) time-slices their
@@ -153,7 +163,12 @@ class HipBackend final : public Backend {
     tune_.chain_spin_log2 = std::min(24, std::max(4, t.i("chain_spin")));
     HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&tune_.err), err_host_, 0));
   }
+  static std::atomic<int>& live_backends(int dev) {
+    static std::atomic<int> n[64];
+    return n[dev & 63];
+  }
   ~HipBackend() override {
+    live_backends(dev_).fetch_sub(1);
     if (prof_on_ && prof_n_ > 0)
       std::fprintf(stderr, "gol host profile: %lld blocks; per block: engine between blocks %.2f us, run_block %.2f us "
                    "(launch call %.2f us)\n", (long long)prof_n_, prof_gap_ / double(std::max<int64_t>(1, prof_n_ - 1)),

@@ -26,9 +26,9 @@ const std::vector<TuningKey>& tuning_keys() {
       {"chain_spin", "GOL_CHAIN_SPIN", "16", 'i', "tune", "log2 of a chained wave's spin budget"},
       {"link", "GOL_LINK", "-1", 'i', "tune",
        "linked launches: -1 where the engine asks (small ring tiles, rank tiles), 0 never, 1 every eligible launch"},
-      {"link_queue", "GOL_LINK_QUEUE", "1", 'i', "tune",
-       "the second linked stream gets a hardware queue of its own (CU-masked to the whole device); 2: the first "
-       "too; 0: HIP's shared queue pool"},
+      {"link_queue", "GOL_LINK_QUEUE", "-1", 'i', "tune",
+       "the second linked stream on a hardware queue of its own (CU-masked to the whole device): -1 when another "
+       "backend already lives on the device in this process, 1 always, 2 both linked streams, 0 never (HIP's pool)"},
       {"wrap", "GOL_WRAP", "1", 'i', "tune", "full-width tiles wrap column reads (no halo columns)"},
       {"fold", "GOL_FOLD", "1", 'i', "tune", "fold a narrow last column strip into the others' waves"},
       {"row_ring", "GOL_ROW_RING", "1", 'i', "tune", "single-rank tiles on a row ring (aliased halo rows)"},

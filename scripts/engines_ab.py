@@ -6,10 +6,10 @@ because of its place in the process shows up beside the others.  Found with
 it: HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by
 default), so the second engine's two linked compute streams shared a queue
 and its linked launches serialised (8192^2 2.83 vs 1.48-1.51 ms; with 8
-queues 1.50 for all three).  Fixed since by giving the second linked stream a
-hardware queue of its own (tuning link_queue = 1, a stream CU-masked to the
-whole device): 1.47-1.52 ms for all three with 4 queues; link_queue=0 shows
-the old behaviour.
+queues 1.50 for all three).  Fixed since: a backend created while another
+lives on its device gives its second linked stream a hardware queue of its own
+(tuning link_queue = -1, a stream CU-masked to the whole device): 1.49-1.55 ms
+for all three with 4 queues; link_queue=0 shows the old behaviour.
 
     python scripts/engines_ab.py [SIZE] [ENGINES] [ROUNDS]
 """
