@@ -163,6 +163,8 @@ class Engine {
   std::string poll_mode() const;
   double poll_trial_ms_joined() const { return poll_ms_[0]; }
   double poll_trial_ms_side() const { return poll_ms_[1]; }
+  // Median of the run of side windows that checked a side decision (-1: none).
+  double poll_trial_ms_side_steady() const { return poll_side_steady_ms_; }
   // Epoch exchanges started by the boundary trigger so far (diagnostics).
   int64_t triggered_sends() const { return triggered_sends_; }
   // Sample per-phase device times into RunResult (event pairs around every
@@ -345,6 +347,8 @@ class Engine {
   std::vector<AutoSpan> ptrial_spans_;
   int ptrial_counts_[2] = {0, 0};
   double poll_ms_[2] = {-1, -1};
+  bool ptrial_verify_ = false;      // checking a side decision on consecutive side windows
+  double poll_side_steady_ms_ = -1;
   // Phase timing.
   bool phase_timing_ = false;
   struct PhaseSpan {

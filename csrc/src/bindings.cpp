@@ -295,6 +295,7 @@ PYBIND11_MODULE(_gol, m) {
       .def("poll_mode", &Engine::poll_mode)
       .def_property_readonly("poll_trial_ms_joined", &Engine::poll_trial_ms_joined)
       .def_property_readonly("poll_trial_ms_side", &Engine::poll_trial_ms_side)
+      .def_property_readonly("poll_trial_ms_side_steady", &Engine::poll_trial_ms_side_steady)
       .def("triggered_sends", &Engine::triggered_sends)
       .def_property("phase_timing", &Engine::phase_timing, &Engine::set_phase_timing)
       .def("graphs", &Engine::graphs)

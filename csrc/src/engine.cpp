@@ -928,7 +928,7 @@ void Engine::trial_medians(std::vector<AutoSpan>& spans, double out[2]) {
   uint32_t v[2];
   for (int k = 0; k < 2; ++k) {
     std::sort(ms[k].begin(), ms[k].end());
-    const double med = ms[k][ms[k].size() / 2];
+    const double med = ms[k].empty() ? 0.0 : ms[k][ms[k].size() / 2];
     v[k] = uint32_t(std::min(4.0e9, std::max(0.0, med * 1e4)));  // 0.1 us units
   }
   uint32_t* dev = alive_dev_ + 4;
@@ -948,8 +948,13 @@ void Engine::trial_medians(std::vector<AutoSpan>& spans, double out[2]) {
 // beside them), after two warm-up windows; each window is timed from its
 // poll's issue to the next's on the compute stream, and when kAutoTrials of
 // each are in, at the same poll on every rank, the medians are MAX-reduced
-// and every rank keeps the faster placement.  The reference all-reduces
-// every generation on the critical path (src/game_mpi_collective.c:70-109).
+// and every rank keeps the faster placement.  A side decision is then
+// checked on kAutoTrials consecutive side windows (after one warm-up) and
+// kept only if their median still beats the joined median: windows that
+// alternate with joined ones can time faster than a run of side windows (the
+// rehearsed rank tiles with the second linked stream on its own queue: side
+// chosen, then 2x slower).  The reference all-reduces every generation on
+// the critical path (src/game_mpi_collective.c:70-109).
 void Engine::poll_trial_step() {
   if (auto_overlap_) return;  // the overlap trial runs first
   if (ptrial_open_) {
@@ -963,16 +968,33 @@ void Engine::poll_trial_step() {
     }
     ptrial_open_ = nullptr;
   }
-  if (ptrial_counts_[0] >= kAutoTrials && ptrial_counts_[1] >= kAutoTrials) {
+  if (!ptrial_verify_ && ptrial_counts_[0] >= kAutoTrials && ptrial_counts_[1] >= kAutoTrials) {
     trial_medians(ptrial_spans_, poll_ms_);
-    poll_side_ = poll_ms_[1] < 0.98 * poll_ms_[0];
+    if (poll_ms_[1] < 0.98 * poll_ms_[0]) {  // side wins the alternation: check a run of side windows
+      ptrial_verify_ = true;
+      ptrial_counts_[0] = ptrial_counts_[1] = 0;
+      ptrial_polls_ = 0;
+    } else {
+      poll_side_ = false;
+      poll_trial_ = false;
+      poll_decided_ = true;
+      return;
+    }
+  } else if (ptrial_verify_ && ptrial_counts_[1] >= kAutoTrials) {
+    double v[2];
+    trial_medians(ptrial_spans_, v);
+    poll_side_steady_ms_ = v[1];
+    poll_side_ = v[1] < poll_ms_[0];
     poll_trial_ = false;
     poll_decided_ = true;
     return;
   }
   const int64_t i = ptrial_polls_++;
-  ptrial_mode_ = i < kAutoWarm ? -1 : int((i - kAutoWarm) % 2);
-  poll_side_ = ptrial_mode_ == 1;
+  if (ptrial_verify_)
+    ptrial_mode_ = i < 1 ? -1 : 1;
+  else
+    ptrial_mode_ = i < kAutoWarm ? -1 : int((i - kAutoWarm) % 2);
+  poll_side_ = ptrial_verify_ || ptrial_mode_ == 1;
   ptrial_open_ = be_->timing_mark(nullptr);
 }
 

@@ -240,7 +240,8 @@ class Simulation:
                 "overlap_trial_ms_trigger": self._eng.trial_ms_trigger,
                 "poll_mode": self._eng.poll_mode(),
                 "poll_trial_ms_per_window": {"joined": self._eng.poll_trial_ms_joined,
-                                             "side": self._eng.poll_trial_ms_side},
+                                             "side": self._eng.poll_trial_ms_side,
+                                             "side_steady": self._eng.poll_trial_ms_side_steady},
                 "triggered_sends": self._eng.triggered_sends(),
                 "u8_compute": ("bits" if self._eng.via_bits else "bytes") if self.config.resolved_layout() == "u8" else None,
                 "row_ring": bool(self._eng.row_ring), "row_ring_fallback": self._eng.row_ring_fallback or None,
