@@ -379,7 +379,8 @@ def main() -> int:
     Hg = a.height or S
     gps = max(1, a.gens_per_step)
     extra = (0 if a.no_phase_step else gps) + max(0, a.verify)
-    total = a.prewarm + (a.warmup + a.steps * a.repeats) * gps + extra
+    trial_cap = 16384  # prewarm generations allowed beyond --prewarm for the placement trials
+    total = a.prewarm + trial_cap + (a.warmup + a.steps * a.repeats) * gps + extra
     cfg = LifeConfig(S, Hg, gen_limit=total, layout=a.layout, decomp=a.decomp, tmax=a.tmax, epoch=a.epoch,
                      poll_gens=a.poll, overlap=a.overlap, graphs=a.graphs, timing_barriers=False,
                      self_exchange=bool(a.rehearse_rccl and world == 1), u8_compute=a.u8_compute,
@@ -400,8 +401,14 @@ def main() -> int:
         """One reference benchmark run: gps generations with termination checks."""
         return eng.run_until(sim.generation + gps)
 
+    trial_gens = 0
     if a.prewarm > 0:
         eng.run_until(sim.generation + a.prewarm)
+        # The overlap and poll-placement trials decide on the ranks over the first epochs and poll
+        # windows (the same generation on every rank); keep them out of the timed region.
+        while "trial" in eng.overlap_mode() + eng.poll_mode() and trial_gens < trial_cap:
+            eng.run_until(sim.generation + 1024)
+            trial_gens += 1024
     for _ in range(a.warmup):
         step()
     best = None
@@ -574,6 +581,7 @@ def main() -> int:
                 "generations_timed": gens,
                 "step_stop_reasons": stops,
                 "prewarm_generations": a.prewarm,
+                "prewarm_trial_generations": trial_gens,
                 "warmup_generations": a.warmup * gps,
                 "loop_ms_engine_per_step": sum(r.loop_ms for r in rs) / max(1, len(rs)),
                 "exchanges_per_step": rs[-1].exchanges if rs else 0,
