@@ -15,7 +15,6 @@
 //   * otherwise -> GEN_LIMIT.
 #pragma once
 
-#include <chrono>
 #include <memory>
 #include <string>
 #include <vector>
@@ -340,14 +339,12 @@ class Engine {
   int auto_counts_[2] = {0, 0};
   double auto_ms_[2] = {-1, -1};
   void trial_medians(std::vector<AutoSpan>& spans, double out[2]);
-  void reduce_medians(std::vector<double> ms[2], double out[2]);
   // Poll placement trial (tuning side_poll = -1, poll_trial_step).
   bool poll_trial_ = false, poll_decided_ = false;
   int64_t ptrial_polls_ = 0;
   int ptrial_mode_ = -1;            // placement of the open window: 0 joined, 1 side, -1 warm-up
-  bool ptrial_open_ = false;        // a poll-trial window is being timed (host clock)
-  std::chrono::steady_clock::time_point ptrial_t0_;
-  std::vector<double> ptrial_ms_[2];
+  void* ptrial_open_ = nullptr;
+  std::vector<AutoSpan> ptrial_spans_;
   int ptrial_counts_[2] = {0, 0};
   double poll_ms_[2] = {-1, -1};
   bool ptrial_verify_ = false;      // checking a side decision on consecutive side windows

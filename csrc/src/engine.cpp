@@ -224,10 +224,12 @@ void Engine::release_graphs() {
 
 Engine::~Engine() {
   release_graphs();
-  for (auto& sp : auto_spans_) {
-    be_->timing_release(sp.a);
-    be_->timing_release(sp.b);
-  }
+  for (auto* spans : {&auto_spans_, &ptrial_spans_})
+    for (auto& sp : *spans) {
+      be_->timing_release(sp.a);
+      be_->timing_release(sp.b);
+    }
+  if (ptrial_open_) be_->timing_release(ptrial_open_);
   if (auto_open_) be_->timing_release(auto_open_);
   for (auto& sp : phase_spans_) {
     be_->timing_release(sp.a);
@@ -838,7 +840,10 @@ RunResult Engine::run_impl(int64_t limit, bool stop_early) {
     be_->timing_release(auto_open_);
     auto_open_ = nullptr;
   }
-  ptrial_open_ = false;  // nor does a poll-trial window
+  if (ptrial_open_) {  // nor does a poll-trial window
+    be_->timing_release(ptrial_open_);
+    ptrial_open_ = nullptr;
+  }
   if (cfg_.timing_barriers) {
     settle_pending(false);
     tr_->barrier();
@@ -920,10 +925,6 @@ void Engine::trial_medians(std::vector<AutoSpan>& spans, double out[2]) {
     be_->timing_release(sp.b);
   }
   spans.clear();
-  reduce_medians(ms, out);
-}
-
-void Engine::reduce_medians(std::vector<double> ms[2], double out[2]) {
   uint32_t v[2];
   for (int k = 0; k < 2; ++k) {
     std::sort(ms[k].begin(), ms[k].end());
@@ -944,12 +945,8 @@ void Engine::reduce_medians(std::vector<double> ms[2], double out[2]) {
 // poll whose flag all-reduce joins the compute stream and one that runs on a
 // side stream through the transport's flags communicator (poll_side_, which
 // also leaves linked launches off for that window: transport work may run
-// beside them), after two warm-up windows; each window is timed on the host
-// clock from its poll's issue to the next's - the host waits for the previous
-// window's lagged poll in between, so that is the loop's throughput, the
-// time a side reduction costs the host included (device events on the compute
-// stream favoured side windows: 8 ranks sharing a GPU timed side 4-8 % faster
-// per window and ran 15-35 % slower) - and when kAutoTrials of
+// beside them), after two warm-up windows; each window is timed from its
+// poll's issue to the next's on the compute stream, and when kAutoTrials of
 // each are in, at the same poll on every rank, the medians are MAX-reduced
 // and every rank keeps the faster placement.  A side decision is then
 // checked on kAutoTrials consecutive side windows (after one warm-up) and
@@ -960,16 +957,19 @@ void Engine::reduce_medians(std::vector<double> ms[2], double out[2]) {
 // the critical path (src/game_mpi_collective.c:70-109).
 void Engine::poll_trial_step() {
   if (auto_overlap_) return;  // the overlap trial runs first
-  const auto now = std::chrono::steady_clock::now();
-  if (ptrial_open_ && ptrial_mode_ >= 0) {
-    ptrial_ms_[ptrial_mode_].push_back(std::chrono::duration<double, std::milli>(now - ptrial_t0_).count());
-    ++ptrial_counts_[ptrial_mode_];
+  if (ptrial_open_) {
+    void* end = be_->timing_mark(nullptr);
+    if (ptrial_mode_ >= 0) {
+      ptrial_spans_.push_back({ptrial_mode_, ptrial_open_, end});
+      ++ptrial_counts_[ptrial_mode_];
+    } else {
+      be_->timing_release(ptrial_open_);
+      be_->timing_release(end);
+    }
+    ptrial_open_ = nullptr;
   }
-  ptrial_open_ = false;
   if (!ptrial_verify_ && ptrial_counts_[0] >= kAutoTrials && ptrial_counts_[1] >= kAutoTrials) {
-    reduce_medians(ptrial_ms_, poll_ms_);
-    ptrial_ms_[0].clear();
-    ptrial_ms_[1].clear();
+    trial_medians(ptrial_spans_, poll_ms_);
     if (poll_ms_[1] < 0.98 * poll_ms_[0]) {  // side wins the alternation: check a run of side windows
       ptrial_verify_ = true;
       ptrial_counts_[0] = ptrial_counts_[1] = 0;
@@ -982,7 +982,7 @@ void Engine::poll_trial_step() {
     }
   } else if (ptrial_verify_ && ptrial_counts_[1] >= kAutoTrials) {
     double v[2];
-    reduce_medians(ptrial_ms_, v);
+    trial_medians(ptrial_spans_, v);
     poll_side_steady_ms_ = v[1];
     poll_side_ = v[1] < poll_ms_[0];
     poll_trial_ = false;
@@ -995,8 +995,7 @@ void Engine::poll_trial_step() {
   else
     ptrial_mode_ = i < kAutoWarm ? -1 : int((i - kAutoWarm) % 2);
   poll_side_ = ptrial_verify_ || ptrial_mode_ == 1;
-  ptrial_open_ = true;
-  ptrial_t0_ = std::chrono::steady_clock::now();
+  ptrial_open_ = be_->timing_mark(nullptr);
 }
 
 std::string Engine::poll_mode() const {
